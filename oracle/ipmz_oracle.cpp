@@ -1,0 +1,496 @@
+// ipmz_oracle -- CPU restatement of ipm-zoo's numerical interior-point Newton
+// step (albfre/ipm-zoo @ 2025-07-04, /root/reference).
+//
+// TEST INFRASTRUCTURE ONLY.  Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg load this library, and only as the checker or
+// the timed CPU baseline -- never as the product path.  The product
+// (ipm-zoo_amd/, libipmz.so) never links it and has no CPU fallback.
+//
+// Pinned by the golden vectors that tests/golden/make_golden.py generates
+// from the compiled reference (oracle/Makefile.ref + oracle/ref_harness.cpp):
+// LDL^T factor/solve and the SlackedSlacks Newton iterations compare BITWISE
+// (tests/test_oracle_golden.py).  The Regularization-equality formulation
+// (config C3) has no end-to-end reference (the reference asserts on its
+// scalar block, Evaluation.cpp:57-60): its KKT / factor / solve are pinned at
+// component level, its rhs and back-substitution formulas are the reference's
+// own symbolic output (tests/golden/formulations.txt).
+//
+// Build: g++ -O3 -ffp-contract=off -fPIC -shared (no -march=native: FMA
+// contraction changes the rounding).  Every expression below
+// keeps the reference evaluator's operand order (Evaluation.cpp:102-176):
+// Sum terms are added left to right, a - b is a + (-b) (bit-identical),
+// Product terms are multiplied left to right, X^{-1} is an element-wise
+// reciprocal with 0 -> sqrt(DBL_MAX) (Evaluation.cpp:267-271).
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+#include <vector>
+
+namespace {
+
+using Vec = std::vector<double>;
+
+// ---------------------------------------------------------------------------
+// Synthetic QP generator.  Identical bit-for-bit to the GPU
+// in-place generator ipm-zoo_amd/csrc/qpgen.h and to oracle/ref_harness.cpp.
+inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+inline double u01(uint64_t seed, uint64_t tag, uint64_t i, uint64_t j) {
+  const uint64_t key = seed ^ (tag << 56) ^ ((i << 32) + j);
+  return (double)(splitmix64(key) >> 11) * 0x1.0p-53;
+}
+enum : uint64_t { TAG_Q = 1, TAG_C = 2, TAG_A = 3, TAG_C_EQ = 4, TAG_D = 5 };
+
+// Evaluation.cpp:267-271
+inline double inv(double x) { return x == 0.0 ? std::sqrt(std::numeric_limits<double>::max()) : 1.0 / x; }
+
+// Canonical Newton-variable slots.  The reference's Newton variable order
+// (SymbolicOptimization get_newton_system; tests/golden/formulations.txt) is
+// this order with absent blocks dropped.
+enum Slot { X, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
+
+struct QP {
+  int64_t n, m, p;
+  double delta;  // EnvironmentBuilder.cpp:48
+  Vec Q, c, A, lA, uA, C, d, lx, ux;
+  Vec v[NSLOT];       // iterate
+  Vec daff[NSLOT], dir[NSLOT];
+  double mu;          // EnvironmentBuilder.cpp:49
+  int64_t size(int s) const {
+    switch (s) {
+      case X: case LY: case LZ: case Y: case Z: return n;
+      case LA: case S: case LG: case LH: case G: case H: return m;
+      default: return p;
+    }
+  }
+  int64_t N() const { return n + m + p; }
+};
+
+// ---------------------------------------------------------------------------
+// Matrix-vector products as the reference evaluates them
+// (Evaluation.cpp:18-21, 35-41; Transpose materialised at :126-140, so A^T v
+// is a row-dot over the transposed rows: sequential sum over the original
+// row index).
+void matvec(const Vec& M, int64_t rows, int64_t cols, const double* x, double* out) {
+  for (int64_t i = 0; i < rows; ++i) {
+    double s = 0.0;
+    const double* r = M.data() + i * cols;
+    for (int64_t j = 0; j < cols; ++j) s = s + r[j] * x[j];
+    out[i] = s;
+  }
+}
+void matvec_t(const Vec& M, int64_t rows, int64_t cols, const double* x, double* out) {
+  for (int64_t j = 0; j < cols; ++j) {
+    double s = 0.0;
+    for (int64_t i = 0; i < rows; ++i) s = s + M[i * cols + j] * x[i];
+    out[j] = s;
+  }
+}
+
+struct Residuals {
+  Vec r[NSLOT];
+};
+
+// Shorthand definitions r_v := -rhs_v (SymbolicOptimization.cpp:480-492),
+// formulas: tests/golden/formulations.txt "shorthand definitions".
+void residuals(const QP& q, double mu, Residuals& R) {
+  const int64_t n = q.n, m = q.m, p = q.p;
+  for (int s = 0; s < NSLOT; ++s) R.r[s].assign(q.size(s), 0.0);
+  const Vec* v = q.v;
+  Vec Qx(n), ATl(n), CTl(n), Ax(m), Cx(p);
+  matvec(q.Q, n, n, v[X].data(), Qx.data());
+  if (m) { matvec_t(q.A, m, n, v[LA].data(), ATl.data()); matvec(q.A, m, n, v[X].data(), Ax.data()); }
+  if (p) { matvec_t(q.C, p, n, v[LC].data(), CTl.data()); matvec(q.C, p, n, v[X].data(), Cx.data()); }
+  for (int64_t i = 0; i < n; ++i) {
+    // r_x := (c + lambda_z + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] - lambda_y)
+    double t = q.c[i] + v[LZ][i];
+    t = t + Qx[i];
+    if (m) t = t + ATl[i];
+    if (p) t = t + CTl[i];
+    R.r[X][i] = t + (-v[LY][i]);
+    R.r[LY][i] = (q.lx[i] + v[Y][i]) + (-v[X][i]);     // (l_x + y - x)
+    R.r[LZ][i] = (v[X][i] + v[Z][i]) + (-q.ux[i]);     // (x + z - u_x)
+    R.r[Y][i] = v[Y][i] * v[LY][i] + (-(mu * 1.0));    // ((Y*lambda_y) - (mu*e_x))
+    R.r[Z][i] = v[Z][i] * v[LZ][i] + (-(mu * 1.0));
+  }
+  for (int64_t i = 0; i < m; ++i) {
+    R.r[LA][i] = Ax[i] + (-v[S][i]);                               // ((A*x) - s)
+    R.r[S][i] = -((v[LA][i] + v[LG][i]) + (-v[LH][i]));           // -(lambda_A + lambda_g - lambda_h)
+    R.r[LG][i] = (q.lA[i] + v[G][i]) + (-v[S][i]);                 // (l_A + g - s)
+    R.r[LH][i] = (v[H][i] + v[S][i]) + (-q.uA[i]);                 // (h + s - u_A)
+    R.r[G][i] = v[G][i] * v[LG][i] + (-(mu * 1.0));
+    R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
+  }
+  for (int64_t i = 0; i < p; ++i) {
+    R.r[LC][i] = (Cx[i] + q.delta * v[P][i]) + (-q.d[i]);          // ((C*x) + (delta*p) - d)
+    R.r[P][i] = v[P][i] + q.delta * v[LC][i];                      // (p + (delta*lambda_C))
+  }
+}
+
+// Newton-variable order of the reference (absent blocks dropped).
+std::vector<int> order(const QP& q) {
+  std::vector<int> o;
+  for (int s = 0; s < NSLOT; ++s)
+    if (q.size(s) > 0) o.push_back(s);
+  return o;
+}
+
+// get_residual_norm_ (Optimizer.cpp:240-247): ||full rhs at mu=0||_2,
+// concatenated in Newton-variable order, inner_product from 0.0.
+double residual_norm(const QP& q) {
+  Residuals R;
+  residuals(q, 0.0, R);
+  double s = 0.0;
+  for (int slot : order(q))
+    for (double r : R.r[slot]) {
+      const double b = -r;
+      s = s + b * b;
+    }
+  return std::sqrt(s);
+}
+
+// get_mu_ (Optimizer.cpp:249-268): mean |complementarity| at mu=0 over the
+// rows containing e and mu, in Newton order (g, h, y, z).
+double mu_of(const QP& q) {
+  double s = 0.0;
+  int64_t cnt = 0;
+  const int comp[4] = {G, H, Y, Z};
+  const int dual[4] = {LG, LH, LY, LZ};
+  for (int k = 0; k < 4; ++k) {
+    const int64_t len = q.size(comp[k]);
+    for (int64_t i = 0; i < len; ++i) {
+      const double r = -(q.v[comp[k]][i] * q.v[dual[k]][i] + (-(0.0 * 1.0)));
+      s = s + std::abs(r);
+    }
+    cnt += len;
+  }
+  return cnt == 0 ? 0.0 : s / (double)cnt;
+}
+
+// Objective 0.5 x^T Q x + c^T x (Optimizer.cpp:45-48; Product evaluation with
+// the "unhandled" x^T, Evaluation.cpp:154-172).
+double objective(const QP& q) {
+  const int64_t n = q.n;
+  Vec Qx(n);
+  matvec(q.Q, n, n, q.v[X].data(), Qx.data());
+  double a = 0.0, b = 0.0;
+  for (int64_t i = 0; i < n; ++i) a = a + (0.5 * q.v[X][i]) * Qx[i];
+  for (int64_t i = 0; i < n; ++i) b = b + q.c[i] * q.v[X][i];
+  return a + b;
+}
+
+// Diagonal of the (lambda_A, lambda_A) block before negation:
+// ((G^{-1}*Lambda_g) + (H^{-1}*Lambda_h))^{-1}.
+inline double ds_inv(const QP& q, int64_t i) {
+  return inv(inv(q.v[G][i]) * q.v[LG][i] + inv(q.v[H][i]) * q.v[LH][i]);
+}
+
+// Augmented KKT (get_as_matrix_, Optimizer.cpp:387-391 / 441-501), dense
+// row-major N x N, both triangles.
+void assemble(const QP& q, double* K) {
+  const int64_t n = q.n, m = q.m, p = q.p, N = q.N();
+  std::memset(K, 0, sizeof(double) * (size_t)(N * N));
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t j = 0; j < n; ++j) K[i * N + j] = q.Q[i * n + j];
+    // (Q + (Y^{-1}*Lambda_y) + (Z^{-1}*Lambda_z)): elementwise_diag_mat_op
+    double h = q.Q[i * n + i] + inv(q.v[Y][i]) * q.v[LY][i];
+    K[i * N + i] = h + inv(q.v[Z][i]) * q.v[LZ][i];
+  }
+  for (int64_t r = 0; r < m; ++r) {
+    for (int64_t j = 0; j < n; ++j) {
+      K[(n + r) * N + j] = q.A[r * n + j];
+      K[j * N + n + r] = q.A[r * n + j];
+    }
+    K[(n + r) * N + n + r] = -ds_inv(q, r);
+  }
+  for (int64_t r = 0; r < p; ++r) {
+    for (int64_t j = 0; j < n; ++j) {
+      K[(n + m + r) * N + j] = q.C[r * n + j];
+      K[j * N + n + m + r] = q.C[r * n + j];
+    }
+    K[(n + m + r) * N + n + m + r] = -(q.delta * q.delta);
+  }
+}
+
+// Augmented rhs (tests/golden/formulations.txt "augmented system rhs").
+void augmented_rhs(const QP& q, const Residuals& R, double* b) {
+  const int64_t n = q.n, m = q.m, p = q.p;
+  const Vec* v = q.v;
+  for (int64_t i = 0; i < n; ++i) {
+    const double tz = inv(v[Z][i]) * (R.r[Z][i] + (-(v[LZ][i] * R.r[LZ][i])));
+    const double ty = inv(v[Y][i]) * (R.r[Y][i] + (-(v[LY][i] * R.r[LY][i])));
+    b[i] = (tz + (-R.r[X][i])) + (-ty);
+  }
+  for (int64_t i = 0; i < m; ++i) {
+    const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
+    const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
+    b[n + i] = ds_inv(q, i) * ((th + (-R.r[S][i])) + (-tg)) + (-R.r[LA][i]);
+  }
+  for (int64_t i = 0; i < p; ++i) b[n + m + i] = q.delta * R.r[P][i] + (-R.r[LC][i]);
+}
+
+// Eliminated-variable back-substitution (delta_definitions evaluated in
+// reverse order, Optimizer.cpp:373-378).
+void back_substitute(const QP& q, const Residuals& R, Vec* D) {
+  const int64_t n = q.n, m = q.m, p = q.p;
+  const Vec* v = q.v;
+  for (int64_t i = 0; i < m; ++i) {
+    const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
+    const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
+    const double ds = ds_inv(q, i) * ((((D[LA][i] + th) + (-R.r[S][i])) + (-tg)));
+    D[S][i] = ds;
+    D[LG][i] = -((inv(v[G][i]) * v[LG][i]) * ((ds + inv(v[LG][i]) * R.r[G][i]) + (-R.r[LG][i])));
+    D[LH][i] = -((inv(v[H][i]) * v[LH][i]) * ((inv(v[LH][i]) * R.r[H][i] + (-R.r[LH][i])) + (-ds)));
+    D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));
+    D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
+  }
+  for (int64_t i = 0; i < p; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
+  for (int64_t i = 0; i < n; ++i) {
+    const double dx = D[X][i];
+    D[LY][i] = -((inv(v[Y][i]) * v[LY][i]) * ((dx + inv(v[LY][i]) * R.r[Y][i]) + (-R.r[LY][i])));
+    D[LZ][i] = -((inv(v[Z][i]) * v[LZ][i]) * ((inv(v[LZ][i]) * R.r[Z][i] + (-R.r[LZ][i])) + (-dx)));
+    D[Y][i] = -(inv(v[LY][i]) * (R.r[Y][i] + v[Y][i] * D[LY][i]));
+    D[Z][i] = -(inv(v[LZ][i]) * (R.r[Z][i] + v[Z][i] * D[LZ][i]));
+  }
+}
+
+// ---------------------------------------------------------------------------
+// LinearSolvers restatement (LinearSolvers.cpp:14-74), same loop and product
+// order; L is a full N x N row-major matrix (zeros above, ones on diagonal).
+void ldlt(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, double* D) {
+  for (int64_t i = 0; i < n; ++i)
+    for (int64_t j = 0; j < n; ++j) L[i * ldl + j] = 0.0;
+  for (int64_t i = 0; i < n; ++i) {
+    double sum_d = A[i * lda + i];
+    const double* Li = L + i * ldl;
+    for (int64_t j = 0; j < i; ++j) sum_d -= Li[j] * Li[j] * D[j];
+    D[i] = sum_d == 0.0 ? 1e-8 : sum_d;  // Vanderbei zero-pivot rule, :26-28
+    for (int64_t j = i + 1; j < n; ++j) {
+      double sum = A[j * lda + i];
+      const double* Lj = L + j * ldl;
+      for (int64_t k = 0; k < i; ++k) sum -= Lj[k] * Li[k] * D[k];
+      L[j * ldl + i] = sum / D[i];
+    }
+    L[i * ldl + i] = 1.0;
+  }
+}
+
+void solve_ldlt(int64_t n, const double* L, int64_t ldl, const double* D, double* b) {
+  if (n == 0) return;
+  for (int64_t i = 0; i < n; ++i) {  // std::inner_product from 0.0
+    double s = 0.0;
+    for (int64_t j = 0; j < i; ++j) s = s + L[i * ldl + j] * b[j];
+    b[i] -= s;
+  }
+  for (int64_t i = 0; i < n; ++i) b[i] /= D[i];
+  for (int64_t i = n - 1; i >= 0; --i) {
+    double s = 0.0;
+    for (int64_t j = i + 1; j < n; ++j) s += L[j * ldl + i] * b[j];
+    b[i] -= s;
+  }
+}
+
+// get_max_step_ (Optimizer.cpp:270-342).
+double max_step(const QP& q, const Vec* D) {
+  double a = 1.0;
+  const int nonneg[8] = {LG, LH, LY, LZ, G, H, Y, Z};
+  for (int slot : order(q)) {
+    bool nn = false;
+    for (int k = 0; k < 8; ++k) nn |= slot == nonneg[k];
+    if (!nn) continue;
+    for (int64_t j = 0; j < q.size(slot); ++j) {
+      const double dij = D[slot][j], vij = q.v[slot][j];
+      if (dij < 0.0) a = std::min(a, -vij / dij);
+    }
+  }
+  if (q.m == 0) {  // neither g nor h is a Newton variable: explicit x bounds
+    for (int64_t j = 0; j < q.n; ++j) {
+      const double dij = D[X][j], vij = q.v[X][j];
+      if (dij < 0.0) a = std::min(a, (q.lx[j] - vij) / dij);
+      if (dij > 0.0) a = std::min(a, (q.ux[j] - vij) / dij);
+    }
+  }
+  return a;
+}
+
+void axpy_all(QP& q, double s, const Vec* D) {
+  for (int slot = 0; slot < NSLOT; ++slot)
+    for (int64_t j = 0; j < q.size(slot); ++j) q.v[slot][j] = q.v[slot][j] + s * D[slot][j];
+}
+
+// One Newton iteration (Optimizer.cpp:127-219).  rec = {f, res, mu,
+// alpha_aff, mu_aff, sigma, alpha, converged}.
+struct Workspace {
+  Vec K, L, Dd, b;
+};
+
+void search_direction(QP& q, const Residuals& R, const Vec& L, const Vec& Dd, Vec* out) {
+  const int64_t N = q.N(), n = q.n, m = q.m;
+  Vec b(N);
+  augmented_rhs(q, R, b.data());
+  solve_ldlt(N, L.data(), N, Dd.data(), b.data());
+  for (int s = 0; s < NSLOT; ++s) out[s].assign(q.size(s), 0.0);
+  std::memcpy(out[X].data(), b.data(), sizeof(double) * n);
+  std::memcpy(out[LA].data(), b.data() + n, sizeof(double) * m);
+  std::memcpy(out[LC].data(), b.data() + n + m, sizeof(double) * q.p);
+  back_substitute(q, R, out);
+}
+
+int iterate(QP& q, double* rec, double* phase_s) {
+  using clk = double;
+  (void)sizeof(clk);
+  const int64_t N = q.N();
+  rec[0] = objective(q);
+  rec[1] = residual_norm(q);
+  rec[2] = mu_of(q);
+  rec[7] = (rec[1] < 1e-8 && rec[2] < 1e-8) ? 1.0 : 0.0;
+  if (rec[7] != 0.0) return 1;
+  Vec K((size_t)(N * N)), L((size_t)(N * N)), Dd(N);
+  assemble(q, K.data());
+  ldlt(N, K.data(), N, L.data(), N, Dd.data());
+  (void)phase_s;
+  const double mu = rec[2];
+  Residuals R;
+  residuals(q, 0.0, R);
+  search_direction(q, R, L, Dd, q.daff);
+  const double a_aff = max_step(q, q.daff);
+  Vec saved[NSLOT];
+  for (int s = 0; s < NSLOT; ++s) saved[s] = q.v[s];
+  axpy_all(q, a_aff, q.daff);
+  const double mu_aff = mu_of(q);
+  for (int s = 0; s < NSLOT; ++s) q.v[s] = saved[s];
+  const double sigma = mu > 0.0 ? std::pow(mu_aff / mu, 3) : 0.0;
+  const double mu_new = mu * sigma;
+  residuals(q, mu_new, R);
+  // Corrector (Optimizer.cpp:183-209): r_v += (dV_aff * dlambda_aff) - (0*e)
+  const int comp[4] = {G, H, Y, Z};
+  const int dual[4] = {LG, LH, LY, LZ};
+  for (int k = 0; k < 4; ++k)
+    for (int64_t i = 0; i < q.size(comp[k]); ++i)
+      R.r[comp[k]][i] = R.r[comp[k]][i] + (q.daff[comp[k]][i] * q.daff[dual[k]][i] + (-(0.0 * 1.0)));
+  search_direction(q, R, L, Dd, q.dir);
+  const double alpha = max_step(q, q.dir);
+  axpy_all(q, 0.995 * alpha, q.dir);
+  rec[3] = a_aff;
+  rec[4] = mu_aff;
+  rec[5] = sigma;
+  rec[6] = alpha;
+  q.mu = mu_new;
+  return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI for ctypes (tests, smoke, bench cpu_baseline)
+extern "C" {
+
+void ipmzo_gen_qp(int64_t n, int64_t m, int64_t p, uint64_t seed, double* Q, double* c, double* A, double* lA,
+                  double* uA, double* C, double* d, double* lx, double* ux) {
+  for (int64_t i = 0; i < n; ++i) {
+    for (int64_t j = 0; j < i; ++j) {
+      const double v = (2.0 * u01(seed, TAG_Q, i, j) - 1.0) / (double)n;
+      Q[i * n + j] = v;
+      Q[j * n + i] = v;
+    }
+    Q[i * n + i] = 1.0 + u01(seed, TAG_Q, i, i);
+    c[i] = 2.0 * u01(seed, TAG_C, i, 0) - 1.0;
+    lx[i] = -1.0;
+    ux[i] = 1.0;
+  }
+  const double sn = std::sqrt((double)n);
+  for (int64_t i = 0; i < m; ++i) {
+    for (int64_t j = 0; j < n; ++j) A[i * n + j] = (2.0 * u01(seed, TAG_A, i, j) - 1.0) / sn;
+    lA[i] = -1.0;
+    uA[i] = 1.0;
+  }
+  for (int64_t i = 0; i < p; ++i) {
+    for (int64_t j = 0; j < n; ++j) C[i * n + j] = (2.0 * u01(seed, TAG_C_EQ, i, j) - 1.0) / sn;
+    d[i] = (2.0 * u01(seed, TAG_D, i, 0) - 1.0) * 0.1;
+  }
+}
+
+double ipmzo_u01(uint64_t seed, uint64_t tag, uint64_t i, uint64_t j) { return u01(seed, tag, i, j); }
+
+void ipmzo_ldlt(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, double* D) {
+  ldlt(n, A, lda, L, ldl, D);
+}
+void ipmzo_solve_ldlt(int64_t n, const double* L, int64_t ldl, const double* D, double* b) {
+  solve_ldlt(n, L, ldl, D, b);
+}
+
+void* ipmzo_create(int64_t n, int64_t m, int64_t p, const double* Q, const double* c, const double* A,
+                   const double* lA, const double* uA, const double* C, const double* d, const double* lx,
+                   const double* ux) {
+  auto* q = new QP();
+  q->n = n;
+  q->m = m;
+  q->p = p;
+  q->delta = 1e-4;
+  q->mu = 1.0;
+  q->Q.assign(Q, Q + n * n);
+  q->c.assign(c, c + n);
+  q->A.assign(A, A + m * n);
+  q->lA.assign(lA, lA + m);
+  q->uA.assign(uA, uA + m);
+  q->C.assign(C, C + p * n);
+  q->d.assign(d, d + p);
+  q->lx.assign(lx, lx + n);
+  q->ux.assign(ux, ux + n);
+  // build_environment initial iterate (EnvironmentBuilder.cpp:34-73)
+  for (int s = 0; s < NSLOT; ++s) {
+    q->v[s].assign(q->size(s), 1.0);
+    q->daff[s].assign(q->size(s), 0.0);
+    q->dir[s].assign(q->size(s), 0.0);
+  }
+  for (int64_t i = 0; i < n; ++i) q->v[X][i] = 0.5 * (lx[i] + ux[i]);
+  for (int64_t i = 0; i < m; ++i) q->v[S][i] = 0.5 * (lA[i] + uA[i]);
+  return q;
+}
+
+void ipmzo_destroy(void* h) { delete static_cast<QP*>(h); }
+
+int64_t ipmzo_kkt_dim(void* h) { return static_cast<QP*>(h)->N(); }
+
+int ipmzo_iterate(void* h, double* rec) { return iterate(*static_cast<QP*>(h), rec, nullptr); }
+
+// Concatenated vectors in the reference's Newton-variable order.
+int64_t ipmzo_state_len(void* h) {
+  const QP& q = *static_cast<QP*>(h);
+  int64_t t = 0;
+  for (int s : order(q)) t += q.size(s);
+  return t;
+}
+static void pack(const QP& q, const Vec* src, double* out) {
+  for (int s : order(q)) {
+    std::memcpy(out, src[s].data(), sizeof(double) * q.size(s));
+    out += q.size(s);
+  }
+}
+void ipmzo_get_vars(void* h, double* out) { const QP& q = *static_cast<QP*>(h); pack(q, q.v, out); }
+void ipmzo_get_daff(void* h, double* out) { const QP& q = *static_cast<QP*>(h); pack(q, q.daff, out); }
+void ipmzo_get_dir(void* h, double* out) { const QP& q = *static_cast<QP*>(h); pack(q, q.dir, out); }
+void ipmzo_set_vars(void* h, const double* in) {
+  QP& q = *static_cast<QP*>(h);
+  for (int s : order(q)) {
+    std::memcpy(q.v[s].data(), in, sizeof(double) * q.size(s));
+    in += q.size(s);
+  }
+}
+void ipmzo_assemble(void* h, double* K) { assemble(*static_cast<QP*>(h), K); }
+void ipmzo_rhs(void* h, double mu, double* b) {
+  QP& q = *static_cast<QP*>(h);
+  Residuals R;
+  residuals(q, mu, R);
+  augmented_rhs(q, R, b);
+}
+double ipmzo_residual_norm(void* h) { return residual_norm(*static_cast<QP*>(h)); }
+double ipmzo_mu(void* h) { return mu_of(*static_cast<QP*>(h)); }
+double ipmzo_objective(void* h) { return objective(*static_cast<QP*>(h)); }
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+"""ctypes wrapper of the CPU oracle (oracle/libipmz_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, as the checker or the timed CPU baseline.  The
+product package (ipm-zoo_amd/ipmz_amd) never imports it.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libipmz_oracle.so")
+
+_P = ctypes.POINTER(ctypes.c_double)
+_i64 = ctypes.c_int64
+_u64 = ctypes.c_uint64
+
+# Canonical slots (ipmz_oracle.cpp enum Slot / include/ipmz.h IPMZ_SLOT_*)
+SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_y", "lambda_z",
+         "g", "h", "y", "z"]
+NONNEG = {"lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"}
+
+
+def slot_size(name, n, m, p):
+    if name in ("x", "lambda_y", "lambda_z", "y", "z"):
+        return n
+    if name in ("lambda_A", "s", "lambda_g", "lambda_h", "g", "h"):
+        return m
+    return p
+
+
+def newton_order(n, m, p):
+    """Reference Newton-variable order with absent blocks dropped."""
+    return [s for s in SLOTS if slot_size(s, n, m, p) > 0]
+
+
+def _dp(a):
+    return a.ctypes.data_as(_P)
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"oracle library missing: {LIB_PATH} (run __graft_entry__.build())")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.ipmzo_create.restype = ctypes.c_void_p
+    lib.ipmzo_create.argtypes = [_i64, _i64, _i64] + [_P] * 9
+    lib.ipmzo_destroy.argtypes = [ctypes.c_void_p]
+    lib.ipmzo_iterate.argtypes = [ctypes.c_void_p, _P]
+    lib.ipmzo_iterate.restype = ctypes.c_int
+    for fn in ("ipmzo_state_len", "ipmzo_kkt_dim"):
+        getattr(lib, fn).restype = _i64
+        getattr(lib, fn).argtypes = [ctypes.c_void_p]
+    for fn in ("ipmzo_get_vars", "ipmzo_get_daff", "ipmzo_get_dir", "ipmzo_set_vars", "ipmzo_assemble"):
+        getattr(lib, fn).argtypes = [ctypes.c_void_p, _P]
+    lib.ipmzo_rhs.argtypes = [ctypes.c_void_p, ctypes.c_double, _P]
+    for fn in ("ipmzo_residual_norm", "ipmzo_mu", "ipmzo_objective"):
+        getattr(lib, fn).restype = ctypes.c_double
+        getattr(lib, fn).argtypes = [ctypes.c_void_p]
+    lib.ipmzo_gen_qp.argtypes = [_i64, _i64, _i64, _u64] + [_P] * 9
+    lib.ipmzo_ldlt.argtypes = [_i64, _P, _i64, _P, _i64, _P]
+    lib.ipmzo_solve_ldlt.argtypes = [_i64, _P, _i64, _P, _P]
+    lib.ipmzo_u01.restype = ctypes.c_double
+    lib.ipmzo_u01.argtypes = [_u64, _u64, _u64, _u64]
+    return lib
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def gen_qp(n, m, p, seed):
+    """Synthetic dense QP of SURVEY.md §8d (counter-based splitmix64)."""
+    Q = np.zeros(n * n)
+    c = np.zeros(n)
+    A = np.zeros(max(m * n, 1))
+    lA = np.zeros(max(m, 1))
+    uA = np.zeros(max(m, 1))
+    C = np.zeros(max(p * n, 1))
+    d = np.zeros(max(p, 1))
+    lx = np.zeros(n)
+    ux = np.zeros(n)
+    lib().ipmzo_gen_qp(n, m, p, seed, _dp(Q), _dp(c), _dp(A), _dp(lA), _dp(uA), _dp(C), _dp(d), _dp(lx), _dp(ux))
+    return dict(n=n, m=m, p=p, Q=Q.reshape(n, n), c=c, A=A[: m * n].reshape(m, n), lA=lA[:m], uA=uA[:m],
+                C=C[: p * n].reshape(p, n), d=d[:p], lx=lx, ux=ux)
+
+
+def ldlt(K):
+    """Restatement of LinearSolvers::ldlt_decomposition (full L, D)."""
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    N = K.shape[0]
+    L = np.zeros((N, N))
+    D = np.zeros(N)
+    lib().ipmzo_ldlt(N, _dp(K), N, _dp(L), N, _dp(D))
+    return L, D
+
+
+def solve_ldlt(L, D, b):
+    """Restatement of LinearSolvers::overwriting_solve_ldlt (returns x)."""
+    L = np.ascontiguousarray(L, dtype=np.float64)
+    x = np.array(b, dtype=np.float64, copy=True)
+    lib().ipmzo_solve_ldlt(len(x), _dp(L), L.shape[1], _dp(np.ascontiguousarray(D, dtype=np.float64)), _dp(x))
+    return x
+
+
+class OracleQP:
+    """CPU restatement of Optimizer (SlackedSlacks inequalities, Regularization
+    equalities) from build_environment's initial iterate."""
+
+    def __init__(self, qp):
+        self.qp = qp
+        n, m, p = qp["n"], qp["m"], qp["p"]
+        self._keep = [np.ascontiguousarray(qp[k], dtype=np.float64).reshape(-1) if np.size(qp[k]) else np.zeros(1)
+                      for k in ("Q", "c", "A", "lA", "uA", "C", "d", "lx", "ux")]
+        self.h = ctypes.c_void_p(lib().ipmzo_create(n, m, p, *[_dp(a) for a in self._keep]))
+        self.N = lib().ipmzo_kkt_dim(self.h)
+        self.L = lib().ipmzo_state_len(self.h)
+        self.order = newton_order(n, m, p)
+
+    def __del__(self):
+        if getattr(self, "h", None) and _lib is not None:
+            _lib.ipmzo_destroy(self.h)
+
+    def iterate(self):
+        rec = np.zeros(8)
+        conv = lib().ipmzo_iterate(self.h, _dp(rec))
+        keys = ("f", "res", "mu", "alpha_aff", "mu_aff", "sigma", "alpha", "converged")
+        return conv, dict(zip(keys, rec))
+
+    def _get(self, fn):
+        out = np.zeros(self.L)
+        getattr(lib(), fn)(self.h, _dp(out))
+        return out
+
+    def vars(self):
+        return self._get("ipmzo_get_vars")
+
+    def daff(self):
+        return self._get("ipmzo_get_daff")
+
+    def dir(self):
+        return self._get("ipmzo_get_dir")
+
+    def set_vars(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        lib().ipmzo_set_vars(self.h, _dp(v))
+
+    def kkt(self):
+        K = np.zeros(self.N * self.N)
+        lib().ipmzo_assemble(self.h, _dp(K))
+        return K.reshape(self.N, self.N)
+
+    def rhs(self, mu=0.0):
+        b = np.zeros(self.N)
+        lib().ipmzo_rhs(self.h, mu, _dp(b))
+        return b
+
+    def residual_norm(self):
+        return lib().ipmzo_residual_norm(self.h)
+
+    def mu(self):
+        return lib().ipmzo_mu(self.h)
+
+    def objective(self):
+        return lib().ipmzo_objective(self.h)
+
+    def split(self, flat):
+        """Split a concatenated state vector into {slot: array}."""
+        n, m, p = self.qp["n"], self.qp["m"], self.qp["p"]
+        out, off = {}, 0
+        for s in self.order:
+            k = slot_size(s, n, m, p)
+            out[s] = flat[off:off + k]
+            off += k
+        return out

@@ -1,0 +1,444 @@
+// Golden-vector harness for the upstream reference (albfre/ipm-zoo).
+//
+// TEST INFRASTRUCTURE ONLY.  Linked against the reference objects built by
+// oracle/Makefile.ref into oracle/_ref/; it never ships in the product
+// library and nothing on the GPU box runs it (the reference does not travel).
+// Its outputs are the small fixtures committed under tests/golden/ by
+// tests/golden/make_golden.py.
+//
+// Modes (all write to the directory given as argv[2]):
+//   formulation <dir>               formulation strings per Settings
+//   ldlt <dir> <N> <seed> <tag>     LinearSolvers::ldlt_decomposition +
+//                                   overwriting_solve_ldlt on a generated
+//                                   quasi-definite K (LinearSolvers.cpp:14-74)
+//   bk <dir> <N> <seed> <tag>       symmetric_indefinite_factorization +
+//                                   overwriting_solve_bunch_kaufman
+//                                   (LinearSolvers.cpp:76-318)
+//   newton <dir> <n> <m> <seed> <iters> <tag>
+//                                   SlackedSlacks (box [+ ineq]) Newton
+//                                   iterations through the reference's own
+//                                   Optimizer private methods
+//                                   (Optimizer.cpp:127-219)
+//   component_eq <dir> <n> <m> <p> <seed> <tag>
+//                                   C3 structure (Regularization equalities):
+//                                   reference Evaluation for every non-scalar
+//                                   block, scalar/zero blocks expanded here
+//                                   to s*I / 0, reference ldlt + solve.
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <fstream>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "Expr.h"
+#include "ExprFactory.h"
+#include "NumericalOptimization/EnvironmentBuilder.h"
+#include "NumericalOptimization/Evaluation.h"
+#include "NumericalOptimization/LinearSolvers.h"
+#include "SymbolicOptimization.h"
+#include "Utils/Helpers.h"
+#define private public
+#include "NumericalOptimization/Optimizer.h"
+#undef private
+
+using Mat = std::vector<std::vector<double>>;
+using Vec = std::vector<double>;
+namespace SO = SymbolicOptimization;
+namespace NO = NumericalOptimization;
+
+// ---------------------------------------------------------------------------
+// Counter-based generator -- identical to
+// ipm-zoo_amd/csrc/qpgen.h and oracle/ipmz_oracle.cpp.
+static inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+static inline double u01(uint64_t seed, uint64_t tag, uint64_t i, uint64_t j) {
+  const uint64_t key = seed ^ (tag << 56) ^ ((i << 32) + j);
+  return (double)(splitmix64(key) >> 11) * 0x1.0p-53;
+}
+enum : uint64_t { TAG_Q = 1, TAG_C = 2, TAG_A = 3, TAG_C_EQ = 4, TAG_D = 5, TAG_K = 6, TAG_B = 7 };
+
+struct QP {
+  size_t n, m, p;
+  Mat Q, A, C;
+  Vec c, lA, uA, d, lx, ux;
+};
+
+static QP make_qp(size_t n, size_t m, size_t p, uint64_t seed) {
+  QP q{n, m, p};
+  q.Q.assign(n, Vec(n));
+  for (size_t i = 0; i < n; ++i) {
+    for (size_t j = 0; j < i; ++j) {
+      const double v = (2.0 * u01(seed, TAG_Q, i, j) - 1.0) / (double)n;
+      q.Q[i][j] = v;
+      q.Q[j][i] = v;
+    }
+    q.Q[i][i] = 1.0 + u01(seed, TAG_Q, i, i);
+  }
+  q.c.resize(n);
+  for (size_t i = 0; i < n; ++i) q.c[i] = 2.0 * u01(seed, TAG_C, i, 0) - 1.0;
+  const double sn = std::sqrt((double)n);
+  q.A.assign(m, Vec(n));
+  for (size_t i = 0; i < m; ++i)
+    for (size_t j = 0; j < n; ++j) q.A[i][j] = (2.0 * u01(seed, TAG_A, i, j) - 1.0) / sn;
+  q.C.assign(p, Vec(n));
+  for (size_t i = 0; i < p; ++i)
+    for (size_t j = 0; j < n; ++j) q.C[i][j] = (2.0 * u01(seed, TAG_C_EQ, i, j) - 1.0) / sn;
+  q.lA.assign(m, -1.0);
+  q.uA.assign(m, 1.0);
+  q.d.resize(p);
+  for (size_t i = 0; i < p; ++i) q.d[i] = (2.0 * u01(seed, TAG_D, i, 0) - 1.0) * 0.1;
+  q.lx.assign(n, -1.0);
+  q.ux.assign(n, 1.0);
+  return q;
+}
+
+// ---------------------------------------------------------------------------
+static void write_bin(const std::string& path, const Vec& v) {
+  std::ofstream f(path, std::ios::binary);
+  f.write(reinterpret_cast<const char*>(v.data()), (std::streamsize)(v.size() * sizeof(double)));
+}
+static Vec flatten(const Mat& M) {
+  Vec out;
+  for (const auto& r : M) out.insert(out.end(), r.begin(), r.end());
+  return out;
+}
+static Vec lower_packed(const Mat& M) {  // row-major packed lower triangle
+  Vec out;
+  for (size_t i = 0; i < M.size(); ++i)
+    for (size_t j = 0; j <= i; ++j) out.push_back(M[i][j]);
+  return out;
+}
+
+struct Silence {  // the reference prints O(N^2) per iteration
+  std::streambuf* old;
+  std::ostringstream sink;
+  Silence() : old(std::cout.rdbuf()) { std::cout.rdbuf(sink.rdbuf()); }
+  ~Silence() { std::cout.rdbuf(old); }
+};
+
+static std::string to_s(const Expression::ExprPtr& e) { return e ? e->to_string() : std::string("<null>"); }
+
+// ---------------------------------------------------------------------------
+static SO::Settings settings_from(const std::string& ineq, const std::string& eq, bool has_ineq) {
+  SO::Settings s;
+  s.inequalities = has_ineq ? SO::Bounds::Both : SO::Bounds::None;
+  s.variable_bounds = SO::Bounds::Both;
+  if (ineq == "Slacks") s.inequality_handling = SO::InequalityHandling::Slacks;
+  else if (ineq == "NaiveSlacks") s.inequality_handling = SO::InequalityHandling::NaiveSlacks;
+  else s.inequality_handling = SO::InequalityHandling::SlackedSlacks;
+  s.equalities = eq != "none";
+  if (eq == "None") s.equality_handling = SO::EqualityHandling::None;
+  else if (eq == "Regularization") s.equality_handling = SO::EqualityHandling::Regularization;
+  else if (eq == "PenaltyFunction") s.equality_handling = SO::EqualityHandling::PenaltyFunction;
+  else if (eq == "SlackedSlacks") s.equality_handling = SO::EqualityHandling::SlackedSlacks;
+  else if (eq == "Slacks") s.equality_handling = SO::EqualityHandling::Slacks;
+  return s;
+}
+
+static void dump_system(std::ostream& os, const SO::NewtonSystem& ns) {
+  os << "  variables:";
+  for (auto& v : ns.variables) os << " [" << to_s(v) << "]";
+  os << "\n  lhs:\n";
+  for (auto& row : ns.lhs) {
+    os << "   ";
+    for (auto& e : row) os << " | " << to_s(e);
+    os << "\n";
+  }
+  os << "  rhs:\n";
+  for (auto& e : ns.rhs) os << "    " << to_s(e) << "\n";
+  os << "  delta_definitions:\n";
+  for (auto& [v, d] : ns.delta_definitions) os << "    " << to_s(v) << " := " << to_s(d) << "\n";
+}
+
+static int mode_formulation(const std::string& dir) {
+  std::ofstream os(dir + "/formulations.txt");
+  const SO::VariableNames names;
+  struct Case { const char* ineq; const char* eq; bool has_ineq; };
+  const Case cases[] = {
+      {"SlackedSlacks", "none", false}, {"SlackedSlacks", "none", true},
+      {"SlackedSlacks", "Regularization", true}, {"Slacks", "none", true},
+      {"SlackedSlacks", "None", true}, {"SlackedSlacks", "PenaltyFunction", true},
+  };
+  for (const auto& c : cases) {
+    const auto s = settings_from(c.ineq, c.eq, c.has_ineq);
+    os << "=== inequality_handling=" << c.ineq << " equalities=" << c.eq
+       << " inequalities=" << (c.has_ineq ? "Both" : "None") << "\n";
+    const auto ns = SO::get_newton_system(s, names);
+    os << "-- newton system\n";
+    dump_system(os, ns);
+    const auto sh = SO::get_shorthand_rhs(ns);
+    os << "-- shorthand definitions\n";
+    for (auto& [v, d] : sh.vector_definitions) os << "    " << to_s(v) << " := " << to_s(d) << "\n";
+    auto ns2 = ns;
+    ns2.rhs = sh.shorthand_rhs;
+    const auto aug = SO::get_augmented_system(ns2);
+    os << "-- augmented system\n";
+    dump_system(os, aug);
+    const auto ne = SO::get_normal_equations(aug);
+    os << "-- normal equations\n";
+    dump_system(os, ne);
+  }
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Seeded quasi-definite K = [H B^T; B -G] with H SPD and G positive diagonal.
+static Mat make_qd(size_t N, uint64_t seed) {
+  const size_t n1 = (N * 3 + 3) / 4;  // leading SPD block
+  Mat K(N, Vec(N, 0.0));
+  for (size_t i = 0; i < N; ++i) {
+    for (size_t j = 0; j < i; ++j) {
+      double v;
+      if (i < n1) v = (2.0 * u01(seed, TAG_K, i, j) - 1.0) / (double)n1;
+      else if (j < n1) v = (2.0 * u01(seed, TAG_K, i, j) - 1.0) / std::sqrt((double)n1);
+      else v = 0.0;
+      K[i][j] = v;
+      K[j][i] = v;
+    }
+    K[i][i] = i < n1 ? 1.0 + u01(seed, TAG_K, i, i) : -(0.5 + u01(seed, TAG_K, i, i));
+  }
+  return K;
+}
+
+static int mode_ldlt(const std::string& dir, size_t N, uint64_t seed, const std::string& tag) {
+  const Mat K = make_qd(N, seed);
+  Vec b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = 2.0 * u01(seed, TAG_B, i, 0) - 1.0;
+  auto [L, D] = NO::LinearSolvers::ldlt_decomposition(K);
+  Vec x = b;
+  NO::LinearSolvers::overwriting_solve_ldlt(L, D, x);
+  write_bin(dir + "/" + tag + "_K.bin", lower_packed(K));
+  write_bin(dir + "/" + tag + "_L.bin", lower_packed(L));
+  write_bin(dir + "/" + tag + "_D.bin", D);
+  write_bin(dir + "/" + tag + "_b.bin", b);
+  write_bin(dir + "/" + tag + "_x.bin", x);
+  return 0;
+}
+
+static int mode_bk(const std::string& dir, size_t N, uint64_t seed, const std::string& tag) {
+  // Indefinite K with a zero trailing diagonal block (EqualityHandling::None
+  // structure): [H C^T; C 0].
+  Mat K = make_qd(N, seed);
+  const size_t n1 = (N * 3 + 3) / 4;
+  for (size_t i = n1; i < N; ++i) K[i][i] = 0.0;
+  Vec b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = 2.0 * u01(seed, TAG_B, i, 0) - 1.0;
+  auto [F, ipiv] = NO::LinearSolvers::symmetric_indefinite_factorization(K);
+  Vec x = b;
+  NO::LinearSolvers::overwriting_solve_bunch_kaufman(F, ipiv, x);
+  Vec piv(ipiv.begin(), ipiv.end());
+  write_bin(dir + "/" + tag + "_K.bin", flatten(K));
+  write_bin(dir + "/" + tag + "_F.bin", flatten(F));
+  write_bin(dir + "/" + tag + "_ipiv.bin", piv);
+  write_bin(dir + "/" + tag + "_b.bin", b);
+  write_bin(dir + "/" + tag + "_x.bin", x);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// One reference Newton iteration, restated around the reference's own private
+// methods (Optimizer.cpp:127-219), recording KKT, directions and scalars.
+struct IterRecord {
+  double f, res, mu, alpha_aff, mu_aff, sigma, alpha;
+  Mat kkt;
+  Vec D;
+  Mat vars, d_aff, d;
+};
+
+static IterRecord reference_iteration(NO::Optimizer& opt) {
+  IterRecord r{};
+  auto& env = opt.env_;
+  const auto& oe = opt.optimization_expressions_;
+  const auto& full_rhs = opt.newton_system_.rhs;
+  r.f = NO::Evaluation::evaluate_scalar(opt.objective_, env);
+  r.res = opt.get_residual_norm_(full_rhs);
+  r.mu = opt.get_mu_(full_rhs);
+  r.kkt = opt.get_as_matrix_(opt.augmented_system_.lhs);
+  auto [L, D] = NO::LinearSolvers::ldlt_decomposition(r.kkt);
+  r.D = D;
+  env.at(oe.mu) = NO::Evaluation::val_scalar(0.0);
+  for (const auto& [vec, def] : opt.shorthand_rhs_.vector_definitions) env[vec] = NO::Evaluation::evaluate(def, env);
+  r.vars = opt.eval_vector_of_expressions_<Vec>(opt.newton_system_.variables);
+  r.d_aff = opt.compute_search_direction_(opt.augmented_system_, L, D);
+  {
+    r.alpha_aff = opt.get_max_step_(r.vars, r.d_aff);
+    std::vector<std::unique_ptr<NO::ScopedEnvironmentOverride>> temps;
+    for (const auto& var : opt.newton_system_.variables) {
+      auto val = NO::Evaluation::evaluate(var, env);
+      temps.push_back(std::make_unique<NO::ScopedEnvironmentOverride>(env, var, val));
+    }
+    opt.update_variables_(r.alpha_aff, r.vars, r.d_aff);
+    r.mu_aff = opt.get_mu_(full_rhs);
+    r.sigma = r.mu > 0.0 ? std::pow(r.mu_aff / r.mu, 3) : 0.0;
+    env.at(oe.mu) = NO::Evaluation::val_scalar(r.mu * r.sigma);
+  }
+  {
+    std::vector<Expression::ExprPtr> delta_aff_variables;
+    for (const auto& v : opt.newton_system_.variables) {
+      const auto dv = SO::get_delta_variable(v);
+      const auto& var = std::get<Expression::Variable>(dv->get_impl());
+      delta_aff_variables.push_back(Expression::ExprFactory::variable(var.name + "_affine"));
+    }
+    for (const auto& [shorthand, expr] : opt.shorthand_rhs_.vector_definitions) {
+      auto val = NO::Evaluation::evaluate(expr, env);
+      if ((expr->contains_subexpression(oe.e_var) || expr->contains_subexpression(oe.e_ineq) ||
+           expr->contains_subexpression(oe.e_eq)) &&
+          expr->contains_subexpression(oe.mu)) {
+        auto dexpr = expr->replace_subexpression(oe.mu, Expression::zero);
+        for (auto& var : expr->get_variables()) {
+          const auto idx = opt.variable_index_.at(var);
+          env[delta_aff_variables.at(idx)] = NO::Evaluation::val_vector(r.d_aff.at(idx));
+          dexpr = dexpr->replace_subexpression(var, delta_aff_variables.at(idx));
+        }
+        val = NO::Evaluation::add(val, NO::Evaluation::evaluate(dexpr, env));
+      }
+      env[shorthand] = val;
+    }
+    r.d = opt.compute_search_direction_(opt.augmented_system_, L, D);
+    r.alpha = opt.get_max_step_(r.vars, r.d);
+    opt.update_variables_(0.995 * r.alpha, r.vars, r.d);
+  }
+  return r;
+}
+
+static int mode_newton(const std::string& dir, size_t n, size_t m, uint64_t seed, int iters, const std::string& tag) {
+  const QP q = make_qp(n, m, 0, seed);
+  NO::Data data;
+  data.Q = q.Q;
+  data.c = q.c;
+  data.A_ineq = q.A;
+  data.l_A_ineq = q.lA;
+  data.u_A_ineq = q.uA;
+  data.l_x = q.lx;
+  data.u_x = q.ux;
+  const SO::VariableNames names;
+  SO::Settings s = settings_from("SlackedSlacks", "none", m > 0);
+  const auto oe = SO::get_optimization_expressions(names);
+  auto env = NO::build_environment(names, data);
+  const auto ns = SO::get_newton_system(s, names);
+  Silence quiet;
+  NO::Optimizer opt(env, oe, ns);
+  std::ofstream meta(dir + "/" + tag + "_trace.txt");
+  meta.precision(17);
+  meta << "variables";
+  for (auto& v : opt.newton_system_.variables) meta << " " << to_s(v);
+  meta << "\n";
+  for (int it = 0; it < iters; ++it) {
+    {
+      const double res = opt.get_residual_norm_(opt.newton_system_.rhs);
+      const double mu = opt.get_mu_(opt.newton_system_.rhs);
+      if (res < 1e-8 && mu < 1e-8) {  // Optimizer.cpp:133
+        meta << "converged " << it << " res " << res << " mu " << mu << "\n";
+        break;
+      }
+    }
+    const IterRecord r = reference_iteration(opt);
+    meta << "iter " << it << " f " << r.f << " res " << r.res << " mu " << r.mu << " alpha_aff " << r.alpha_aff
+         << " mu_aff " << r.mu_aff << " sigma " << r.sigma << " alpha " << r.alpha << "\n";
+    const std::string p = dir + "/" + tag + "_it" + std::to_string(it);
+    if (it == 0) write_bin(p + "_kkt.bin", lower_packed(r.kkt));
+    write_bin(p + "_D.bin", r.D);
+    write_bin(p + "_vars.bin", flatten(r.vars));
+    write_bin(p + "_daff.bin", flatten(r.d_aff));
+    write_bin(p + "_d.bin", flatten(r.d));
+  }
+  return 0;
+}
+
+// C3 structure, component level: the reference's numeric path asserts on the
+// scalar (-delta^2) and zero blocks (Evaluation.cpp:57-60), so those blocks
+// are expanded here; every other block is the reference's own evaluation.
+static int mode_component_eq(const std::string& dir, size_t n, size_t m, size_t p, uint64_t seed,
+                             const std::string& tag) {
+  const QP q = make_qp(n, m, p, seed);
+  NO::Data data;
+  data.Q = q.Q;
+  data.c = q.c;
+  data.A_ineq = q.A;
+  data.l_A_ineq = q.lA;
+  data.u_A_ineq = q.uA;
+  data.A_eq = q.C;
+  data.b_eq = q.d;
+  data.l_x = q.lx;
+  data.u_x = q.ux;
+  const SO::VariableNames names;
+  SO::Settings s = settings_from("SlackedSlacks", "Regularization", true);
+  auto env = NO::build_environment(names, data);
+  const auto ns = SO::get_newton_system(s, names);
+  auto ns2 = ns;
+  const auto sh = SO::get_shorthand_rhs(ns);
+  ns2.rhs = sh.shorthand_rhs;
+  const auto aug = SO::get_augmented_system(ns2);
+  const size_t sizes[3] = {n, m, p};
+  const size_t nb = aug.lhs.size();
+  size_t N = 0;
+  for (size_t i = 0; i < nb; ++i) N += sizes[i];
+  Mat K(N, Vec(N, 0.0));
+  std::ofstream meta(dir + "/" + tag + "_blocks.txt");
+  size_t r0 = 0;
+  for (size_t bi = 0; bi < nb; ++bi) {
+    size_t c0 = 0;
+    for (size_t bj = 0; bj < nb; ++bj) {
+      const auto& e = aug.lhs[bi][bj];
+      const auto val = NO::Evaluation::evaluate(e, env);
+      meta << bi << " " << bj << " " << to_s(e) << " kind " << val.index() << "\n";
+      if (std::holds_alternative<double>(val)) {
+        const double sv = std::get<double>(val);
+        if (bi == bj) {
+          for (size_t k = 0; k < sizes[bi]; ++k) K[r0 + k][c0 + k] = sv;  // s*I expansion
+        } else if (sv != 0.0) {
+          std::cerr << "non-zero scalar off-diagonal block\n";
+          return 4;
+        }
+      } else {
+        const Mat M = NO::Evaluation::evaluate_matrix(e, env);
+        for (size_t a = 0; a < M.size(); ++a)
+          for (size_t b = 0; b < M[a].size(); ++b) K[r0 + a][c0 + b] = M[a][b];
+      }
+      c0 += sizes[bj];
+    }
+    r0 += sizes[bi];
+  }
+  Vec b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = 2.0 * u01(seed, TAG_B, i, 0) - 1.0;
+  auto [L, D] = NO::LinearSolvers::ldlt_decomposition(K);
+  Vec x = b;
+  NO::LinearSolvers::overwriting_solve_ldlt(L, D, x);
+  write_bin(dir + "/" + tag + "_K.bin", lower_packed(K));
+  write_bin(dir + "/" + tag + "_D.bin", D);
+  write_bin(dir + "/" + tag + "_b.bin", b);
+  write_bin(dir + "/" + tag + "_x.bin", x);
+  return 0;
+}
+
+int main(int argc, char** argv) {
+  if (argc < 3) {
+    std::cerr << "usage: ref_harness <mode> <dir> ...\n";
+    return 2;
+  }
+  const std::string mode = argv[1], dir = argv[2];
+  try {
+    if (mode == "formulation") return mode_formulation(dir);
+    if (mode == "ldlt" && argc == 6) return mode_ldlt(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
+    if (mode == "bk" && argc == 6) return mode_bk(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
+    if (mode == "newton" && argc == 8)
+      return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
+                         argv[7]);
+    if (mode == "component_eq" && argc == 8)
+      return mode_component_eq(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoul(argv[5]),
+                               std::stoull(argv[6]), argv[7]);
+  } catch (const std::exception& e) {
+    std::cerr << "reference threw: " << e.what() << "\n";
+    return 3;
+  }
+  std::cerr << "bad arguments\n";
+  return 2;
+}
