@@ -1,0 +1,195 @@
+#!/usr/bin/env python3
+"""Benchmark: Newton steps/sec + factor TFLOP/s on the dense QP n=8192
+(BASELINE.json configs[2], "C3": n=8192, m=2048 inequality rows, p=1024
+equality rows -> KKT N = 11264, augmented LDL^T), synthetic data (SURVEY.md
+§8d generator, seed 1234 + rank), generated in place in HBM.
+
+A "step" is one Newton iteration of Optimizer::solve_quasi_definite_
+(Optimizer.cpp:127-219) on the device: KKT assembly, blocked LDL^T, two
+(rhs + triangular solves + back-substitution), two ratio tests, mu_aff/sigma,
+update, and the next iterate's residuals/objective/mu.  A converged iterate
+is reset to the initial point on the device (no host round trip), so every
+timed step is a full Newton step.
+
+Multi-GPU (torchrun, one process per GPU): each rank solves its own
+independent QP -- the path does not shard a single QP (replicas, weak
+scaling) -- and RCCL all-reduces only the convergence scalars
+(max res, max mu, sum converged) once per step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+"""
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
+
+FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (BASELINE.md "Peaks")
+
+WORKLOADS = {
+    "c3": dict(n=8192, m=2048, p=1024, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
+                                          "(Regularization), augmented LDL^T, KKT N=11264"),
+    "c2size": dict(n=2048, m=512, p=0, desc="dense QP n=2048, m=512 ineq, augmented LDL^T, KKT N=2560"),
+    "small": dict(n=1024, m=256, p=128, desc="dense QP n=1024, m=256, p=128 (smoke size)"),
+}
+
+
+def cpu_baseline(wl, sample_scale=4):
+    """Time the CPU oracle (a bit-faithful restatement of the reference path,
+    oracle/ipmz_oracle.cpp, single thread) on a bounded sample: one Newton
+    step of the same workload with every dimension divided by sample_scale,
+    extrapolated per phase by its complexity (LDL^T N^3, assembly and the
+    rest O(N^2)).  The reference itself cannot run C3 (its evaluator asserts on
+    the Regularization block, Evaluation.cpp:57-60)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # test/baseline infrastructure only
+
+    n, m, p = (wl[k] // sample_scale for k in ("n", "m", "p"))
+    qp = oracle.gen_qp(n, m, p, 1234)
+    o = oracle.OracleQP(qp)
+    t0 = time.perf_counter()
+    _, _, ph = o.iterate_timed()
+    wall = time.perf_counter() - t0
+    Ns = n + m + p
+    Nf = wl["n"] + wl["m"] + wl["p"]
+    r = Nf / Ns
+    head = wall - (ph["assemble"] + ph["ldlt"] + ph["rest"])  # objective/res/mu evaluation
+    t_full = ph["ldlt"] * r ** 3 + (ph["assemble"] + ph["rest"] + head) * r ** 2
+    return {
+        "value": 1.0 / t_full,
+        "unit": "steps/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"1 Newton step of the oracle at n={n}, m={m}, p={p} (N={Ns}) took {wall:.2f} s "
+                   f"(LDL^T {ph['ldlt']:.2f} s); extrapolated to N={Nf} as LDL^T x{r ** 3:.0f} (N^3) + "
+                   f"rest x{r ** 2:.0f} (N^2) = {t_full:.1f} s/step; cpu={platform.processor() or platform.machine()}"),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
+    ap.add_argument("--nbo", type=int, default=int(os.environ.get("IPMZ_NBO", 256)))
+    ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 128)))
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (allows graph replay)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    else:
+        torch.cuda.set_device(0)
+
+    import ipmz_amd as I
+
+    wl = WORKLOADS[args.workload]
+    n, m, p = wl["n"], wl["m"], wl["p"]
+    Nk = n + m + p
+    stream = torch.cuda.current_stream()
+    ctx = I.Context(local_rank, stream=stream.cuda_stream, nbo=args.nbo, nbi=args.nbi)
+    qp = I.Optimizer(n, m, p, ctx)
+    qp.generate(1234 + rank)
+    timing = not args.no_timing
+    flags = I.STEP_RESTART_IF_CONVERGED | (0 if timing else I.STEP_GRAPH)
+    red = torch.zeros(3, dtype=torch.float64, device="cuda")
+    sc = torch.zeros(I.SC_COUNT, dtype=torch.float64, device="cuda")
+
+    def one_step():
+        qp.step(flags)
+        if world > 1:
+            # RCCL all-reduce of the convergence scalars only
+            qp.copy_scalars(sc.data_ptr())
+            red[0] = sc[I.SC["res"]]
+            red[1] = sc[I.SC["mu"]]
+            dist.all_reduce(red[:2], op=dist.ReduceOp.MAX)
+
+    for _ in range(args.warmup):
+        one_step()
+    torch.cuda.synchronize()
+    if timing:
+        qp.set_timing(True)  # resets the phase accumulators
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        one_step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = tt.item()
+    s = qp.scalars()
+    ph = qp.phase_times() if timing else None
+
+    if rank == 0:
+        steps_total = args.steps * world
+        value = steps_total / elapsed
+        out = {
+            "metric": "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X",
+            "value": value,
+            "unit": "steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": 1e3 * elapsed / args.steps,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; seed 1234+rank)",
+            "config": {"workload": args.workload, "n": n, "m": m, "p": p, "kkt_N": Nk,
+                       "formulation": "SlackedSlacks ineq + Regularization eq (delta=1e-4), augmented LDL^T",
+                       "parallelism": f"replicas x{world} (independent QPs, RCCL all-reduce of convergence "
+                                      f"scalars only)",
+                       "blocking": {"nbo": args.nbo, "nbi": args.nbi},
+                       "description": wl["desc"]},
+            "restarts": s["restarts"],
+        }
+        if ph:
+            k = args.steps
+            factor_ms = ph["factor"] / k
+            out["factor_tflops"] = (Nk ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
+            out["phase_ms_per_step"] = {kk: ph[kk] / k for kk in ("step", "assemble", "factor", "solve", "eval")}
+            tr_s = ph["trailing"] * 1e-3
+            launches = ph["trailing_launches"]
+            achieved = ph["trailing_flops"] / tr_s / 1e12 if tr_s > 0 else 0.0
+            out["roofline"] = {
+                "bound": "mfma",
+                "kernel": "gemm_nt_f64_kernel<128,128,EPI_SUB> (trailing update A22 -= W21 L21^T, fp64 MFMA)",
+                "achieved": achieved,
+                "peak": FP64_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
+                "traffic": None,
+                "launches": launches,
+                "avg_launch_ms": ph["trailing"] / max(1, launches),
+                "flops_per_launch": ph["trailing_flops"] / max(1, launches),
+            }
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(wl)
+        print(json.dumps(out))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,177 @@
+/*
+ * ipmz.h -- C ABI of libipmz, the MI355X (gfx950) implementation of
+ * ipm-zoo's numerical interior-point Newton step.
+ *
+ * Drop-in boundary.  The reference has no FFI: its hot path
+ * is a set of C++ free functions plus one class, all called from Optimizer.
+ * Each entry point below replaces one of them:
+ *
+ *   ipmz_ldlt_decomposition     <- LinearSolvers::ldlt_decomposition
+ *                                  (include/NumericalOptimization/LinearSolvers.h:11,
+ *                                   src/NumericalOptimization/LinearSolvers.cpp:14-42)
+ *   ipmz_overwriting_solve_ldlt <- LinearSolvers::overwriting_solve_ldlt
+ *                                  (LinearSolvers.h:16-17, LinearSolvers.cpp:44-74)
+ *   ipmz_ldlt_factor / _solve   <- the same pair on device-resident K (no copies)
+ *   ipmz_qp_create + ipmz_qp_load_host
+ *                               <- NumericalOptimization::build_environment
+ *                                  (EnvironmentBuilder.h:19-20, EnvironmentBuilder.cpp:7-76)
+ *                                  + Optimizer::Optimizer (Optimizer.h:15-18)
+ *   ipmz_qp_step                <- one body of Optimizer::solve_quasi_definite_
+ *                                  (Optimizer.cpp:127-219): assembly
+ *                                  (get_as_matrix_, :387-391), factor, two
+ *                                  compute_search_direction_ (:344-380), two
+ *                                  get_max_step_ (:270-342), update (:222-231)
+ *   ipmz_qp_solve               <- Optimizer::solve (Optimizer.h:20, Optimizer.cpp:63-73)
+ *
+ * Conventions
+ *   - Plain pointers and sizes only.  "device" pointers are HIP device
+ *     memory on the context's device, "host" pointers are ordinary memory.
+ *   - Dense matrices are row-major.  K is symmetric; only its lower triangle
+ *     (i >= j) is read, and the factor overwrites the strict lower triangle
+ *     with L (unit diagonal implicit) -- row-major lower == the reference's
+ *     L[i][j], i > j.
+ *   - Return value: 0 success; > 0 = 1-based index of the first non-finite
+ *     pivot (the factorization still completes, as the reference's does);
+ *     < 0 = error (IPMZ_ERR_*), message via ipmz_last_error().  The zero-pivot
+ *     rule of the reference (an exactly-zero pivot becomes 1e-8,
+ *     LinearSolvers.cpp:26-28) is not an error, as in the reference.
+ *   - All device work is enqueued on the context's stream; functions whose
+ *     outputs are host memory synchronize it.
+ *   - There is no CPU fallback: without a usable gfx950 device every entry
+ *     point that computes returns IPMZ_ERR_NO_DEVICE.
+ */
+#ifndef IPMZ_H
+#define IPMZ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IPMZ_OK 0
+#define IPMZ_ERR_INVALID (-1)
+#define IPMZ_ERR_HIP (-2)
+#define IPMZ_ERR_NOMEM (-3)
+#define IPMZ_ERR_NO_DEVICE (-4)
+#define IPMZ_ERR_STATE (-5)
+
+/* Canonical Newton-variable slots.  The reference's Newton-variable order
+ * (get_newton_system, SlackedSlacks + Regularization) is this order with the
+ * absent blocks dropped; state vectors are concatenated in it. */
+enum ipmz_slot {
+  IPMZ_SLOT_X = 0, IPMZ_SLOT_LAMBDA_A, IPMZ_SLOT_LAMBDA_C, IPMZ_SLOT_S, IPMZ_SLOT_P,
+  IPMZ_SLOT_LAMBDA_G, IPMZ_SLOT_LAMBDA_H, IPMZ_SLOT_LAMBDA_Y, IPMZ_SLOT_LAMBDA_Z,
+  IPMZ_SLOT_G, IPMZ_SLOT_H, IPMZ_SLOT_Y, IPMZ_SLOT_Z, IPMZ_NSLOT
+};
+
+/* Per-iteration scalars (device block of IPMZ_SC_COUNT doubles). */
+enum ipmz_scalar {
+  IPMZ_SC_F = 0,        /* objective 0.5 x'Qx + c'x of the current iterate   */
+  IPMZ_SC_RES,          /* ||full rhs at mu = 0||_2 (get_residual_norm_)      */
+  IPMZ_SC_MU,           /* mean |complementarity| (get_mu_)                   */
+  IPMZ_SC_ALPHA_AFF,    /* last step: affine step length                      */
+  IPMZ_SC_MU_AFF,       /* last step: mu at the affine trial point            */
+  IPMZ_SC_SIGMA,        /* last step: (mu_aff / mu)^3                         */
+  IPMZ_SC_ALPHA,        /* last step: corrector step length (before 0.995)    */
+  IPMZ_SC_CONVERGED,    /* 1.0 when res < 1e-8 and mu < 1e-8                  */
+  IPMZ_SC_MU_NEW,       /* last step: sigma * mu                              */
+  IPMZ_SC_RESTARTS,     /* benchmark restarts taken                           */
+  IPMZ_SC_COUNT = 16
+};
+
+typedef struct ipmz_ctx ipmz_ctx;
+typedef struct ipmz_qp ipmz_qp;
+
+/* ---- context ---------------------------------------------------------- */
+int ipmz_ctx_create(ipmz_ctx** out, int device);
+int ipmz_ctx_destroy(ipmz_ctx* ctx);
+/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
+ * NULL restores the context's own stream. */
+int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* hip_stream);
+int ipmz_ctx_sync(ipmz_ctx* ctx);
+const char* ipmz_last_error(void);
+/* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512),
+ * inner diagonal block nbi (64 or 128).  Defaults 256 / 128. */
+int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);
+
+/* ---- LinearSolvers on device memory ------------------------------------ */
+/* Workspace for factor + solve of order N (bytes). */
+int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N);
+/* In-place LDL^T of the lower triangle of K (device, row-major, ld >= N,
+ * ld even).  D: device, N doubles.  ws: device workspace; it keeps the
+ * inverted diagonal blocks that ipmz_ldlt_solve consumes. */
+int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes);
+/* b <- K^{-1} b with the factor left by ipmz_ldlt_factor (device b). */
+int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b);
+/* Rebuild the solve workspace from an explicit unit-lower L (device). */
+int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, void* ws, int64_t ws_bytes);
+
+/* ---- LinearSolvers with the reference's host signatures ------------------ */
+/* A: host N x N row-major (lower triangle read).  L: host N x N, written
+ * full (zeros above, ones on the diagonal); D: host N. */
+int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, double* D);
+/* L: host N x N unit lower; D: host N; b: host N, overwritten with the
+ * solution.  N == 0 is a no-op (LinearSolvers.cpp:46-48). */
+int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const double* D, double* b);
+
+/* ---- the Newton-step solver --------------------------------------------- */
+typedef struct ipmz_qp_config {
+  int n;         /* primal dimension                                  */
+  int m;         /* inequality rows  l_A <= A x <= u_A (SlackedSlacks) */
+  int p;         /* equality rows C x = d (Regularization)            */
+  double delta;  /* regularization (EnvironmentBuilder.cpp:48: 1e-4)  */
+} ipmz_qp_config;
+
+int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out);
+int ipmz_qp_destroy(ipmz_qp* qp);
+/* build_environment: validates l_x < u_x and l_A <= u_A (throws in the
+ * reference, IPMZ_ERR_INVALID here), copies the data, sets the initial
+ * iterate and evaluates it.  Host pointers; unused blocks may be NULL. */
+int ipmz_qp_load_host(ipmz_qp* qp, const double* Q, const double* c, const double* A, const double* l_A,
+                      const double* u_A, const double* C, const double* d, const double* l_x, const double* u_x);
+/* The synthetic QP of SURVEY.md §8d generated in place on the device. */
+int ipmz_qp_generate(ipmz_qp* qp, uint64_t seed);
+/* Enqueue one Newton step (asynchronous).  flags: */
+#define IPMZ_STEP_RESTART_IF_CONVERGED 1 /* reset a converged iterate to the initial one first */
+#define IPMZ_STEP_GRAPH 2                /* capture once into a hipGraph, then replay */
+int ipmz_qp_step(ipmz_qp* qp, int flags);
+/* Synchronize and copy the IPMZ_SC_COUNT scalars to host memory. */
+int ipmz_qp_scalars(ipmz_qp* qp, double* out);
+/* Device pointer of the scalar block (for collectives). */
+int ipmz_qp_device_scalars(ipmz_qp* qp, double** out);
+/* Enqueue a device-to-device copy of the scalar block to dst (device). */
+int ipmz_qp_copy_scalars(ipmz_qp* qp, double* dst_device);
+/* Optimizer::solve: iterate until res < 1e-8 and mu < 1e-8 or max_iter.
+ * trace (host, may be NULL): max_iter rows of 8 doubles
+ * {f, res, mu, alpha_aff, mu_aff, sigma, alpha, converged}. */
+int ipmz_qp_solve(ipmz_qp* qp, int max_iter, double* trace, int* iterations);
+/* Concatenated state in Newton order.  which: 0 iterate, 1 affine
+ * direction, 2 corrector direction, 3 residual vectors r_v. */
+#define IPMZ_STATE_VARS 0
+#define IPMZ_STATE_DAFF 1
+#define IPMZ_STATE_DIR 2
+#define IPMZ_STATE_RES 3
+int64_t ipmz_qp_state_len(ipmz_qp* qp);
+int ipmz_qp_get_state(ipmz_qp* qp, int which, double* host_out);
+/* Overwrite the iterate (host, Newton order) and re-evaluate it. */
+int ipmz_qp_set_state(ipmz_qp* qp, const double* host_vars);
+/* Assemble the KKT matrix of the current iterate; host N x N row-major
+ * (lower triangle written, upper zero).  For parity tests. */
+int ipmz_qp_get_kkt(ipmz_qp* qp, double* host_K);
+int ipmz_qp_kkt_dim(ipmz_qp* qp);
+
+/* Phase timing (HIP events on the context stream; eager launches only).
+ * ms: host array of IPMZ_PH_COUNT floats, cumulative since enable. */
+enum ipmz_phase {
+  IPMZ_PH_STEP = 0, IPMZ_PH_ASSEMBLE, IPMZ_PH_FACTOR, IPMZ_PH_SOLVE, IPMZ_PH_TRAILING, IPMZ_PH_EVAL,
+  IPMZ_PH_COUNT = 8
+};
+int ipmz_qp_set_timing(ipmz_qp* qp, int enable);
+int ipmz_qp_phase_times(ipmz_qp* qp, double* ms, double* trailing_flops, int64_t* trailing_launches);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IPMZ_H */

@@ -1,0 +1,670 @@
+// C ABI of libipmz (include/ipmz.h): contexts, the LinearSolvers entry
+// points and the Newton-step solver object.  Host orchestration only -- all
+// arithmetic runs in the gfx950 kernels of ldlt.hip / trsv.hip / newton.hip.
+// There is deliberately no CPU fallback: without a device every computing
+// entry point fails with IPMZ_ERR_NO_DEVICE.
+#include <hip/hip_runtime.h>
+
+#include <climits>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ipmz.h"
+#include "kernels.h"
+
+using namespace ipmz;
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+#define HIP_OK(expr)                                                                                     \
+  do {                                                                                                   \
+    hipError_t _e = (expr);                                                                              \
+    if (_e != hipSuccess)                                                                                \
+      return fail(IPMZ_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(_e) + " @" + __FILE__ + ":" + \
+                                    std::to_string(__LINE__));                                           \
+  } while (0)
+
+int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+
+}  // namespace
+
+struct ipmz_ctx {
+  int device = 0;
+  hipStream_t own = nullptr;
+  hipStream_t stream = nullptr;
+  int nbo = 256, nbi = 128;
+};
+
+static int check_device(int device) {
+  int count = 0;
+  if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
+    return fail(IPMZ_ERR_NO_DEVICE, "no HIP device visible: libipmz has no CPU fallback");
+  if (device < 0 || device >= count) return fail(IPMZ_ERR_INVALID, "device index out of range");
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail(IPMZ_ERR_NO_DEVICE, "device query failed");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(IPMZ_ERR_NO_DEVICE, std::string("libipmz is built for gfx950, device is ") + prop.gcnArchName);
+  return IPMZ_OK;
+}
+
+extern "C" {
+
+const char* ipmz_last_error(void) { return g_last_error.c_str(); }
+
+int ipmz_ctx_create(ipmz_ctx** out, int device) {
+  if (!out) return fail(IPMZ_ERR_INVALID, "null out");
+  *out = nullptr;
+  int rc = check_device(device);
+  if (rc) return rc;
+  HIP_OK(hipSetDevice(device));
+  auto* c = new ipmz_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(IPMZ_ERR_HIP, "hipStreamCreate failed");
+  }
+  c->stream = c->own;
+  *out = c;
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_destroy(ipmz_ctx* ctx) {
+  if (!ctx) return IPMZ_OK;
+  hipSetDevice(ctx->device);
+  hipStreamSynchronize(ctx->stream);
+  if (ctx->own) hipStreamDestroy(ctx->own);
+  delete ctx;
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* s) {
+  if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
+  ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_sync(ipmz_ctx* ctx) {
+  if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
+  if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
+  if ((nbi != 64 && nbi != 128) || nbo < nbi || nbo % nbi != 0 || nbo > IPMZ_NBO_MAX)
+    return fail(IPMZ_ERR_INVALID, "blocking: nbi in {64,128}, nbo a multiple of nbi, <= 512");
+  ctx->nbo = nbo;
+  ctx->nbi = nbi;
+  return IPMZ_OK;
+}
+
+// ---------------------------------------------------------------------------
+// Workspace: [info int (256 B)] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
+namespace {
+struct WsLayout {
+  int64_t info_off, side_off, linv_off, w_off, total;
+};
+WsLayout ws_layout(int N, int nbo, int nbi) {
+  WsLayout l;
+  const int64_t nblk = (N + nbi - 1) / nbi;
+  l.info_off = 0;
+  l.side_off = 256;
+  l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
+  l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
+  l.total = l.w_off + round_up((int64_t)N * nbo * 8, 256);
+  return l;
+}
+}  // namespace
+
+int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N) {
+  if (!ctx || N < 0) return 0;
+  return ws_layout(N, ctx->nbo, ctx->nbi).total;
+}
+
+static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, char* ws, TrailTimer* timer) {
+  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
+  int* info = reinterpret_cast<int*>(ws + l.info_off);
+  HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
+  HIP_OK(ldlt_factor(K, ld, N, D, reinterpret_cast<double*>(ws + l.linv_off), reinterpret_cast<double*>(ws + l.w_off),
+                     ctx->nbo, ctx->nbi, info, ctx->stream, timer));
+  return IPMZ_OK;
+}
+
+static int read_info(ipmz_ctx* ctx, const char* ws) {
+  int info = 0;
+  HIP_OK(hipMemcpyAsync(&info, ws, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return info == 0x7f7f7f7f ? IPMZ_OK : info;
+}
+
+int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes) {
+  if (!ctx || N < 0 || (N > 0 && (!K || !D || !ws)) || ld < N || (ld & 1))
+    return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_factor: bad arguments (ld >= N, ld even)");
+  if (N == 0) return IPMZ_OK;
+  if (ws_bytes < ws_layout(N, ctx->nbo, ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  HIP_OK(hipSetDevice(ctx->device));
+  int rc = factor_impl(ctx, N, K, ld, D, static_cast<char*>(ws), nullptr);
+  if (rc) return rc;
+  return read_info(ctx, static_cast<char*>(ws));
+}
+
+int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b) {
+  if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_solve: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
+  const char* w = static_cast<const char*>(ws);
+  HIP_OK(ldlt_solve(K, ld, N, D, reinterpret_cast<const double*>(w + l.linv_off), ctx->nbi, b,
+                    reinterpret_cast<double*>(const_cast<char*>(w) + l.side_off), ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, void* ws, int64_t ws_bytes) {
+  if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_prepare_solve: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  if (ws_bytes < ws_layout(N, ctx->nbo, ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  HIP_OK(hipSetDevice(ctx->device));
+  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
+  HIP_OK(linv_from_l(L, ld, N, ctx->nbi, reinterpret_cast<double*>(static_cast<char*>(ws) + l.linv_off),
+                     ctx->stream));
+  return IPMZ_OK;
+}
+
+// Host adapters with the reference's signatures ------------------------------
+int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, double* D) {
+  if (!ctx || N < 0 || (N > 0 && (!A || !L || !D))) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_decomposition: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  const int64_t ld = round_up(N, 64);
+  const int64_t wsb = ws_layout(N, ctx->nbo, ctx->nbi).total;
+  double *dK = nullptr, *dD = nullptr;
+  char* ws = nullptr;
+  HIP_OK(hipMalloc(&dK, (size_t)(ld * N * 8)));
+  if (hipMalloc(&dD, (size_t)N * 8) != hipSuccess || hipMalloc(&ws, (size_t)wsb) != hipSuccess) {
+    hipFree(dK);
+    hipFree(dD);
+    return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  }
+  int rc = IPMZ_OK;
+  if (hipMemcpy2DAsync(dK, ld * 8, A, (size_t)N * 8, (size_t)N * 8, N, hipMemcpyHostToDevice, ctx->stream) !=
+      hipSuccess)
+    rc = fail(IPMZ_ERR_HIP, "copy-in failed");
+  if (!rc) rc = factor_impl(ctx, N, dK, ld, dD, ws, nullptr);
+  int info = 0;
+  if (!rc) {
+    info = read_info(ctx, ws);
+    if (info < 0) rc = info;
+  }
+  if (!rc) {
+    if (hipMemcpy2D(L, (size_t)N * 8, dK, ld * 8, (size_t)N * 8, N, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(D, dD, (size_t)N * 8, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = fail(IPMZ_ERR_HIP, "copy-out failed");
+  }
+  hipFree(dK);
+  hipFree(dD);
+  hipFree(ws);
+  if (rc) return rc;
+  // the reference returns a full L: zeros above, ones on the diagonal (LinearSolvers.cpp:18, :38)
+  for (int i = 0; i < N; ++i) {
+    L[(int64_t)i * N + i] = 1.0;
+    for (int j = i + 1; j < N; ++j) L[(int64_t)i * N + j] = 0.0;
+  }
+  return info;
+}
+
+int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const double* D, double* b) {
+  if (!ctx || N < 0) return fail(IPMZ_ERR_INVALID, "ipmz_overwriting_solve_ldlt: bad arguments");
+  if (N == 0) return IPMZ_OK;  // LinearSolvers.cpp:46-48
+  if (!L || !D || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
+  HIP_OK(hipSetDevice(ctx->device));
+  const int64_t ld = round_up(N, 64);
+  const int64_t wsb = ws_layout(N, ctx->nbo, ctx->nbi).total;
+  double *dL = nullptr, *dD = nullptr, *db = nullptr;
+  char* ws = nullptr;
+  bool ok = hipMalloc(&dL, (size_t)(ld * N * 8)) == hipSuccess && hipMalloc(&dD, (size_t)N * 8) == hipSuccess &&
+            hipMalloc(&db, (size_t)N * 8) == hipSuccess && hipMalloc(&ws, (size_t)wsb) == hipSuccess;
+  int rc = ok ? IPMZ_OK : fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  if (!rc && (hipMemcpy2DAsync(dL, ld * 8, L, (size_t)N * 8, (size_t)N * 8, N, hipMemcpyHostToDevice, ctx->stream) !=
+                  hipSuccess ||
+              hipMemcpyAsync(dD, D, (size_t)N * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+              hipMemcpyAsync(db, b, (size_t)N * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
+    rc = fail(IPMZ_ERR_HIP, "copy-in failed");
+  if (!rc) rc = ipmz_ldlt_prepare_solve(ctx, N, dL, ld, ws, wsb);
+  if (!rc) rc = ipmz_ldlt_solve(ctx, N, dL, ld, dD, ws, db);
+  if (!rc && (hipMemcpyAsync(b, db, (size_t)N * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+              hipStreamSynchronize(ctx->stream) != hipSuccess))
+    rc = fail(IPMZ_ERR_HIP, "copy-out failed");
+  hipFree(dL);
+  hipFree(dD);
+  hipFree(db);
+  hipFree(ws);
+  return rc;
+}
+
+}  // extern "C"
+
+// ===========================================================================
+// Newton-step solver
+struct ipmz_qp {
+  ipmz_ctx* ctx = nullptr;
+  int n = 0, m = 0, p = 0, N = 0;
+  int64_t ldn = 0, ldk = 0, state_len = 0;
+  double delta = 1e-4;
+  std::vector<void*> allocs;
+  QPDev q{};
+  double *K = nullptr, *D = nullptr;
+  char* ws = nullptr;
+  int64_t ws_bytes = 0;
+  double *v0 = nullptr, *r0 = nullptr, *scal0 = nullptr;
+  bool loaded = false;
+  hipGraph_t graph = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  int graph_flags = -1;
+  // timing
+  bool timing = false;
+  std::vector<hipEvent_t> ev;  // phase boundary events
+  hipEvent_t (*tr_pairs)[2] = nullptr;
+  int tr_cap = 0;
+  double ph_ms[IPMZ_PH_COUNT] = {0};
+  double tr_flops = 0.0;
+  int64_t tr_launches = 0;
+};
+
+namespace {
+int64_t slot_len(const ipmz_qp* s, int slot) {
+  switch (slot) {
+    case X: case LY: case LZ: case Y: case Z: return s->n;
+    case LA: case S: case LG: case LH: case G: case H: return s->m;
+    default: return s->p;
+  }
+}
+
+template <typename T>
+int dev_alloc(ipmz_qp* s, T** p, int64_t count) {
+  void* ptr = nullptr;
+  const size_t bytes = (size_t)round_up(count < 1 ? 1 : count, 8) * sizeof(T);
+  if (hipMalloc(&ptr, bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "hipMalloc failed");
+  s->allocs.push_back(ptr);
+  *p = static_cast<T*>(ptr);
+  return IPMZ_OK;
+}
+
+// slot pointers into one contiguous Newton-order vector
+void carve(const ipmz_qp* s, double* base, double** slots) {
+  int64_t off = 0;
+  for (int k = 0; k < NSLOT; ++k) {
+    slots[k] = base + off;
+    off += slot_len(s, k);
+  }
+}
+
+int run_step(ipmz_qp* s, int flags) {
+  hipStream_t st = s->ctx->stream;
+  QPDev& q = s->q;
+  const bool t = s->timing;
+  auto mark = [&](int i) {
+    if (t) hipEventRecord(s->ev[i], st);
+  };
+  if (flags & IPMZ_STEP_RESTART_IF_CONVERGED)
+    HIP_OK(qp_restart_if_converged(q, s->v0, s->r0, s->scal0, s->state_len, st));
+  mark(0);
+  HIP_OK(qp_assemble(q, s->K, s->ldk, st));
+  mark(1);
+  TrailTimer tt;
+  tt.pairs = s->tr_pairs;
+  tt.cap = t ? s->tr_cap : 0;
+  int rc = factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, t ? &tt : nullptr);
+  if (rc) return rc;
+  mark(2);
+  const WsLayout l = ws_layout(s->N, s->ctx->nbo, s->ctx->nbi);
+  const double* Linv = reinterpret_cast<const double*>(s->ws + l.linv_off);
+  double* side = reinterpret_cast<double*>(s->ws + l.side_off);
+  const int nbi = s->ctx->nbi;
+  // predictor (affine scaling) direction
+  HIP_OK(qp_rhs(q, st));
+  HIP_OK(ldlt_solve(s->K, s->ldk, s->N, s->D, Linv, nbi, q.b, side, st));
+  mark(3);
+  HIP_OK(qp_backsub(q, q.daff, st));
+  HIP_OK(qp_ratio(q, q.daff, SC_ALPHA_AFF, st));
+  HIP_OK(qp_mu_aff(q, st));
+  // centering-corrector direction
+  HIP_OK(qp_corrector_residuals(q, st));
+  HIP_OK(qp_rhs(q, st));
+  mark(4);
+  HIP_OK(ldlt_solve(s->K, s->ldk, s->N, s->D, Linv, nbi, q.b, side, st));
+  mark(5);
+  HIP_OK(qp_backsub(q, q.dir, st));
+  HIP_OK(qp_ratio(q, q.dir, SC_ALPHA, st));
+  HIP_OK(qp_update(q, st));
+  mark(6);
+  HIP_OK(qp_evaluate(q, st));
+  mark(7);
+  if (t) {
+    HIP_OK(hipStreamSynchronize(st));
+    float ms = 0.f;
+    auto el = [&](int a, int b) {
+      hipEventElapsedTime(&ms, s->ev[a], s->ev[b]);
+      return (double)ms;
+    };
+    s->ph_ms[IPMZ_PH_STEP] += el(0, 7);
+    s->ph_ms[IPMZ_PH_ASSEMBLE] += el(0, 1);
+    s->ph_ms[IPMZ_PH_FACTOR] += el(1, 2);
+    s->ph_ms[IPMZ_PH_SOLVE] += el(2, 3) + el(4, 5);
+    s->ph_ms[IPMZ_PH_EVAL] += el(6, 7);
+    for (int i = 0; i < tt.used; ++i) {
+      hipEventElapsedTime(&ms, s->tr_pairs[i][0], s->tr_pairs[i][1]);
+      s->ph_ms[IPMZ_PH_TRAILING] += ms;
+    }
+    s->tr_launches += tt.used;
+    s->tr_flops += tt.flops;
+  }
+  return IPMZ_OK;
+}
+
+int evaluate_and_save(ipmz_qp* s) {
+  hipStream_t st = s->ctx->stream;
+  HIP_OK(qp_evaluate(s->q, st));
+  HIP_OK(hipMemcpyAsync(s->v0, s->q.v[0], s->state_len * 8, hipMemcpyDeviceToDevice, st));
+  HIP_OK(hipMemcpyAsync(s->r0, s->q.r[0], s->state_len * 8, hipMemcpyDeviceToDevice, st));
+  HIP_OK(hipMemcpyAsync(s->scal0, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToDevice, st));
+  s->loaded = true;
+  return IPMZ_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out) {
+  if (!ctx || !cfg || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+  *out = nullptr;
+  if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0) return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0");
+  HIP_OK(hipSetDevice(ctx->device));
+  auto* s = new ipmz_qp();
+  s->ctx = ctx;
+  s->n = cfg->n;
+  s->m = cfg->m;
+  s->p = cfg->p;
+  s->N = cfg->n + cfg->m + cfg->p;
+  s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
+  s->ldn = round_up(s->n, 8);
+  s->ldk = round_up(s->N, 64);
+  s->state_len = 2 * (int64_t)s->n * 2 + s->n + 6 * (int64_t)s->m + 2 * (int64_t)s->p;  // 5n + 6m + 2p
+  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + 2 * (int64_t)s->p;
+  QPDev& q = s->q;
+  q.n = s->n;
+  q.m = s->m;
+  q.p = s->p;
+  q.N = s->N;
+  q.ldn = s->ldn;
+  q.delta = s->delta;
+  int rc = 0;
+  double *Q, *A, *C, *c, *lA, *uA, *d, *lx, *ux, *v, *r, *da, *di;
+  rc |= dev_alloc(s, &Q, (int64_t)s->n * s->ldn);
+  rc |= dev_alloc(s, &A, (int64_t)s->m * s->ldn);
+  rc |= dev_alloc(s, &C, (int64_t)s->p * s->ldn);
+  rc |= dev_alloc(s, &c, s->n);
+  rc |= dev_alloc(s, &lA, s->m);
+  rc |= dev_alloc(s, &uA, s->m);
+  rc |= dev_alloc(s, &d, s->p);
+  rc |= dev_alloc(s, &lx, s->n);
+  rc |= dev_alloc(s, &ux, s->n);
+  rc |= dev_alloc(s, &v, s->state_len);
+  rc |= dev_alloc(s, &r, s->state_len);
+  rc |= dev_alloc(s, &da, s->state_len);
+  rc |= dev_alloc(s, &di, s->state_len);
+  rc |= dev_alloc(s, &q.Qx, s->n);
+  rc |= dev_alloc(s, &q.ATl, s->n);
+  rc |= dev_alloc(s, &q.CTl, s->n);
+  rc |= dev_alloc(s, &q.Ax, s->m);
+  rc |= dev_alloc(s, &q.Cx, s->p);
+  rc |= dev_alloc(s, &q.b, s->N);
+  rc |= dev_alloc(s, &q.scal, SC_COUNT);
+  rc |= dev_alloc(s, &q.part, 4 * 1024);
+  rc |= dev_alloc(s, &q.tpart, (int64_t)((s->m > s->p ? s->m : s->p) + 127) / 128 * s->n + 8);
+  rc |= dev_alloc(s, &s->K, (int64_t)s->N * s->ldk);
+  rc |= dev_alloc(s, &s->D, s->N);
+  s->ws_bytes = ws_layout(s->N, ctx->nbo, ctx->nbi).total;
+  rc |= dev_alloc(s, &s->ws, s->ws_bytes);
+  rc |= dev_alloc(s, &s->v0, s->state_len);
+  rc |= dev_alloc(s, &s->r0, s->state_len);
+  rc |= dev_alloc(s, &s->scal0, SC_COUNT);
+  if (rc) {
+    ipmz_qp_destroy(s);
+    return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  }
+  q.Q = Q;
+  q.A = A;
+  q.C = C;
+  q.c = c;
+  q.lA = lA;
+  q.uA = uA;
+  q.d = d;
+  q.lx = lx;
+  q.ux = ux;
+  carve(s, v, q.v);
+  carve(s, r, q.r);
+  carve(s, da, q.daff);
+  carve(s, di, q.dir);
+  HIP_OK(hipMemsetAsync(q.scal, 0, SC_COUNT * 8, ctx->stream));
+  HIP_OK(hipMemsetAsync(s->K, 0, (size_t)s->N * s->ldk * 8, ctx->stream));
+  *out = s;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_destroy(ipmz_qp* s) {
+  if (!s) return IPMZ_OK;
+  hipSetDevice(s->ctx->device);
+  hipStreamSynchronize(s->ctx->stream);
+  if (s->gexec) hipGraphExecDestroy(s->gexec);
+  if (s->graph) hipGraphDestroy(s->graph);
+  for (auto e : s->ev) hipEventDestroy(e);
+  if (s->tr_pairs) {
+    for (int i = 0; i < s->tr_cap; ++i) {
+      hipEventDestroy(s->tr_pairs[i][0]);
+      hipEventDestroy(s->tr_pairs[i][1]);
+    }
+    delete[] s->tr_pairs;
+  }
+  for (void* p : s->allocs) hipFree(p);
+  delete s;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_load_host(ipmz_qp* s, const double* Q, const double* c, const double* A, const double* lA,
+                      const double* uA, const double* C, const double* d, const double* lx, const double* ux) {
+  if (!s || !Q || !c || !lx || !ux || (s->m && (!A || !lA || !uA)) || (s->p && (!C || !d)))
+    return fail(IPMZ_ERR_INVALID, "ipmz_qp_load_host: missing data block");
+  // EnvironmentBuilder.cpp:12-17 (the reference ASSERTs; here an error code)
+  for (int i = 0; i < s->n; ++i)
+    if (!(lx[i] < ux[i])) return fail(IPMZ_ERR_INVALID, "l_x < u_x violated at " + std::to_string(i));
+  for (int i = 0; i < s->m; ++i)
+    if (!(lA[i] <= uA[i])) return fail(IPMZ_ERR_INVALID, "l_A <= u_A violated at " + std::to_string(i));
+  HIP_OK(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  QPDev& q = s->q;
+  const size_t rowb = (size_t)s->n * 8, ldb = (size_t)s->ldn * 8;
+  HIP_OK(hipMemcpy2DAsync((void*)q.Q, ldb, Q, rowb, rowb, s->n, hipMemcpyHostToDevice, st));
+  if (s->m) HIP_OK(hipMemcpy2DAsync((void*)q.A, ldb, A, rowb, rowb, s->m, hipMemcpyHostToDevice, st));
+  if (s->p) HIP_OK(hipMemcpy2DAsync((void*)q.C, ldb, C, rowb, rowb, s->p, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync((void*)q.c, c, rowb, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync((void*)q.lx, lx, rowb, hipMemcpyHostToDevice, st));
+  HIP_OK(hipMemcpyAsync((void*)q.ux, ux, rowb, hipMemcpyHostToDevice, st));
+  if (s->m) {
+    HIP_OK(hipMemcpyAsync((void*)q.lA, lA, (size_t)s->m * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync((void*)q.uA, uA, (size_t)s->m * 8, hipMemcpyHostToDevice, st));
+  }
+  if (s->p) HIP_OK(hipMemcpyAsync((void*)q.d, d, (size_t)s->p * 8, hipMemcpyHostToDevice, st));
+  HIP_OK(qp_init_iterate(q, st));
+  int rc = evaluate_and_save(s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(st));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_generate(ipmz_qp* s, uint64_t seed) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  QPDev& q = s->q;
+  HIP_OK(qp_generate(s->n, s->m, s->p, s->ldn, seed, (double*)q.Q, (double*)q.c, (double*)q.A, (double*)q.lA,
+                     (double*)q.uA, (double*)q.C, (double*)q.d, (double*)q.lx, (double*)q.ux, st));
+  HIP_OK(qp_init_iterate(q, st));
+  int rc = evaluate_and_save(s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(st));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_step(ipmz_qp* s, int flags) {
+  if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  if (!(flags & IPMZ_STEP_GRAPH) || s->timing) return run_step(s, flags);
+  hipStream_t st = s->ctx->stream;
+  if (!s->gexec || s->graph_flags != flags) {
+    if (s->gexec) hipGraphExecDestroy(s->gexec);
+    if (s->graph) hipGraphDestroy(s->graph);
+    s->gexec = nullptr;
+    s->graph = nullptr;
+    HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    int rc = run_step(s, flags);
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc) {
+      if (g) hipGraphDestroy(g);
+      return rc;
+    }
+    if (e != hipSuccess) return fail(IPMZ_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
+    s->graph = g;
+    HIP_OK(hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0));
+    s->graph_flags = flags;
+  }
+  HIP_OK(hipGraphLaunch(s->gexec, st));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_scalars(ipmz_qp* s, double* out) {
+  if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(hipMemcpyAsync(out, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_device_scalars(ipmz_qp* s, double** out) {
+  if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+  *out = s->q.scal;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_copy_scalars(ipmz_qp* s, double* dst) {
+  if (!s || !dst) return fail(IPMZ_ERR_INVALID, "null argument");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(hipMemcpyAsync(dst, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToDevice, s->ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
+  if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
+  double sc[SC_COUNT];
+  int rc = ipmz_qp_scalars(s, sc);
+  if (rc) return rc;
+  int it = 0;
+  for (; it < max_iter; ++it) {  // Optimizer.cpp:127-135
+    double* row = trace ? trace + 8 * (int64_t)it : nullptr;
+    if (row) {
+      row[0] = sc[SC_F];
+      row[1] = sc[SC_RES];
+      row[2] = sc[SC_MU];
+      row[7] = sc[SC_CONVERGED];
+      row[3] = row[4] = row[5] = row[6] = 0.0;
+    }
+    if (sc[SC_CONVERGED] != 0.0) break;
+    rc = ipmz_qp_step(s, 0);
+    if (rc) return rc;
+    rc = ipmz_qp_scalars(s, sc);
+    if (rc) return rc;
+    if (row) {
+      row[3] = sc[SC_ALPHA_AFF];
+      row[4] = sc[SC_MU_AFF];
+      row[5] = sc[SC_SIGMA];
+      row[6] = sc[SC_ALPHA];
+    }
+  }
+  if (iterations) *iterations = it;
+  return IPMZ_OK;
+}
+
+int64_t ipmz_qp_state_len(ipmz_qp* s) { return s ? s->state_len : 0; }
+
+int ipmz_qp_get_state(ipmz_qp* s, int which, double* out) {
+  if (!s || !out || which < 0 || which > 3) return fail(IPMZ_ERR_INVALID, "bad arguments");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  const double* src = which == 0 ? s->q.v[0] : which == 1 ? s->q.daff[0] : which == 2 ? s->q.dir[0] : s->q.r[0];
+  HIP_OK(hipMemcpyAsync(out, src, s->state_len * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_set_state(ipmz_qp* s, const double* in) {
+  if (!s || !in) return fail(IPMZ_ERR_INVALID, "bad arguments");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(hipMemcpyAsync(s->q.v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  HIP_OK(qp_evaluate(s->q, s->ctx->stream));
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  s->loaded = true;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_kkt_dim(ipmz_qp* s) { return s ? s->N : 0; }
+
+int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
+  if (!s || !out) return fail(IPMZ_ERR_INVALID, "bad arguments");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  HIP_OK(qp_assemble(s->q, s->K, s->ldk, st));
+  HIP_OK(hipMemcpy2DAsync(out, (size_t)s->N * 8, s->K, s->ldk * 8, (size_t)s->N * 8, s->N, hipMemcpyDeviceToHost,
+                          st));
+  HIP_OK(hipStreamSynchronize(st));
+  for (int i = 0; i < s->N; ++i)
+    for (int j = i + 1; j < s->N; ++j) out[(int64_t)i * s->N + j] = 0.0;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_set_timing(ipmz_qp* s, int enable) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  s->timing = enable != 0;
+  if (s->timing && s->ev.empty()) {
+    s->ev.resize(8);
+    for (auto& e : s->ev) HIP_OK(hipEventCreate(&e));
+    s->tr_cap = (s->N + 63) / 64 + 8;
+    s->tr_pairs = new hipEvent_t[s->tr_cap][2];
+    for (int i = 0; i < s->tr_cap; ++i) {
+      HIP_OK(hipEventCreate(&s->tr_pairs[i][0]));
+      HIP_OK(hipEventCreate(&s->tr_pairs[i][1]));
+    }
+  }
+  for (double& x : s->ph_ms) x = 0.0;
+  s->tr_flops = 0.0;
+  s->tr_launches = 0;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_phase_times(ipmz_qp* s, double* ms, double* flops, int64_t* launches) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  if (ms)
+    for (int i = 0; i < IPMZ_PH_COUNT; ++i) ms[i] = s->ph_ms[i];
+  if (flops) *flops = s->tr_flops;
+  if (launches) *launches = s->tr_launches;
+  return IPMZ_OK;
+}
+
+}  // extern "C"

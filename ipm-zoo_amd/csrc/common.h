@@ -1,0 +1,54 @@
+// Shared definitions for the gfx950 (MI355X, CDNA4) kernels of libipmz.
+//
+// Storage conventions (DESIGN.md "Data layout in HBM"):
+//   * dense matrices are row-major with a leading dimension `ld` (elements);
+//   * the KKT matrix K is symmetric and only its LOWER triangle (i >= j) is
+//     read; the LDL^T factor overwrites the strict lower triangle with L
+//     (unit diagonal implicit) and writes D to a separate vector.  Row-major
+//     lower == column-major upper, so the reference's row-major Matrix
+//     (LinearSolvers.cpp:14-42) maps onto it by a plain copy.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define IPMZ_HOST_DEVICE __host__ __device__ __forceinline__
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// hipcc builds this library with -ffp-contract=off: element-wise Newton
+// formulas then round exactly like the reference evaluator
+// (Evaluation.cpp:202-257); the dense kernels use explicit fma / MFMA.
+
+// Evaluation.cpp:267-271 -- element-wise reciprocal, 0 -> sqrt(DBL_MAX).
+IPMZ_HOST_DEVICE double ipmz_inv(double x) {
+  return x == 0.0 ? 1.3407807929942596e+154 : 1.0 / x;
+}
+
+// Counter-based splitmix64 generator, identical to
+// oracle/ipmz_oracle.cpp so GPU-generated inputs match the oracle bitwise.
+IPMZ_HOST_DEVICE uint64_t ipmz_splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ULL;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+  return z ^ (z >> 31);
+}
+IPMZ_HOST_DEVICE double ipmz_u01(uint64_t seed, uint64_t tag, uint64_t i, uint64_t j) {
+  const uint64_t key = seed ^ (tag << 56) ^ ((i << 32) + j);
+  return (double)(ipmz_splitmix64(key) >> 11) * 0x1.0p-53;
+}
+
+__device__ __forceinline__ double4_t mfma_f64_16x16x4(double a, double b, double4_t c) {
+  return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
+
+// Wave-level reductions (wave64).
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ double wave_min(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
+  return v;
+}

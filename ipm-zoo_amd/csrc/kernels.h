@@ -1,0 +1,87 @@
+// Host-side launchers of the gfx950 kernels (internal to libipmz).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define IPMZ_NBO_MAX 512
+
+namespace ipmz {
+
+// ldlt.hip -------------------------------------------------------------------
+// In-place blocked LDL^T of the lower triangle of K (row-major, ld).
+// Linv: (ceil(N/nbi)) blocks of nbi x nbi (inverse unit-lower diagonal
+// blocks, consumed by ldlt_solve); W: N x nbo workspace.  info: device int,
+// preset to INT_MAX-ish; receives min(1-based index of a non-finite pivot).
+struct TrailTimer {  // HIP-event pairs around every trailing-update launch
+  hipEvent_t (*pairs)[2] = nullptr;
+  int cap = 0, used = 0;
+  double flops = 0.0;
+  hipEvent_t* next() { return used < cap ? pairs[used++] : nullptr; }
+};
+hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
+                       int* info, hipStream_t st, TrailTimer* timer = nullptr);
+hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
+hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
+                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st);
+hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
+                         double* C, int64_t ldc, hipStream_t st);
+
+// trsv.hip -------------------------------------------------------------------
+// In-place b <- L^{-T} D^{-1} L^{-1} b; side: 2*nbi doubles of scratch.
+hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,
+                      double* side, hipStream_t st);
+
+// newton.hip -----------------------------------------------------------------
+enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
+
+// device scalar block
+enum Scalar {
+  SC_F = 0,
+  SC_RES,
+  SC_MU,
+  SC_ALPHA_AFF,
+  SC_MU_AFF,
+  SC_SIGMA,
+  SC_ALPHA,
+  SC_CONVERGED,
+  SC_MU_NEW,
+  SC_RESTARTS,
+  SC_COUNT = 16
+};
+
+struct QPDev {
+  int n, m, p;
+  int N;
+  int64_t ldn;  // leading dimension of Q, A, C (multiple of 8)
+  double delta;
+  // problem data (row-major, ld = ldn)
+  const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;
+  double* v[NSLOT];
+  double* r[NSLOT];
+  double* daff[NSLOT];
+  double* dir[NSLOT];
+  double *Qx, *ATl, *CTl, *Ax, *Cx;
+  double* b;      // augmented rhs / solution, length N
+  double* scal;   // SC_COUNT doubles
+  double* part;   // reduction partials
+  double* tpart;  // transposed-GEMV partials
+};
+
+hipError_t qp_generate(int n, int m, int p, int64_t ld, uint64_t seed, double* Q, double* c, double* A, double* lA,
+                       double* uA, double* C, double* d, double* lx, double* ux, hipStream_t st);
+hipError_t qp_init_iterate(const QPDev& q, hipStream_t st);
+// residual vectors of the current iterate at mu = 0, plus f, res, mu,
+// converged into scal (the head of Optimizer.cpp:127-135)
+hipError_t qp_evaluate(const QPDev& q, hipStream_t st);
+hipError_t qp_assemble(const QPDev& q, double* K, int64_t ld, hipStream_t st);
+// predictor / corrector pieces
+hipError_t qp_rhs(const QPDev& q, hipStream_t st);
+hipError_t qp_backsub(const QPDev& q, double* const* dslots, hipStream_t st);
+hipError_t qp_ratio(const QPDev& q, double* const* dslots, int out_index, hipStream_t st);
+hipError_t qp_mu_aff(const QPDev& q, hipStream_t st);
+hipError_t qp_corrector_residuals(const QPDev& q, hipStream_t st);
+hipError_t qp_update(const QPDev& q, hipStream_t st);
+hipError_t qp_restart_if_converged(const QPDev& q, const double* saved_v, const double* saved_r,
+                                   const double* saved_scal, int64_t state_len, hipStream_t st);
+
+}  // namespace ipmz

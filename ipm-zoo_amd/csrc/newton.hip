@@ -1,0 +1,577 @@
+// Newton-step kernels around the factorization: synthetic QP generation,
+// build_environment's initial iterate, residual (shorthand) vectors,
+// KKT assembly, augmented rhs, eliminated-variable back-substitution, ratio
+// tests, mu / sigma, corrector residuals and the iterate update.
+//
+// Formulation: InequalityHandling::SlackedSlacks, variable bounds Both,
+// optional EqualityHandling::Regularization (tests/golden/formulations.txt
+// is the reference's own symbolic output these formulas restate).  The
+// element-wise formulas keep the reference evaluator's operand order
+// (Evaluation.cpp:102-176) and the library is built with -ffp-contract=off,
+// so they round exactly like oracle/ipmz_oracle.cpp; only the reductions
+// (matvecs, norms, means) and the factor/solve change summation order.
+//
+// Everything here is HBM-bound O(n^2) (matvecs, assembly) or O(N) work.
+#include "common.h"
+#include "kernels.h"
+
+namespace ipmz {
+
+namespace {
+constexpr int NT = 256;
+constexpr int RED_BLOCKS = 512;  // partial-reduction grid
+enum : uint64_t { TAG_Q = 1, TAG_C = 2, TAG_A = 3, TAG_C_EQ = 4, TAG_D = 5 };
+
+__device__ __forceinline__ double block_sum(double v, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < NT / 64; ++w) t += sh[w];
+  return t;  // valid in thread 0
+}
+__device__ __forceinline__ double block_min(double v, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_min(v);
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 1.0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < NT / 64; ++w) t = fmin(t, sh[w]);
+  return t;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Generator, bit-identical to the oracle's generator.  Matrices are
+// written row-major with leading dimension n.
+__global__ void k_gen_Q(int n, int64_t ld, uint64_t seed, double* Q) {
+  const int64_t total = (int64_t)n * n;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int64_t i = t / n, j = t % n;
+    double v;
+    if (i == j) v = 1.0 + ipmz_u01(seed, TAG_Q, i, i);
+    else if (j < i) v = (2.0 * ipmz_u01(seed, TAG_Q, i, j) - 1.0) / (double)n;
+    else v = (2.0 * ipmz_u01(seed, TAG_Q, j, i) - 1.0) / (double)n;
+    Q[i * ld + j] = v;
+  }
+}
+__global__ void k_gen_rect(int rows, int n, int64_t ld, uint64_t seed, uint64_t tag, double* M) {
+  const int64_t total = (int64_t)rows * n;
+  const double sn = sqrt((double)n);
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
+    const int64_t i = t / n, j = t % n;
+    M[i * ld + j] = (2.0 * ipmz_u01(seed, tag, i, j) - 1.0) / sn;
+  }
+}
+__global__ void k_gen_vec(int n, int m, int p, uint64_t seed, double* c, double* lA, double* uA, double* d,
+                          double* lx, double* ux) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  if (t < n) {
+    c[t] = 2.0 * ipmz_u01(seed, TAG_C, t, 0) - 1.0;
+    lx[t] = -1.0;
+    ux[t] = 1.0;
+  }
+  if (t < m) {
+    lA[t] = -1.0;
+    uA[t] = 1.0;
+  }
+  if (t < p) d[t] = (2.0 * ipmz_u01(seed, TAG_D, t, 0) - 1.0) * 0.1;
+}
+
+hipError_t qp_generate(int n, int m, int p, int64_t ld, uint64_t seed, double* Q, double* c, double* A, double* lA,
+                       double* uA, double* C, double* d, double* lx, double* ux, hipStream_t st) {
+  hipLaunchKernelGGL(k_gen_Q, dim3(2048), dim3(NT), 0, st, n, ld, seed, Q);
+  if (m) hipLaunchKernelGGL(k_gen_rect, dim3(1024), dim3(NT), 0, st, m, n, ld, seed, (uint64_t)TAG_A, A);
+  if (p) hipLaunchKernelGGL(k_gen_rect, dim3(1024), dim3(NT), 0, st, p, n, ld, seed, (uint64_t)TAG_C_EQ, C);
+  const int mx = n > m ? (n > p ? n : p) : (m > p ? m : p);
+  hipLaunchKernelGGL(k_gen_vec, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, n, m, p, seed, c, lA, uA, d, lx, ux);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// build_environment (EnvironmentBuilder.cpp:34-73): x = (l+u)/2, s = (l_A+u_A)/2,
+// every other slack and dual 1.
+__global__ void k_init_iterate(QPDev q) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  if (t < q.n) {
+    q.v[X][t] = 0.5 * (q.lx[t] + q.ux[t]);
+    q.v[LY][t] = 1.0;
+    q.v[LZ][t] = 1.0;
+    q.v[Y][t] = 1.0;
+    q.v[Z][t] = 1.0;
+  }
+  if (t < q.m) {
+    q.v[S][t] = 0.5 * (q.lA[t] + q.uA[t]);
+    q.v[LA][t] = 1.0;
+    q.v[LG][t] = 1.0;
+    q.v[LH][t] = 1.0;
+    q.v[G][t] = 1.0;
+    q.v[H][t] = 1.0;
+  }
+  if (t < q.p) {
+    q.v[LC][t] = 1.0;
+    q.v[P][t] = 1.0;
+  }
+}
+
+static inline int max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
+
+hipError_t qp_init_iterate(const QPDev& q, hipStream_t st) {
+  const int mx = max3(q.n, q.m, q.p);
+  hipLaunchKernelGGL(k_init_iterate, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, q);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Dense matvecs (Evaluation.cpp:35-41 and the materialised transpose at
+// :126-140): out[i] = M[i,:] . x, one wave per row, 16-byte loads.
+__global__ __launch_bounds__(NT) void k_matvec_rows(const double* __restrict__ M, int rows, int cols, int64_t ld,
+                                                    const double* __restrict__ x, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const double* r = M + (int64_t)row * ld;
+  double s0 = 0.0, s1 = 0.0;
+  int j = lane * 2;
+  for (; j + 1 < cols; j += 128) {
+    const double2 a = *reinterpret_cast<const double2*>(r + j);
+    const double2 b = *reinterpret_cast<const double2*>(x + j);
+    s0 += a.x * b.x;
+    s1 += a.y * b.y;
+  }
+  if (j < cols) s0 += r[j] * x[j];
+  const double s = wave_sum(s0 + s1);
+  if (lane == 0) out[row] = s;
+}
+
+// out[j] = sum_i M[i][j] y[i]: column blocks of NT x row chunks of 128,
+// deterministic two-pass (chunk partials, then an ordered sum).
+constexpr int TCHUNK = 128;
+__global__ __launch_bounds__(NT) void k_matvec_t_part(const double* __restrict__ M, int rows, int cols, int64_t ld,
+                                                      const double* __restrict__ y, double* __restrict__ part) {
+  const int j = blockIdx.x * NT + threadIdx.x;
+  const int i0 = blockIdx.y * TCHUNK;
+  if (j >= cols) return;
+  const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
+  double s = 0.0;
+  for (int i = i0; i < i1; ++i) s += M[(int64_t)i * ld + j] * y[i];
+  part[(int64_t)blockIdx.y * cols + j] = s;
+}
+__global__ void k_sum_chunks(const double* __restrict__ part, int nchunk, int cols, double* __restrict__ out) {
+  const int j = blockIdx.x * NT + threadIdx.x;
+  if (j >= cols) return;
+  double s = 0.0;
+  for (int c = 0; c < nchunk; ++c) s += part[(int64_t)c * cols + j];
+  out[j] = s;
+}
+
+static hipError_t matvec_t(const double* M, int rows, int cols, int64_t ld, const double* y, double* out,
+                           double* tpart, hipStream_t st) {
+  const int nchunk = (rows + TCHUNK - 1) / TCHUNK;
+  hipLaunchKernelGGL(k_matvec_t_part, dim3((cols + NT - 1) / NT, nchunk), dim3(NT), 0, st, M, rows, cols, ld, y,
+                     tpart);
+  hipLaunchKernelGGL(k_sum_chunks, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, tpart, nchunk, cols, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Shorthand residuals r_v := -rhs_v at mu (SymbolicOptimization.cpp:480-492),
+// plus per-block partials of ||rhs||^2, sum |complementarity|, and the two
+// objective sums (Optimizer.cpp:128-130).
+__global__ __launch_bounds__(NT) void k_residuals(QPDev q, double mu, int with_stats) {
+  __shared__ double sh[NT / 64];
+  double res2 = 0.0, comp = 0.0, fa = 0.0, fb = 0.0;
+  const int n = q.n, m = q.m, p = q.p;
+  const int total = n + m + p;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
+    if (t < n) {
+      const int i = t;
+      double s = q.c[i] + q.v[LZ][i];
+      s = s + q.Qx[i];
+      if (m) s = s + q.ATl[i];
+      if (p) s = s + q.CTl[i];
+      const double rx = s + (-q.v[LY][i]);
+      const double rly = (q.lx[i] + q.v[Y][i]) + (-q.v[X][i]);
+      const double rlz = (q.v[X][i] + q.v[Z][i]) + (-q.ux[i]);
+      const double ry = q.v[Y][i] * q.v[LY][i] + (-(mu * 1.0));
+      const double rz = q.v[Z][i] * q.v[LZ][i] + (-(mu * 1.0));
+      q.r[X][i] = rx;
+      q.r[LY][i] = rly;
+      q.r[LZ][i] = rlz;
+      q.r[Y][i] = ry;
+      q.r[Z][i] = rz;
+      res2 += rx * rx + rly * rly + rlz * rlz + ry * ry + rz * rz;
+      comp += fabs(ry) + fabs(rz);
+      fa += (0.5 * q.v[X][i]) * q.Qx[i];
+      fb += q.c[i] * q.v[X][i];
+    } else if (t < n + m) {
+      const int i = t - n;
+      const double rla = q.Ax[i] + (-q.v[S][i]);
+      const double rs = -((q.v[LA][i] + q.v[LG][i]) + (-q.v[LH][i]));
+      const double rlg = (q.lA[i] + q.v[G][i]) + (-q.v[S][i]);
+      const double rlh = (q.v[H][i] + q.v[S][i]) + (-q.uA[i]);
+      const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));
+      const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
+      q.r[LA][i] = rla;
+      q.r[S][i] = rs;
+      q.r[LG][i] = rlg;
+      q.r[LH][i] = rlh;
+      q.r[G][i] = rg;
+      q.r[H][i] = rh;
+      res2 += rla * rla + rs * rs + rlg * rlg + rlh * rlh + rg * rg + rh * rh;
+      comp += fabs(rg) + fabs(rh);
+    } else {
+      const int i = t - n - m;
+      const double rlc = (q.Cx[i] + q.delta * q.v[P][i]) + (-q.d[i]);
+      const double rp = q.v[P][i] + q.delta * q.v[LC][i];
+      q.r[LC][i] = rlc;
+      q.r[P][i] = rp;
+      res2 += rlc * rlc + rp * rp;
+    }
+  }
+  if (!with_stats) return;
+  double a = block_sum(res2, sh);
+  if (threadIdx.x == 0) q.part[4 * blockIdx.x + 0] = a;
+  a = block_sum(comp, sh);
+  if (threadIdx.x == 0) q.part[4 * blockIdx.x + 1] = a;
+  a = block_sum(fa, sh);
+  if (threadIdx.x == 0) q.part[4 * blockIdx.x + 2] = a;
+  a = block_sum(fb, sh);
+  if (threadIdx.x == 0) q.part[4 * blockIdx.x + 3] = a;
+}
+
+__global__ void k_stats_final(QPDev q, int nblocks) {
+  __shared__ double sh[4][NT];
+  double s[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int b = threadIdx.x; b < nblocks; b += NT)
+    for (int k = 0; k < 4; ++k) s[k] += q.part[4 * b + k];
+  for (int k = 0; k < 4; ++k) sh[k][threadIdx.x] = s[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int i = 0; i < NT; ++i)
+      for (int k = 0; k < 4; ++k) t[k] += sh[k][i];
+    const double res = sqrt(t[0]);
+    const int cnt = 2 * q.n + 2 * q.m;
+    const double mu = cnt == 0 ? 0.0 : t[1] / (double)cnt;
+    q.scal[SC_F] = t[2] + t[3];
+    q.scal[SC_RES] = res;
+    q.scal[SC_MU] = mu;
+    q.scal[SC_CONVERGED] = (res < 1e-8 && mu < 1e-8) ? 1.0 : 0.0;  // Optimizer.cpp:124,133
+  }
+}
+
+static int red_blocks(int total) {
+  int b = (total + NT - 1) / NT;
+  return b < 1 ? 1 : (b > RED_BLOCKS ? RED_BLOCKS : b);
+}
+
+hipError_t qp_evaluate(const QPDev& q, hipStream_t st) {
+  const int64_t ld = q.ldn;
+  hipLaunchKernelGGL(k_matvec_rows, dim3((q.n + 3) / 4), dim3(NT), 0, st, q.Q, q.n, q.n, ld, q.v[X], q.Qx);
+  if (q.m) {
+    hipLaunchKernelGGL(k_matvec_rows, dim3((q.m + 3) / 4), dim3(NT), 0, st, q.A, q.m, q.n, ld, q.v[X], q.Ax);
+    matvec_t(q.A, q.m, q.n, ld, q.v[LA], q.ATl, q.tpart, st);
+  }
+  if (q.p) {
+    hipLaunchKernelGGL(k_matvec_rows, dim3((q.p + 3) / 4), dim3(NT), 0, st, q.C, q.p, q.n, ld, q.v[X], q.Cx);
+    matvec_t(q.C, q.p, q.n, ld, q.v[LC], q.CTl, q.tpart, st);
+  }
+  const int nb = red_blocks(q.n + q.m + q.p);
+  hipLaunchKernelGGL(k_residuals, dim3(nb), dim3(NT), 0, st, q, 0.0, 1);
+  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(NT), 0, st, q, nb);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Augmented KKT (get_as_matrix_, Optimizer.cpp:387-391, 441-501): lower
+// triangle only, row-major ld.  One workgroup per row, coalesced stores.
+__device__ __forceinline__ double ds_inv(const QPDev& q, int i) {
+  return ipmz_inv(ipmz_inv(q.v[G][i]) * q.v[LG][i] + ipmz_inv(q.v[H][i]) * q.v[LH][i]);
+}
+
+__global__ __launch_bounds__(NT) void k_assemble(QPDev q, double* __restrict__ K, int64_t ld) {
+  const int i = blockIdx.x;
+  const int n = q.n, m = q.m;
+  double* Kr = K + (int64_t)i * ld;
+  if (i < n) {
+    const double* Qr = q.Q + (int64_t)i * q.ldn;
+    for (int j = threadIdx.x; j < i; j += NT) Kr[j] = Qr[j];
+    if (threadIdx.x == 0) {
+      const double h = Qr[i] + ipmz_inv(q.v[Y][i]) * q.v[LY][i];
+      Kr[i] = h + ipmz_inv(q.v[Z][i]) * q.v[LZ][i];
+    }
+  } else if (i < n + m) {
+    const int r = i - n;
+    const double* Ar = q.A + (int64_t)r * q.ldn;
+    for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Ar[j];
+    for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
+    if (threadIdx.x == 0) Kr[i] = -ds_inv(q, r);
+  } else {
+    const int r = i - n - m;
+    const double* Cr = q.C + (int64_t)r * q.ldn;
+    for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Cr[j];
+    for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
+    if (threadIdx.x == 0) Kr[i] = -(q.delta * q.delta);
+  }
+}
+
+hipError_t qp_assemble(const QPDev& q, double* K, int64_t ld, hipStream_t st) {
+  hipLaunchKernelGGL(k_assemble, dim3(q.N), dim3(NT), 0, st, q, K, ld);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Augmented rhs (formulations.txt, augmented system rhs rows 0..2).
+__global__ void k_rhs(QPDev q) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  const int n = q.n, m = q.m;
+  if (t < n) {
+    const int i = t;
+    const double tz = ipmz_inv(q.v[Z][i]) * (q.r[Z][i] + (-(q.v[LZ][i] * q.r[LZ][i])));
+    const double ty = ipmz_inv(q.v[Y][i]) * (q.r[Y][i] + (-(q.v[LY][i] * q.r[LY][i])));
+    q.b[i] = (tz + (-q.r[X][i])) + (-ty);
+  } else if (t < n + m) {
+    const int i = t - n;
+    const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
+    const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
+    q.b[t] = ds_inv(q, i) * ((th + (-q.r[S][i])) + (-tg)) + (-q.r[LA][i]);
+  } else if (t < q.N) {
+    const int i = t - n - m;
+    q.b[t] = q.delta * q.r[P][i] + (-q.r[LC][i]);
+  }
+}
+
+hipError_t qp_rhs(const QPDev& q, hipStream_t st) {
+  hipLaunchKernelGGL(k_rhs, dim3((q.N + NT - 1) / NT), dim3(NT), 0, st, q);
+  return hipGetLastError();
+}
+
+// Back-substitution of the eliminated variables (delta_definitions,
+// Optimizer.cpp:373-378).  dslots: the 13 output vectors.
+struct DSlots {
+  double* d[NSLOT];
+};
+__global__ void k_backsub(QPDev q, DSlots D) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  const int n = q.n, m = q.m;
+  if (t < n) {
+    const int i = t;
+    const double dx = q.b[i];
+    D.d[X][i] = dx;
+    D.d[LY][i] = -((ipmz_inv(q.v[Y][i]) * q.v[LY][i]) *
+                   ((dx + ipmz_inv(q.v[LY][i]) * q.r[Y][i]) + (-q.r[LY][i])));
+    D.d[LZ][i] = -((ipmz_inv(q.v[Z][i]) * q.v[LZ][i]) *
+                   ((ipmz_inv(q.v[LZ][i]) * q.r[Z][i] + (-q.r[LZ][i])) + (-dx)));
+    D.d[Y][i] = -(ipmz_inv(q.v[LY][i]) * (q.r[Y][i] + q.v[Y][i] * D.d[LY][i]));
+    D.d[Z][i] = -(ipmz_inv(q.v[LZ][i]) * (q.r[Z][i] + q.v[Z][i] * D.d[LZ][i]));
+  } else if (t < n + m) {
+    const int i = t - n;
+    const double dla = q.b[t];
+    D.d[LA][i] = dla;
+    const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
+    const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
+    const double ds = ds_inv(q, i) * (((dla + th) + (-q.r[S][i])) + (-tg));
+    D.d[S][i] = ds;
+    const double dlg =
+        -((ipmz_inv(q.v[G][i]) * q.v[LG][i]) * ((ds + ipmz_inv(q.v[LG][i]) * q.r[G][i]) + (-q.r[LG][i])));
+    const double dlh =
+        -((ipmz_inv(q.v[H][i]) * q.v[LH][i]) * ((ipmz_inv(q.v[LH][i]) * q.r[H][i] + (-q.r[LH][i])) + (-ds)));
+    D.d[LG][i] = dlg;
+    D.d[LH][i] = dlh;
+    D.d[G][i] = -(ipmz_inv(q.v[LG][i]) * (q.r[G][i] + q.v[G][i] * dlg));
+    D.d[H][i] = -(ipmz_inv(q.v[LH][i]) * (q.r[H][i] + q.v[H][i] * dlh));
+  } else if (t < q.N) {
+    const int i = t - n - m;
+    const double dlc = q.b[t];
+    D.d[LC][i] = dlc;
+    D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
+  }
+}
+
+hipError_t qp_backsub(const QPDev& q, double* const* dslots, hipStream_t st) {
+  DSlots D;
+  for (int s = 0; s < NSLOT; ++s) D.d[s] = dslots[s];
+  hipLaunchKernelGGL(k_backsub, dim3((q.N + NT - 1) / NT), dim3(NT), 0, st, q, D);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// get_max_step_ (Optimizer.cpp:270-342): fraction-to-boundary over the
+// non-negative Newton variables, plus explicit x bounds when neither g nor h
+// is a Newton variable (m == 0).
+__global__ __launch_bounds__(NT) void k_ratio_part(QPDev q, DSlots D) {
+  __shared__ double sh[NT / 64];
+  double a = 1.0;
+  const int n = q.n, m = q.m;
+  const int total = n + m;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
+    if (t < n) {
+      const int i = t;
+      const int sl[4] = {LY, LZ, Y, Z};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double d = D.d[sl[k]][i];
+        if (d < 0.0) a = fmin(a, -q.v[sl[k]][i] / d);
+      }
+      if (m == 0) {
+        const double d = D.d[X][i], v = q.v[X][i];
+        if (d < 0.0) a = fmin(a, (q.lx[i] - v) / d);
+        if (d > 0.0) a = fmin(a, (q.ux[i] - v) / d);
+      }
+    } else {
+      const int i = t - n;
+      const int sl[4] = {LG, LH, G, H};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double d = D.d[sl[k]][i];
+        if (d < 0.0) a = fmin(a, -q.v[sl[k]][i] / d);
+      }
+    }
+  }
+  a = block_min(a, sh);
+  if (threadIdx.x == 0) q.part[blockIdx.x] = a;
+}
+__global__ void k_min_final(QPDev q, int nblocks, int out_index) {
+  __shared__ double sh[NT / 64];
+  double a = 1.0;
+  for (int b = threadIdx.x; b < nblocks; b += NT) a = fmin(a, q.part[b]);
+  a = block_min(a, sh);
+  if (threadIdx.x == 0) q.scal[out_index] = a;
+}
+
+hipError_t qp_ratio(const QPDev& q, double* const* dslots, int out_index, hipStream_t st) {
+  DSlots D;
+  for (int s = 0; s < NSLOT; ++s) D.d[s] = dslots[s];
+  const int nb = red_blocks(q.n + q.m);
+  hipLaunchKernelGGL(k_ratio_part, dim3(nb), dim3(NT), 0, st, q, D);
+  hipLaunchKernelGGL(k_min_final, dim3(1), dim3(NT), 0, st, q, nb, out_index);
+  return hipGetLastError();
+}
+
+// mu at the affine trial point v + alpha_aff * daff (Optimizer.cpp:167-180).
+__global__ __launch_bounds__(NT) void k_mu_aff_part(QPDev q) {
+  __shared__ double sh[NT / 64];
+  const double al = q.scal[SC_ALPHA_AFF];
+  double s = 0.0;
+  const int n = q.n, m = q.m;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < n + m; t += gridDim.x * NT) {
+    int c0, d0, c1, d1, i;
+    if (t < n) {
+      i = t;
+      c0 = Y; d0 = LY; c1 = Z; d1 = LZ;
+    } else {
+      i = t - n;
+      c0 = G; d0 = LG; c1 = H; d1 = LH;
+    }
+    const double a0 = q.v[c0][i] + al * q.daff[c0][i], b0 = q.v[d0][i] + al * q.daff[d0][i];
+    const double a1 = q.v[c1][i] + al * q.daff[c1][i], b1 = q.v[d1][i] + al * q.daff[d1][i];
+    s += fabs(-(a0 * b0 + (-(0.0 * 1.0)))) + fabs(-(a1 * b1 + (-(0.0 * 1.0))));
+  }
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) q.part[blockIdx.x] = s;
+}
+__global__ void k_mu_aff_final(QPDev q, int nblocks) {
+  __shared__ double sh[NT / 64];
+  double s = 0.0;
+  for (int b = threadIdx.x; b < nblocks; b += NT) s += q.part[b];
+  s = block_sum(s, sh);
+  if (threadIdx.x == 0) {
+    const int cnt = 2 * q.n + 2 * q.m;
+    const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
+    const double mu = q.scal[SC_MU];
+    const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
+    q.scal[SC_MU_AFF] = mu_aff;
+    q.scal[SC_SIGMA] = sigma;
+    q.scal[SC_MU_NEW] = mu * sigma;
+  }
+}
+
+hipError_t qp_mu_aff(const QPDev& q, hipStream_t st) {
+  const int nb = red_blocks(q.n + q.m);
+  hipLaunchKernelGGL(k_mu_aff_part, dim3(nb), dim3(NT), 0, st, q);
+  hipLaunchKernelGGL(k_mu_aff_final, dim3(1), dim3(NT), 0, st, q, nb);
+  return hipGetLastError();
+}
+
+// Corrector (Optimizer.cpp:183-209): r_v = (V lambda - mu_new e) + dV_aff dlambda_aff.
+__global__ void k_corrector(QPDev q) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  const double mu = q.scal[SC_MU_NEW];
+  const int n = q.n, m = q.m;
+  int c0, d0, c1, d1, i;
+  if (t < n) {
+    i = t;
+    c0 = Y; d0 = LY; c1 = Z; d1 = LZ;
+  } else if (t < n + m) {
+    i = t - n;
+    c0 = G; d0 = LG; c1 = H; d1 = LH;
+  } else {
+    return;
+  }
+  q.r[c0][i] = (q.v[c0][i] * q.v[d0][i] + (-(mu * 1.0))) + (q.daff[c0][i] * q.daff[d0][i] + (-(0.0 * 1.0)));
+  q.r[c1][i] = (q.v[c1][i] * q.v[d1][i] + (-(mu * 1.0))) + (q.daff[c1][i] * q.daff[d1][i] + (-(0.0 * 1.0)));
+}
+
+hipError_t qp_corrector_residuals(const QPDev& q, hipStream_t st) {
+  hipLaunchKernelGGL(k_corrector, dim3((q.n + q.m + NT - 1) / NT), dim3(NT), 0, st, q);
+  return hipGetLastError();
+}
+
+// update_variables_(0.995 * alpha, ...) (Optimizer.cpp:216-231)
+__global__ void k_update(QPDev q) {
+  const int t = blockIdx.x * NT + threadIdx.x;
+  const double s = 0.995 * q.scal[SC_ALPHA];
+  const int n = q.n, m = q.m, p = q.p;
+  if (t < n) {
+    const int sl[5] = {X, LY, LZ, Y, Z};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) q.v[sl[k]][t] = q.v[sl[k]][t] + s * q.dir[sl[k]][t];
+  }
+  if (t < m) {
+    const int sl[6] = {LA, S, LG, LH, G, H};
+#pragma unroll
+    for (int k = 0; k < 6; ++k) q.v[sl[k]][t] = q.v[sl[k]][t] + s * q.dir[sl[k]][t];
+  }
+  if (t < p) {
+    q.v[LC][t] = q.v[LC][t] + s * q.dir[LC][t];
+    q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
+  }
+}
+
+hipError_t qp_update(const QPDev& q, hipStream_t st) {
+  const int mx = max3(q.n, q.m, q.p);
+  hipLaunchKernelGGL(k_update, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, q);
+  return hipGetLastError();
+}
+
+// Benchmark restart: a converged iterate is reset (on device, no host sync)
+// to the saved initial state, so every timed step is a real Newton step.
+__global__ void k_restart_copy(const double* __restrict__ sv, const double* __restrict__ sr, double* v, double* r,
+                               const double* scal, int64_t len) {
+  if (scal[SC_CONVERGED] == 0.0) return;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < len; t += (int64_t)gridDim.x * NT) {
+    v[t] = sv[t];
+    r[t] = sr[t];
+  }
+}
+__global__ void k_restart_scal(const double* __restrict__ ss, double* scal) {
+  if (threadIdx.x != 0 || scal[SC_CONVERGED] == 0.0) return;
+  const double restarts = scal[SC_RESTARTS];
+  for (int k = 0; k < SC_RESTARTS; ++k) scal[k] = ss[k];
+  scal[SC_RESTARTS] = restarts + 1.0;
+}
+
+hipError_t qp_restart_if_converged(const QPDev& q, const double* saved_v, const double* saved_r,
+                                   const double* saved_scal, int64_t state_len, hipStream_t st) {
+  hipLaunchKernelGGL(k_restart_copy, dim3(256), dim3(NT), 0, st, saved_v, saved_r, q.v[0], q.r[0], q.scal, state_len);
+  hipLaunchKernelGGL(k_restart_scal, dim3(1), dim3(64), 0, st, saved_scal, q.scal);
+  return hipGetLastError();
+}
+
+}  // namespace ipmz

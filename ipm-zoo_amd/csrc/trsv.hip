@@ -1,0 +1,215 @@
+// Triangular solves with the LDL^T factor: x = L^{-T} D^{-1} L^{-1} b.
+//
+// Replaces LinearSolvers::overwriting_solve_ldlt (LinearSolvers.cpp:44-74):
+// forward substitution (:56-59), diagonal scaling (:62-64), backward
+// substitution with L^T (:67-73).  Blocked by the factor's inner block size
+// nb; the diagonal-block solves use the L11^{-1} blocks saved by the factor
+// (ldlt.hip), the off-diagonal work is a wave-per-row (forward) or
+// lane-per-column (backward) GEMV over the strict lower triangle.
+//
+// One launch per block step.  Workgroup 0 of step J owns the NEXT diagonal
+// block: it applies step J's update to those rows first and then solves
+// them, so step J+1 finds its block solution ready in the side buffer and no
+// workgroup re-reads an L11^{-1} block redundantly.  The solve runs in place
+// on b (the rows a step writes are never read by a later step).
+#include "common.h"
+#include "kernels.h"
+
+namespace ipmz {
+
+constexpr int TRSV_NT = 256;
+
+// y = Linv . v for one nb-block, Linv row-major nb x nb (unit lower).
+// Reads v[0..bj) from LDS, writes y to LDS.  4 waves, each row a wave dot.
+template <int NB>
+__device__ void block_lower_apply(const double* __restrict__ Linv, const double* vs, double* ys, int bj,
+                                  bool transpose) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int t = wave; t < bj; t += TRSV_NT / 64) {
+    double s = 0.0;
+    for (int c = lane; c < bj; c += 64) {
+      const double l = transpose ? Linv[(int64_t)c * NB + t] : Linv[(int64_t)t * NB + c];
+      s += l * vs[c];
+    }
+    s = wave_sum(s);
+    if (lane == 0) ys[t] = s;
+  }
+}
+
+// prologue: y_0 = Linv_0 b_0; b_0 <- y_0 / D_0; ybuf <- y_0
+template <int NB>
+__global__ __launch_bounds__(TRSV_NT) void trsv_fwd_first(const double* __restrict__ Linv,
+                                                          const double* __restrict__ D, double* __restrict__ b,
+                                                          double* __restrict__ ybuf, int bj) {
+  __shared__ double vs[NB], ys[NB];
+  for (int t = threadIdx.x; t < bj; t += TRSV_NT) vs[t] = b[t];
+  __syncthreads();
+  block_lower_apply<NB>(Linv, vs, ys, bj, false);
+  __syncthreads();
+  for (int t = threadIdx.x; t < bj; t += TRSV_NT) {
+    ybuf[t] = ys[t];
+    b[t] = ys[t] / D[t];
+  }
+}
+
+// forward step J: rows below block J: b_i -= L[i, J] . y_J.  Workgroup 0
+// owns block J+1 (rows [j1, j1+nb)) and solves it afterwards.
+template <int NB>
+__global__ __launch_bounds__(TRSV_NT) void trsv_fwd_step(const double* __restrict__ K, int64_t ld, int N, int j0,
+                                                         const double* __restrict__ LinvNext,
+                                                         const double* __restrict__ D, double* __restrict__ b,
+                                                         const double* __restrict__ yin, double* __restrict__ yout,
+                                                         int rows_per_wg) {
+  __shared__ double ys[NB], vs[NB], yn[NB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int j1 = j0 + NB;
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) ys[t] = yin[t];
+  __syncthreads();
+  int r_begin, r_end;
+  const int bn = N - j1 < NB ? N - j1 : NB;  // size of block J+1
+  if (blockIdx.x == 0) {
+    r_begin = j1;
+    r_end = j1 + bn;
+  } else {
+    r_begin = j1 + bn + (blockIdx.x - 1) * rows_per_wg;
+    r_end = r_begin + rows_per_wg < N ? r_begin + rows_per_wg : N;
+  }
+  // each wave takes a row: NB doubles = NB/64 per lane (coalesced)
+  for (int i = r_begin + wave; i < r_end; i += TRSV_NT / 64) {
+    const double* Lr = K + (int64_t)i * ld + j0;
+    double s = 0.0;
+#pragma unroll
+    for (int q = 0; q < NB / 64; ++q) s += Lr[lane + 64 * q] * ys[lane + 64 * q];
+    s = wave_sum(s);
+    if (lane == 0) {
+      const double v = b[i] - s;
+      b[i] = v;
+      if (blockIdx.x == 0) vs[i - j1] = v;
+    }
+  }
+  if (blockIdx.x != 0) return;
+  __syncthreads();
+  block_lower_apply<NB>(LinvNext, vs, yn, bn, false);
+  __syncthreads();
+  for (int t = threadIdx.x; t < bn; t += TRSV_NT) {
+    yout[t] = yn[t];
+    b[j1 + t] = yn[t] / D[j1 + t];
+  }
+}
+
+// backward prologue: last block: x_L = Linv_L^T z_L
+template <int NB>
+__global__ __launch_bounds__(TRSV_NT) void trsv_bwd_first(const double* __restrict__ Linv, double* __restrict__ b,
+                                                          double* __restrict__ xbuf, int jl, int bj) {
+  __shared__ double vs[NB], xs[NB];
+  for (int t = threadIdx.x; t < bj; t += TRSV_NT) vs[t] = b[jl + t];
+  __syncthreads();
+  block_lower_apply<NB>(Linv, vs, xs, bj, true);
+  __syncthreads();
+  for (int t = threadIdx.x; t < bj; t += TRSV_NT) {
+    xbuf[t] = xs[t];
+    b[jl + t] = xs[t];
+  }
+}
+
+// backward step J (block rows [j0, j0+bj)): z_i -= sum_r L[r][i] x_r for
+// i < j0.  Each workgroup owns 64 columns; its 4 waves split the nb rows and
+// reduce through LDS.  Workgroup 0 owns block J-1 and solves it afterwards.
+template <int NB>
+__global__ __launch_bounds__(TRSV_NT) void trsv_bwd_step(const double* __restrict__ K, int64_t ld, int j0, int bj,
+                                                         const double* __restrict__ LinvPrev,
+                                                         double* __restrict__ b, const double* __restrict__ xin,
+                                                         double* __restrict__ xout) {
+  __shared__ double xs[NB], part[4][NB], vs[NB], xn[NB];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) xs[t] = t < bj ? xin[t] : 0.0;
+  __syncthreads();
+  const int jp = j0 - NB;  // block J-1 start (j0 is a multiple of NB, >= NB)
+  int c_begin, c_end;
+  if (blockIdx.x == 0) {
+    c_begin = jp;
+    c_end = j0;
+  } else {
+    c_begin = (blockIdx.x - 1) * NB;
+    c_end = c_begin + NB;
+  }
+  // NB columns per workgroup: lane handles column c_begin + lane + 64*q
+  constexpr int CQ = NB / 64;
+  double s[CQ];
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) s[q] = 0.0;
+  for (int r = wave; r < bj; r += 4) {
+    const double* Lr = K + (int64_t)(j0 + r) * ld + c_begin;
+    const double xr = xs[r];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) s[q] += Lr[lane + 64 * q] * xr;
+  }
+#pragma unroll
+  for (int q = 0; q < CQ; ++q) part[wave][lane + 64 * q] = s[q];
+  __syncthreads();
+  for (int c = threadIdx.x; c < NB; c += TRSV_NT) {
+    const double t = (part[0][c] + part[1][c]) + (part[2][c] + part[3][c]);
+    const double v = b[c_begin + c] - t;
+    b[c_begin + c] = v;
+    vs[c] = v;
+  }
+  (void)c_end;
+  if (blockIdx.x != 0) return;
+  __syncthreads();
+  block_lower_apply<NB>(LinvPrev, vs, xn, NB, true);
+  __syncthreads();
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
+    xout[t] = xn[t];
+    b[jp + t] = xn[t];
+  }
+}
+
+template <int NB>
+static hipError_t ldlt_solve_nb(const double* K, int64_t ld, int N, const double* D, const double* Linv, double* b,
+                                double* side, hipStream_t st) {
+  const int nblk = (N + NB - 1) / NB;
+  double* y0 = side;       // ping-pong block-solution buffers
+  double* y1 = side + NB;
+  const int64_t LB = (int64_t)NB * NB;
+  const int bj0 = N < NB ? N : NB;
+  hipLaunchKernelGGL((trsv_fwd_first<NB>), dim3(1), dim3(TRSV_NT), 0, st, Linv, D, b, y0, bj0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  const int rows_per_wg = 64;
+  for (int J = 0; J + 1 < nblk; ++J) {
+    const int j0 = J * NB, j1 = j0 + NB;
+    const int bn = N - j1 < NB ? N - j1 : NB;
+    const int rest = N - j1 - bn;
+    const int nwg = 1 + (rest + rows_per_wg - 1) / rows_per_wg;
+    double* yin = (J & 1) ? y1 : y0;
+    double* yout = (J & 1) ? y0 : y1;
+    hipLaunchKernelGGL((trsv_fwd_step<NB>), dim3(nwg), dim3(TRSV_NT), 0, st, K, ld, N, j0, Linv + (J + 1) * LB, D,
+                       b, yin, yout, rows_per_wg);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  // backward
+  const int jl = (nblk - 1) * NB, bl = N - jl;
+  hipLaunchKernelGGL((trsv_bwd_first<NB>), dim3(1), dim3(TRSV_NT), 0, st, Linv + (nblk - 1) * LB, b, y0, jl, bl);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  for (int J = nblk - 1, it = 0; J >= 1; --J, ++it) {
+    const int j0 = J * NB;
+    const int bj = N - j0 < NB ? N - j0 : NB;
+    const int nwg = 1 + (j0 - NB) / NB;
+    double* xin = (it & 1) ? y1 : y0;
+    double* xout = (it & 1) ? y0 : y1;
+    hipLaunchKernelGGL((trsv_bwd_step<NB>), dim3(nwg), dim3(TRSV_NT), 0, st, K, ld, j0, bj, Linv + (J - 1) * LB, b,
+                       xin, xout);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
+hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,
+                      double* side, hipStream_t st) {
+  if (N <= 0) return hipSuccess;
+  if (nbi == 128) return ldlt_solve_nb<128>(K, ld, N, D, Linv, b, side, st);
+  if (nbi == 64) return ldlt_solve_nb<64>(K, ld, N, D, Linv, b, side, st);
+  return hipErrorInvalidValue;
+}
+
+}  // namespace ipmz

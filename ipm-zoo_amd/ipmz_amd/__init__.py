@@ -1,0 +1,321 @@
+"""Python binding of libipmz (the MI355X Newton-step library) over its C ABI
+(include/ipmz.h), via ctypes.
+
+Mirrors the reference's NumericalOptimization interface for the hot path:
+
+    LinearSolvers.ldlt_decomposition(A)        -> (L, D)   LinearSolvers.h:11
+    LinearSolvers.overwriting_solve_ldlt(L, D, b)  (b overwritten)  LinearSolvers.h:16-17
+    Data / build_environment / Optimizer(...).solve()     EnvironmentBuilder.h:7-20,
+                                                           Optimizer.h:15-20
+
+Errors raise AssertionError (a subclass of the reference's
+Utils::AssertionError -> std::logic_error convention, Assert.h:7-12, maps to
+Python's AssertionError/ValueError family here).  There is no CPU fallback:
+loading fails loudly when lib/libipmz.so is missing, and every computing
+call fails when no gfx950 device is visible.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libipmz.so")
+
+IPMZ_OK = 0
+ERR = {-1: "invalid argument", -2: "HIP error", -3: "out of device memory", -4: "no gfx950 device",
+       -5: "bad state"}
+SC = dict(f=0, res=1, mu=2, alpha_aff=3, mu_aff=4, sigma=5, alpha=6, converged=7, mu_new=8, restarts=9)
+SC_COUNT = 16
+PH = dict(step=0, assemble=1, factor=2, solve=3, trailing=4, eval=5)
+STEP_RESTART_IF_CONVERGED = 1
+STEP_GRAPH = 2
+SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"]
+
+EXPORTS = [
+    "ipmz_ctx_create", "ipmz_ctx_destroy", "ipmz_ctx_set_stream", "ipmz_ctx_sync", "ipmz_last_error",
+    "ipmz_ctx_set_blocking", "ipmz_ldlt_workspace_bytes", "ipmz_ldlt_factor", "ipmz_ldlt_solve",
+    "ipmz_ldlt_prepare_solve", "ipmz_ldlt_decomposition", "ipmz_overwriting_solve_ldlt", "ipmz_qp_create",
+    "ipmz_qp_destroy", "ipmz_qp_load_host", "ipmz_qp_generate", "ipmz_qp_step", "ipmz_qp_scalars",
+    "ipmz_qp_device_scalars", "ipmz_qp_copy_scalars", "ipmz_qp_solve", "ipmz_qp_state_len", "ipmz_qp_get_state", "ipmz_qp_set_state",
+    "ipmz_qp_get_kkt", "ipmz_qp_kkt_dim", "ipmz_qp_set_timing", "ipmz_qp_phase_times",
+]
+
+_P = ctypes.POINTER(ctypes.c_double)
+_VP = ctypes.c_void_p
+_I = ctypes.c_int
+_I64 = ctypes.c_int64
+
+
+class IpmzError(AssertionError):
+    """A failed libipmz call (the reference throws Utils::AssertionError)."""
+
+
+class _QPConfig(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_int), ("m", ctypes.c_int), ("p", ctypes.c_int), ("delta", ctypes.c_double)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libipmz not built: {LIB_PATH} missing (run __graft_entry__.build()); "
+                          "there is no CPU fallback")
+    lib = ctypes.CDLL(LIB_PATH)
+    sig = {
+        "ipmz_ctx_create": ([ctypes.POINTER(_VP), _I], _I),
+        "ipmz_ctx_destroy": ([_VP], _I),
+        "ipmz_ctx_set_stream": ([_VP, _VP], _I),
+        "ipmz_ctx_sync": ([_VP], _I),
+        "ipmz_last_error": ([], ctypes.c_char_p),
+        "ipmz_ctx_set_blocking": ([_VP, _I, _I], _I),
+        "ipmz_ldlt_workspace_bytes": ([_VP, _I], _I64),
+        "ipmz_ldlt_factor": ([_VP, _I, _VP, _I64, _VP, _VP, _I64], _I),
+        "ipmz_ldlt_solve": ([_VP, _I, _VP, _I64, _VP, _VP, _VP], _I),
+        "ipmz_ldlt_prepare_solve": ([_VP, _I, _VP, _I64, _VP, _I64], _I),
+        "ipmz_ldlt_decomposition": ([_VP, _I, _P, _P, _P], _I),
+        "ipmz_overwriting_solve_ldlt": ([_VP, _I, _P, _P, _P], _I),
+        "ipmz_qp_create": ([_VP, ctypes.POINTER(_QPConfig), ctypes.POINTER(_VP)], _I),
+        "ipmz_qp_destroy": ([_VP], _I),
+        "ipmz_qp_load_host": ([_VP] + [_P] * 9, _I),
+        "ipmz_qp_generate": ([_VP, ctypes.c_uint64], _I),
+        "ipmz_qp_step": ([_VP, _I], _I),
+        "ipmz_qp_scalars": ([_VP, _P], _I),
+        "ipmz_qp_device_scalars": ([_VP, ctypes.POINTER(_VP)], _I),
+        "ipmz_qp_copy_scalars": ([_VP, _VP], _I),
+        "ipmz_qp_solve": ([_VP, _I, _P, ctypes.POINTER(_I)], _I),
+        "ipmz_qp_state_len": ([_VP], _I64),
+        "ipmz_qp_get_state": ([_VP, _I, _P], _I),
+        "ipmz_qp_set_state": ([_VP, _P], _I),
+        "ipmz_qp_get_kkt": ([_VP, _P], _I),
+        "ipmz_qp_kkt_dim": ([_VP], _I),
+        "ipmz_qp_set_timing": ([_VP, _I], _I),
+        "ipmz_qp_phase_times": ([_VP, _P, _P, ctypes.POINTER(_I64)], _I),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = res
+    return lib
+
+
+lib = _load()
+
+
+def _check(rc, what):
+    if rc < 0:
+        msg = lib.ipmz_last_error().decode(errors="replace")
+        raise IpmzError(f"{what}: {ERR.get(rc, rc)}: {msg}")
+    return rc
+
+
+def _dp(a):
+    return a.ctypes.data_as(_P)
+
+
+class Context:
+    """A device + HIP stream (one per GPU / process)."""
+
+    def __init__(self, device=0, stream=None, nbo=None, nbi=None):
+        h = _VP()
+        _check(lib.ipmz_ctx_create(ctypes.byref(h), device), "ipmz_ctx_create")
+        self.h = h
+        self.device = device
+        if stream is not None:
+            self.set_stream(stream)
+        if nbo or nbi:
+            self.set_blocking(nbo or 256, nbi or 128)
+
+    def set_stream(self, stream):
+        _check(lib.ipmz_ctx_set_stream(self.h, _VP(stream)), "ipmz_ctx_set_stream")
+
+    def set_blocking(self, nbo, nbi):
+        _check(lib.ipmz_ctx_set_blocking(self.h, nbo, nbi), "ipmz_ctx_set_blocking")
+
+    def sync(self):
+        _check(lib.ipmz_ctx_sync(self.h), "ipmz_ctx_sync")
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.ipmz_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- device-memory LinearSolvers (pointers, e.g. torch tensor data_ptr()) --
+    def workspace_bytes(self, N):
+        return lib.ipmz_ldlt_workspace_bytes(self.h, N)
+
+    def ldlt_factor(self, N, K_ptr, ld, D_ptr, ws_ptr, ws_bytes):
+        return _check(lib.ipmz_ldlt_factor(self.h, N, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), ws_bytes),
+                      "ipmz_ldlt_factor")
+
+    def ldlt_solve(self, N, K_ptr, ld, D_ptr, ws_ptr, b_ptr):
+        return _check(lib.ipmz_ldlt_solve(self.h, N, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), _VP(b_ptr)),
+                      "ipmz_ldlt_solve")
+
+
+_default_ctx = None
+
+
+def default_context():
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+class LinearSolvers:
+    """NumericalOptimization::LinearSolvers with the reference's value semantics
+    (LinearSolvers.h:11-17): fresh L and D returned, b overwritten."""
+
+    @staticmethod
+    def ldlt_decomposition(A, ctx=None):
+        A = np.ascontiguousarray(A, dtype=np.float64)
+        if A.ndim != 2 or A.shape[0] != A.shape[1]:
+            raise IpmzError("ldlt_decomposition: matrix must be square")  # LinearSolvers.cpp:16-17
+        N = A.shape[0]
+        L = np.zeros((N, N))
+        D = np.zeros(N)
+        info = _check(lib.ipmz_ldlt_decomposition((ctx or default_context()).h, N, _dp(A), _dp(L), _dp(D)),
+                      "ipmz_ldlt_decomposition")
+        return L, D, info
+
+    @staticmethod
+    def overwriting_solve_ldlt(L, D, b, ctx=None):
+        L = np.ascontiguousarray(L, dtype=np.float64)
+        D = np.ascontiguousarray(D, dtype=np.float64)
+        if not (isinstance(b, np.ndarray) and b.dtype == np.float64 and b.flags.c_contiguous):
+            raise IpmzError("overwriting_solve_ldlt: b must be a contiguous float64 array")
+        N = b.shape[0]
+        if N and (D.shape[0] != N or L.shape != (N, N)):
+            raise IpmzError("overwriting_solve_ldlt: size mismatch")  # LinearSolvers.cpp:50-53
+        _check(lib.ipmz_overwriting_solve_ldlt((ctx or default_context()).h, N, _dp(L), _dp(D), _dp(b)),
+               "ipmz_overwriting_solve_ldlt")
+        return b
+
+
+class Data:
+    """NumericalOptimization::Data (EnvironmentBuilder.h:7-17)."""
+
+    def __init__(self, Q, c, l_x, u_x, A_ineq=None, l_A_ineq=None, u_A_ineq=None, A_eq=None, b_eq=None):
+        self.Q = np.ascontiguousarray(Q, dtype=np.float64)
+        self.c = np.ascontiguousarray(c, dtype=np.float64)
+        self.l_x = np.ascontiguousarray(l_x, dtype=np.float64)
+        self.u_x = np.ascontiguousarray(u_x, dtype=np.float64)
+        n = self.Q.shape[0]
+        self.A_ineq = np.zeros((0, n)) if A_ineq is None else np.ascontiguousarray(A_ineq, dtype=np.float64)
+        self.l_A_ineq = np.zeros(0) if l_A_ineq is None else np.ascontiguousarray(l_A_ineq, dtype=np.float64)
+        self.u_A_ineq = np.zeros(0) if u_A_ineq is None else np.ascontiguousarray(u_A_ineq, dtype=np.float64)
+        self.A_eq = np.zeros((0, n)) if A_eq is None else np.ascontiguousarray(A_eq, dtype=np.float64)
+        self.b_eq = np.zeros(0) if b_eq is None else np.ascontiguousarray(b_eq, dtype=np.float64)
+
+
+class Optimizer:
+    """The Newton-step solver: build_environment + Optimizer (Optimizer.h:15-20).
+
+    Formulation: InequalityHandling::SlackedSlacks with Bounds::Both, and
+    EqualityHandling::Regularization (delta = 1e-4) when equalities exist.
+    """
+
+    def __init__(self, n, m=0, p=0, ctx=None, delta=1e-4):
+        self.ctx = ctx or default_context()
+        cfg = _QPConfig(n, m, p, delta)
+        h = _VP()
+        _check(lib.ipmz_qp_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)), "ipmz_qp_create")
+        self.h = h
+        self.n, self.m, self.p = n, m, p
+        self.N = n + m + p
+        self.state_len = lib.ipmz_qp_state_len(h)
+
+    @classmethod
+    def from_data(cls, data, ctx=None):
+        n, m, p = data.Q.shape[0], data.A_ineq.shape[0], data.A_eq.shape[0]
+        o = cls(n, m, p, ctx)
+        o.load(data)
+        return o
+
+    def load(self, data):
+        keep = [data.Q, data.c, data.A_ineq, data.l_A_ineq, data.u_A_ineq, data.A_eq, data.b_eq, data.l_x, data.u_x]
+        keep = [np.ascontiguousarray(a, dtype=np.float64).reshape(-1) if np.size(a) else np.zeros(1) for a in keep]
+        _check(lib.ipmz_qp_load_host(self.h, *[_dp(a) for a in keep]), "ipmz_qp_load_host (build_environment)")
+
+    def generate(self, seed):
+        _check(lib.ipmz_qp_generate(self.h, seed), "ipmz_qp_generate")
+
+    def step(self, flags=0):
+        _check(lib.ipmz_qp_step(self.h, flags), "ipmz_qp_step")
+
+    def scalars(self):
+        out = np.zeros(SC_COUNT)
+        _check(lib.ipmz_qp_scalars(self.h, _dp(out)), "ipmz_qp_scalars")
+        return {k: out[i] for k, i in SC.items()}
+
+    def device_scalars_ptr(self):
+        p = _VP()
+        _check(lib.ipmz_qp_device_scalars(self.h, ctypes.byref(p)), "ipmz_qp_device_scalars")
+        return p.value
+
+    def copy_scalars(self, dst_ptr):
+        """Async device-to-device copy of the scalar block (ctx stream)."""
+        _check(lib.ipmz_qp_copy_scalars(self.h, _VP(dst_ptr)), "ipmz_qp_copy_scalars")
+
+    def solve(self, max_iter=100):
+        trace = np.zeros((max_iter + 1, 8))
+        it = ctypes.c_int(0)
+        _check(lib.ipmz_qp_solve(self.h, max_iter, _dp(trace), ctypes.byref(it)), "ipmz_qp_solve")
+        rows = min(it.value + 1, max_iter)
+        keys = ("f", "res", "mu", "alpha_aff", "mu_aff", "sigma", "alpha", "converged")
+        return it.value, [dict(zip(keys, r)) for r in trace[:rows]]
+
+    def _state(self, which):
+        out = np.zeros(self.state_len)
+        _check(lib.ipmz_qp_get_state(self.h, which, _dp(out)), "ipmz_qp_get_state")
+        return out
+
+    def vars(self):
+        return self._state(0)
+
+    def daff(self):
+        return self._state(1)
+
+    def dir(self):
+        return self._state(2)
+
+    def residuals(self):
+        return self._state(3)
+
+    def set_vars(self, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        _check(lib.ipmz_qp_set_state(self.h, _dp(v)), "ipmz_qp_set_state")
+
+    def kkt(self):
+        K = np.zeros((self.N, self.N))
+        _check(lib.ipmz_qp_get_kkt(self.h, _dp(K)), "ipmz_qp_get_kkt")
+        return K
+
+    def set_timing(self, on=True):
+        _check(lib.ipmz_qp_set_timing(self.h, 1 if on else 0), "ipmz_qp_set_timing")
+
+    def phase_times(self):
+        ms = np.zeros(8)
+        fl = ctypes.c_double(0)
+        nl = ctypes.c_int64(0)
+        _check(lib.ipmz_qp_phase_times(self.h, _dp(ms), ctypes.byref(fl), ctypes.byref(nl)), "ipmz_qp_phase_times")
+        out = {k: ms[i] for k, i in PH.items()}
+        out["trailing_flops"] = fl.value
+        out["trailing_launches"] = nl.value
+        return out
+
+    def close(self):
+        if getattr(self, "h", None):
+            lib.ipmz_qp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

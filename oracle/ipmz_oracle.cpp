@@ -21,6 +21,7 @@
 // Sum terms are added left to right, a - b is a + (-b) (bit-identical),
 // Product terms are multiplied left to right, X^{-1} is an element-wise
 // reciprocal with 0 -> sqrt(DBL_MAX) (Evaluation.cpp:267-271).
+#include <chrono>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -351,9 +352,15 @@ int iterate(QP& q, double* rec, double* phase_s) {
   rec[7] = (rec[1] < 1e-8 && rec[2] < 1e-8) ? 1.0 : 0.0;
   if (rec[7] != 0.0) return 1;
   Vec K((size_t)(N * N)), L((size_t)(N * N)), Dd(N);
+  const auto t0 = std::chrono::steady_clock::now();
   assemble(q, K.data());
+  const auto t1 = std::chrono::steady_clock::now();
   ldlt(N, K.data(), N, L.data(), N, Dd.data());
-  (void)phase_s;
+  const auto t2 = std::chrono::steady_clock::now();
+  if (phase_s) {
+    phase_s[0] = std::chrono::duration<double>(t1 - t0).count();
+    phase_s[1] = std::chrono::duration<double>(t2 - t1).count();
+  }
   const double mu = rec[2];
   Residuals R;
   residuals(q, 0.0, R);
@@ -376,6 +383,7 @@ int iterate(QP& q, double* rec, double* phase_s) {
   search_direction(q, R, L, Dd, q.dir);
   const double alpha = max_step(q, q.dir);
   axpy_all(q, 0.995 * alpha, q.dir);
+  if (phase_s) phase_s[2] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t2).count();
   rec[3] = a_aff;
   rec[4] = mu_aff;
   rec[5] = sigma;
@@ -458,6 +466,10 @@ void ipmzo_destroy(void* h) { delete static_cast<QP*>(h); }
 int64_t ipmzo_kkt_dim(void* h) { return static_cast<QP*>(h)->N(); }
 
 int ipmzo_iterate(void* h, double* rec) { return iterate(*static_cast<QP*>(h), rec, nullptr); }
+// phase_s = {assemble, ldlt, rest-of-step (rhs, 2 solves, back-substitution,
+// ratio tests, update)} in seconds; the head (objective, residual norm, mu)
+// is included in neither.
+int ipmzo_iterate_timed(void* h, double* rec, double* phase_s) { return iterate(*static_cast<QP*>(h), rec, phase_s); }
 
 // Concatenated vectors in the reference's Newton-variable order.
 int64_t ipmzo_state_len(void* h) {

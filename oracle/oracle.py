@@ -48,6 +48,8 @@ def _load():
     lib.ipmzo_destroy.argtypes = [ctypes.c_void_p]
     lib.ipmzo_iterate.argtypes = [ctypes.c_void_p, _P]
     lib.ipmzo_iterate.restype = ctypes.c_int
+    lib.ipmzo_iterate_timed.argtypes = [ctypes.c_void_p, _P, _P]
+    lib.ipmzo_iterate_timed.restype = ctypes.c_int
     for fn in ("ipmzo_state_len", "ipmzo_kkt_dim"):
         getattr(lib, fn).restype = _i64
         getattr(lib, fn).argtypes = [ctypes.c_void_p]
@@ -132,6 +134,13 @@ class OracleQP:
         conv = lib().ipmzo_iterate(self.h, _dp(rec))
         keys = ("f", "res", "mu", "alpha_aff", "mu_aff", "sigma", "alpha", "converged")
         return conv, dict(zip(keys, rec))
+
+    def iterate_timed(self):
+        """One iteration; returns (converged, record, {assemble, ldlt, rest} seconds)."""
+        rec = np.zeros(8)
+        ph = np.zeros(3)
+        conv = lib().ipmzo_iterate_timed(self.h, _dp(rec), _dp(ph))
+        return conv, rec, dict(assemble=ph[0], ldlt=ph[1], rest=ph[2])
 
     def _get(self, fn):
         out = np.zeros(self.L)
