@@ -77,7 +77,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
     ap.add_argument("--nbo", type=int, default=int(os.environ.get("IPMZ_NBO", 256)))
-    ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 128)))
+    ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 64)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (allows graph replay)")
     args = ap.parse_args()

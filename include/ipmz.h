@@ -93,7 +93,7 @@ int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* hip_stream);
 int ipmz_ctx_sync(ipmz_ctx* ctx);
 const char* ipmz_last_error(void);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512),
- * inner diagonal block nbi (64 or 128).  Defaults 256 / 128. */
+ * inner diagonal block nbi (64 or 128).  Defaults 256 / 64. */
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);
 
 /* ---- LinearSolvers on device memory ------------------------------------ */

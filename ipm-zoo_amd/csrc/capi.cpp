@@ -40,7 +40,7 @@ struct ipmz_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  int nbo = 256, nbi = 128;
+  int nbo = 256, nbi = 64;
 };
 
 static int check_device(int device) {

@@ -41,14 +41,47 @@ __device__ __forceinline__ double4_t mfma_f64_16x16x4(double a, double b, double
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
-// Wave-level reductions (wave64).
+// Wave-level all-reductions (wave64) on the VALU: DPP inside 16-lane rows
+// (xor 1, xor 2, rotate 4, rotate 8), then v_permlane16_swap / 32_swap across
+// rows (gfx950).  No LDS round trips (ds_bpermute-based __shfl_xor costs ~6
+// dependent LDS latencies for a double).
+template <int CTRL>
+__device__ __forceinline__ double dpp_double(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ void swap16(double v, double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
+  a = __hiloint2double(hi[0], lo[0]);
+  b = __hiloint2double(hi[1], lo[1]);
+}
+__device__ __forceinline__ void swap32(double v, double& a, double& b) {
+  const auto lo = __builtin_amdgcn_permlane32_swap(__double2loint(v), __double2loint(v), false, false);
+  const auto hi = __builtin_amdgcn_permlane32_swap(__double2hiint(v), __double2hiint(v), false, false);
+  a = __hiloint2double(hi[0], lo[0]);
+  b = __hiloint2double(hi[1], lo[1]);
+}
 __device__ __forceinline__ double wave_sum(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  v += dpp_double<0xb1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_double<0x4e>(v);   // quad_perm [2,3,0,1]
+  v += dpp_double<0x124>(v);  // row_ror:4
+  v += dpp_double<0x128>(v);  // row_ror:8
+  double a, b;
+  swap16(v, a, b);
+  v = a + b;
+  swap32(v, a, b);
+  return a + b;
 }
 __device__ __forceinline__ double wave_min(double v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, 64));
-  return v;
+  v = fmin(v, dpp_double<0xb1>(v));
+  v = fmin(v, dpp_double<0x4e>(v));
+  v = fmin(v, dpp_double<0x124>(v));
+  v = fmin(v, dpp_double<0x128>(v));
+  double a, b;
+  swap16(v, a, b);
+  v = fmin(a, b);
+  swap32(v, a, b);
+  return fmin(a, b);
 }

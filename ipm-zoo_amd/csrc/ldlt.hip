@@ -24,52 +24,107 @@
 namespace ipmz {
 
 // ---------------------------------------------------------------------------
-// Diagonal block: M[r][c] holds A/L in the lower triangle (r >= c) and
-// X^T = L^{-T} in the strict upper triangle (r < c); X = L^{-1} is built by
-// applying the elimination steps to the identity.
-template <int NB, int NT>
-__global__ __launch_bounds__(NT) void ldlt_diag_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
-                                                       double* __restrict__ D, double* __restrict__ Linv,
-                                                       int* __restrict__ info) {
-  __shared__ double M[NB][NB + 1];
-  __shared__ double lcol[NB];
-  __shared__ double dvals[NB];
+// Diagonal block (NB x NB, NB in {64, 128}) in REGISTERS.
+//
+// Thread grid T x T (T = NB/4; NB^2/16 threads), thread (tr, tc) holds the
+// 16 elements (tr + T a, tc + T b), a, b in 0..3.  Threads are numbered
+// column-major (tid = tc*T + tr), so the owners of one matrix column are T
+// consecutive lanes of ONE wave.  Lower-triangle elements hold A -> L; upper
+// elements (r < c) hold X^T where X = L^{-1} is built by applying every
+// elimination step to the identity (Gauss-Jordan), so the solve and the
+// panel TRSM get L11^{-1} for free.
+//
+// Step k (one workgroup barrier per step):
+//   owner wave: d_k from the diagonal owner (readlane), the zero-pivot rule of
+//     LinearSolvers.cpp:26-28, publish w_r = A[r][k] (r > k; = l_r d_k),
+//     l_r = w_r / d_k, and x_r = X[k][r] (r < k) to LDS (double-buffered by k)
+//   everyone: A[r][c] -= l_r w_c (k < c <= r),  X^T[r][c] -= l_c x_r (r <= k < c)
+// The update is the reference's  sum -= L[r][k] * L[c][k] * D[k]
+// (LinearSolvers.cpp:33) with L[c][k] * D[k] = w_c formed exactly once.
+template <int NB>
+__global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
+                                                                double* __restrict__ D, double* __restrict__ Linv,
+                                                                int* __restrict__ info) {
+  constexpr int T = NB / 4, NT = T * T;
+  __shared__ double M[NB][NB + 1];  // coalesced staging in/out
+  __shared__ double wsh[2][NB], lsh[2][NB], xsh[2][NB];
+  __shared__ double dsh[NB];
   const int tid = threadIdx.x;
+  const int tr = tid % T, tc = tid / T;
+  const int lane = tid & 63, wave = tid >> 6;
   for (int idx = tid; idx < NB * NB; idx += NT) {
     const int r = idx / NB, c = idx % NB;
-    double v = 0.0;
-    if (r < b && c <= r) v = K[(int64_t)(k0 + r) * ld + k0 + c];
-    M[r][c] = v;
+    M[r][c] = (r < b && c <= r) ? K[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? 1.0 : 0.0);
   }
   __syncthreads();
-  const int lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = NT / 64;
-  for (int k = 0; k < b; ++k) {
-    const double s = M[k][k];
-    const double dk = s == 0.0 ? 1e-8 : s;  // LinearSolvers.cpp:28
-    if (tid == 0) dvals[k] = dk;
-    for (int i = k + 1 + tid; i < b; i += NT) {
-      const double l = M[i][k] / dk;
-      M[i][k] = l;
-      lcol[i] = l;
-    }
-    __syncthreads();
-    // columns c > k: lower rows r >= c get the rank-1 update, rows r <= k
-    // (upper storage of X^T) get the Gauss-Jordan row operation.
-    for (int r = wave; r < b; r += NW) {
-      const double lr = r > k ? lcol[r] : 0.0;
-      const double xk = r < k ? M[r][k] : 1.0;  // X[k][r]
-      for (int c = k + 1 + lane; c < b; c += 64) {
-        if (r >= c) {
-          M[r][c] = M[r][c] - (lr * lcol[c]) * dk;
-        } else if (r <= k) {
-          M[r][c] = M[r][c] - lcol[c] * xk;
+  double v[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) v[a][c4] = M[tr + T * a][tc + T * c4];
+
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    for (int kk = 0; kk < T; ++kk) {
+      const int k = kb * T + kk;
+      if (k >= b) break;
+      const int buf = k & 1;
+      const int owner_wave = (kk * T) >> 6;
+      if (wave == owner_wave) {
+        const int diag_lane = (kk * T + kk) & 63;
+        const double draw =
+            __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v[kb][kb]), diag_lane),
+                             __builtin_amdgcn_readlane(__double2loint(v[kb][kb]), diag_lane));
+        const double dk = draw == 0.0 ? 1e-8 : draw;
+        if (tc == kk) {
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            const int r = tr + T * a;
+            const double w = v[a][kb];
+            if (r > k) {
+              const double l = w / dk;
+              v[a][kb] = l;
+              wsh[buf][r] = w;
+              lsh[buf][r] = l;
+            } else if (r < k) {
+              xsh[buf][r] = w;
+            } else {
+              xsh[buf][r] = 1.0;
+              dsh[k] = dk;
+            }
+          }
+        }
+      }
+      __syncthreads();
+      double lr[4], xr[4];
+#pragma unroll
+      for (int a = 0; a < 4; ++a) {
+        const int r = tr + T * a;
+        lr[a] = r > k ? lsh[buf][r] : 0.0;
+        xr[a] = r <= k ? xsh[buf][r] : 0.0;
+      }
+#pragma unroll
+      for (int c4 = kb; c4 < 4; ++c4) {  // columns of blocks < kb are finished
+        const int c = tc + T * c4;
+        if (c > k) {
+          const double wc = wsh[buf][c], lc = lsh[buf][c];
+#pragma unroll
+          for (int a = 0; a < 4; ++a) {
+            const int r = tr + T * a;
+            if (r >= c) v[a][c4] = fma(-lr[a], wc, v[a][c4]);
+            else if (r <= k) v[a][c4] = fma(-lc, xr[a], v[a][c4]);
+          }
         }
       }
     }
-    __syncthreads();
   }
-  // write back L (strict lower), D, and L^{-1} (NB x NB, identity-padded)
+  __syncthreads();
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c4 = 0; c4 < 4; ++c4) M[tr + T * a][tc + T * c4] = v[a][c4];
+  __syncthreads();
+  // write back L (strict lower), D, and L^{-1} (NB x NB row-major, identity-padded)
   for (int idx = tid; idx < NB * NB; idx += NT) {
     const int r = idx / NB, c = idx % NB;
     if (r < b && c < r) K[(int64_t)(k0 + r) * ld + k0 + c] = M[r][c];
@@ -80,7 +135,7 @@ __global__ __launch_bounds__(NT) void ldlt_diag_kernel(double* __restrict__ K, i
     Linv[idx] = x;
   }
   for (int k = tid; k < b; k += NT) {
-    const double dk = dvals[k];
+    const double dk = dsh[k];
     D[k0 + k] = dk;
     if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(info, k0 + k + 1);  // first non-finite pivot
   }
@@ -154,25 +209,77 @@ struct GemmArgs {
   int ntm, ntn;
 };
 
+// Tile pipeline: one LDS buffer is computed while the next k-chunk sits in
+// registers (loads issued before the MFMAs, written to the other buffer
+// after them): one barrier per 16-deep k-chunk.
+template <int BM, int BN>
+struct TileLoader {
+  static constexpr int BK = 16, PAD = 18;
+  static constexpr int QA = BM * BK / 2 / 256, QB = BN * BK / 2 / 256;  // double2 per thread
+  double2 ra[QA], rb[QB];
+  __device__ __forceinline__ void load(const GemmArgs& g, int i0, int j0, int kk) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      ra[q] = fetch(g.A, g.lda, i0 + r, g.M, kk + c, g.Kd);
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      rb[q] = fetch(g.B, g.ldb, j0 + r, g.N, kk + c, g.Kd);
+    }
+  }
+  __device__ __forceinline__ void store(double* As, double* Bs) const {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int q = 0; q < QA; ++q) {
+      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      *reinterpret_cast<double2*>(&As[r * PAD + c]) = ra[q];
+    }
+#pragma unroll
+    for (int q = 0; q < QB; ++q) {
+      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      *reinterpret_cast<double2*>(&Bs[r * PAD + c]) = rb[q];
+    }
+  }
+  static __device__ __forceinline__ double2 fetch(const double* P, int64_t ld, int row, int rows, int k, int Kd) {
+    double2 t = make_double2(0.0, 0.0);
+    if (row < rows) {
+      const double* p = P + (int64_t)row * ld + k;
+      if (k + 1 < Kd) t = *reinterpret_cast<const double2*>(p);
+      else if (k < Kd) t.x = p[0];
+    }
+    return t;
+  }
+};
+
 template <int BM, int BN, int EPI>
 __global__ __launch_bounds__(256) void gemm_nt_f64_kernel(GemmArgs g) {
   constexpr int BK = 16, PAD = 18;
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
-  __shared__ __attribute__((aligned(16))) double As[BM * PAD];
-  __shared__ __attribute__((aligned(16))) double Bs[BN * PAD];
+  __shared__ __attribute__((aligned(16))) double As[2][BM * PAD];
+  __shared__ __attribute__((aligned(16))) double Bs[2][BN * PAD];
 
+  // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks
+  // b and b+8 share an XCD, so consecutive logical tiles -- which share W
+  // (A) rows in both enumerations -- are handed to one XCD's L2.
+  int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = bid % 8;
+    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+  }
   int tm, tn;
   if (g.lower == 2) {
     // triangular enumeration of lower tiles: bid -> (tm >= tn)
-    const int bid = blockIdx.x;
     int r = (int)((sqrt(8.0 * (double)bid + 1.0) - 1.0) * 0.5);
     while ((r + 1) * (r + 2) / 2 <= bid) ++r;
     while (r * (r + 1) / 2 > bid) --r;
     tm = r;
     tn = bid - r * (r + 1) / 2;
   } else {
-    tm = blockIdx.x % g.ntm;
-    tn = blockIdx.x / g.ntm;
+    tn = bid % g.ntn;
+    tm = bid / g.ntn;
   }
   const int i0 = tm * BM, j0 = tn * BN;
   if (g.lower == 1 && g.row0 + i0 + BM - 1 < g.col0 + j0) return;
@@ -185,62 +292,30 @@ __global__ __launch_bounds__(256) void gemm_nt_f64_kernel(GemmArgs g) {
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
 
-  for (int kk = 0; kk < g.Kd; kk += BK) {
-    // stage A (BM x BK) and B (BN x BK): 8 threads per row, 2 doubles each
-#pragma unroll
-    for (int q = 0; q < (BM * BK / 2 + 255) / 256; ++q) {
-      const int ch = tid + 256 * q;
-      if (ch < BM * BK / 2) {
-        const int r = ch >> 3, c = (ch & 7) * 2;
-        const int gi = i0 + r, gk = kk + c;
-        double v0 = 0.0, v1 = 0.0;
-        if (gi < g.M) {
-          const double* p = g.A + (int64_t)gi * g.lda + gk;
-          if (gk + 1 < g.Kd) {
-            const double2 t = *reinterpret_cast<const double2*>(p);
-            v0 = t.x;
-            v1 = t.y;
-          } else if (gk < g.Kd) {
-            v0 = p[0];
-          }
-        }
-        *reinterpret_cast<double2*>(&As[r * PAD + c]) = make_double2(v0, v1);
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < (BN * BK / 2 + 255) / 256; ++q) {
-      const int ch = tid + 256 * q;
-      if (ch < BN * BK / 2) {
-        const int r = ch >> 3, c = (ch & 7) * 2;
-        const int gj = j0 + r, gk = kk + c;
-        double v0 = 0.0, v1 = 0.0;
-        if (gj < g.N) {
-          const double* p = g.B + (int64_t)gj * g.ldb + gk;
-          if (gk + 1 < g.Kd) {
-            const double2 t = *reinterpret_cast<const double2*>(p);
-            v0 = t.x;
-            v1 = t.y;
-          } else if (gk < g.Kd) {
-            v0 = p[0];
-          }
-        }
-        *reinterpret_cast<double2*>(&Bs[r * PAD + c]) = make_double2(v0, v1);
-      }
-    }
-    __syncthreads();
+  TileLoader<BM, BN> ld;
+  const int nch = (g.Kd + BK - 1) / BK;
+  ld.load(g, i0, j0, 0);
+  ld.store(As[0], Bs[0]);
+  __syncthreads();
+  for (int t = 0; t < nch; ++t) {
+    const int cur = t & 1;
+    if (t + 1 < nch) ld.load(g, i0, j0, (t + 1) * BK);
+    const double* as = As[cur];
+    const double* bs = Bs[cur];
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       const int k = 4 * s + (lane >> 4);
       double af[TM], bf[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) af[a] = As[(wr * WM + a * 16 + (lane & 15)) * PAD + k];
+      for (int a = 0; a < TM; ++a) af[a] = as[(wr * WM + a * 16 + (lane & 15)) * PAD + k];
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bf[b] = Bs[(wc * WN + b * 16 + (lane & 15)) * PAD + k];
+      for (int b = 0; b < TN; ++b) bf[b] = bs[(wc * WN + b * 16 + (lane & 15)) * PAD + k];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
         for (int b = 0; b < TN; ++b) acc[a][b] = mfma_f64_16x16x4(af[a], bf[b], acc[a][b]);
     }
+    if (t + 1 < nch) ld.store(As[cur ^ 1], Bs[cur ^ 1]);
     __syncthreads();
   }
 
@@ -330,9 +405,9 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
       const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
       double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
       if (nbi == 128)
-        hipLaunchKernelGGL((ldlt_diag_kernel<128, 512>), dim3(1), dim3(512), 0, st, K, ld, j0, bi, D, Lb, info);
+        hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info);
       else
-        hipLaunchKernelGGL((ldlt_diag_kernel<64, 256>), dim3(1), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info);
+        hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info);
       if ((e = hipGetLastError()) != hipSuccess) return e;
       const int r1 = j0 + bi;
       if (r1 >= N) continue;

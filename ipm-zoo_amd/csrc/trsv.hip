@@ -3,15 +3,16 @@
 // Replaces LinearSolvers::overwriting_solve_ldlt (LinearSolvers.cpp:44-74):
 // forward substitution (:56-59), diagonal scaling (:62-64), backward
 // substitution with L^T (:67-73).  Blocked by the factor's inner block size
-// nb; the diagonal-block solves use the L11^{-1} blocks saved by the factor
-// (ldlt.hip), the off-diagonal work is a wave-per-row (forward) or
-// lane-per-column (backward) GEMV over the strict lower triangle.
+// NB; the diagonal-block solves use the L11^{-1} blocks saved by the factor
+// (ldlt.hip), the off-diagonal work is a wave-per-row GEMV (forward, DPP
+// reductions) or a lane-per-column GEMV (backward) over the strict lower
+// triangle.  HBM/latency-bound: every step reads its NB-wide panel of L once.
 //
 // One launch per block step.  Workgroup 0 of step J owns the NEXT diagonal
 // block: it applies step J's update to those rows first and then solves
-// them, so step J+1 finds its block solution ready in the side buffer and no
-// workgroup re-reads an L11^{-1} block redundantly.  The solve runs in place
-// on b (the rows a step writes are never read by a later step).
+// them (its L^{-1} block is staged into LDS while the rows update), so step
+// J+1 finds its block solution ready in a side buffer.  The solve runs in
+// place on b (the rows a step writes are never read by a later step).
 #include "common.h"
 #include "kernels.h"
 
@@ -19,21 +20,30 @@ namespace ipmz {
 
 constexpr int TRSV_NT = 256;
 
-// y = Linv . v for one nb-block, Linv row-major nb x nb (unit lower).
-// Reads v[0..bj) from LDS, writes y to LDS.  4 waves, each row a wave dot.
+// Stage an NB x NB row-major block into LDS (padded rows) -- coalesced.
 template <int NB>
-__device__ void block_lower_apply(const double* __restrict__ Linv, const double* vs, double* ys, int bj,
-                                  bool transpose) {
+__device__ __forceinline__ void stage_block(const double* __restrict__ src, double (*dst)[NB + 1]) {
+  for (int idx = threadIdx.x; idx < NB * NB; idx += TRSV_NT) dst[idx / NB][idx % NB] = src[idx];
+}
+
+// y = Linv v (transpose: y = Linv^T v) from LDS; lanes own output rows, the 4
+// waves split the inner index.  Result in ys (LDS).  Caller syncs before.
+template <int NB>
+__device__ __forceinline__ void block_apply(const double (*Ls)[NB + 1], const double* vs, double* ys,
+                                            double (*part)[NB], bool transpose) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int t = wave; t < bj; t += TRSV_NT / 64) {
+  constexpr int CH = NB / 4;
+#pragma unroll
+  for (int q = 0; q < NB / 64; ++q) {
+    const int t = lane + 64 * q;
     double s = 0.0;
-    for (int c = lane; c < bj; c += 64) {
-      const double l = transpose ? Linv[(int64_t)c * NB + t] : Linv[(int64_t)t * NB + c];
-      s += l * vs[c];
-    }
-    s = wave_sum(s);
-    if (lane == 0) ys[t] = s;
+#pragma unroll 8
+    for (int c = wave * CH; c < (wave + 1) * CH; ++c) s += (transpose ? Ls[c][t] : Ls[t][c]) * vs[c];
+    part[wave][t] = s;
   }
+  __syncthreads();
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) ys[t] = (part[0][t] + part[1][t]) + (part[2][t] + part[3][t]);
+  __syncthreads();
 }
 
 // prologue: y_0 = Linv_0 b_0; b_0 <- y_0 / D_0; ybuf <- y_0
@@ -41,56 +51,81 @@ template <int NB>
 __global__ __launch_bounds__(TRSV_NT) void trsv_fwd_first(const double* __restrict__ Linv,
                                                           const double* __restrict__ D, double* __restrict__ b,
                                                           double* __restrict__ ybuf, int bj) {
-  __shared__ double vs[NB], ys[NB];
-  for (int t = threadIdx.x; t < bj; t += TRSV_NT) vs[t] = b[t];
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double vs[NB], ys[NB], part[4][NB];
+  stage_block<NB>(Linv, Ls);
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) vs[t] = t < bj ? b[t] : 0.0;
   __syncthreads();
-  block_lower_apply<NB>(Linv, vs, ys, bj, false);
-  __syncthreads();
+  block_apply<NB>(Ls, vs, ys, part, false);
   for (int t = threadIdx.x; t < bj; t += TRSV_NT) {
     ybuf[t] = ys[t];
     b[t] = ys[t] / D[t];
   }
 }
 
+// rows [r_begin, r_end): b_i -= L[i, j0:j0+NB] . y  (wave per row, 4 rows in
+// flight per wave).  If vout, the updated values are also written to
+// vout[i - r_begin] (LDS).
+template <int NB>
+__device__ __forceinline__ void rows_update(const double* __restrict__ K, int64_t ld, int j0, int r_begin, int r_end,
+                                            const double* ys, double* __restrict__ b, double* vout) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  constexpr int Q = NB / 64, R = 4;
+  double yl[Q];
+#pragma unroll
+  for (int q = 0; q < Q; ++q) yl[q] = ys[lane + 64 * q];
+  for (int i0 = r_begin + wave * R; i0 < r_end; i0 += (TRSV_NT / 64) * R) {
+    double s[R];
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      s[rr] = 0.0;
+      const int i = i0 + rr;
+      if (i < r_end) {
+        const double* Lr = K + (int64_t)i * ld + j0;
+#pragma unroll
+        for (int q = 0; q < Q; ++q) s[rr] += Lr[lane + 64 * q] * yl[q];
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < R; ++rr) {
+      const int i = i0 + rr;
+      const double t = wave_sum(s[rr]);
+      if (lane == 0 && i < r_end) {
+        const double v = b[i] - t;
+        b[i] = v;
+        if (vout) vout[i - r_begin] = v;
+      }
+    }
+  }
+}
+
 // forward step J: rows below block J: b_i -= L[i, J] . y_J.  Workgroup 0
-// owns block J+1 (rows [j1, j1+nb)) and solves it afterwards.
+// owns block J+1 (rows [j1, j1+bn)) and solves it afterwards.
 template <int NB>
 __global__ __launch_bounds__(TRSV_NT) void trsv_fwd_step(const double* __restrict__ K, int64_t ld, int N, int j0,
                                                          const double* __restrict__ LinvNext,
                                                          const double* __restrict__ D, double* __restrict__ b,
                                                          const double* __restrict__ yin, double* __restrict__ yout,
                                                          int rows_per_wg) {
-  __shared__ double ys[NB], vs[NB], yn[NB];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double ys[NB], vs[NB], yn[NB], part[4][NB];
   const int j1 = j0 + NB;
-  for (int t = threadIdx.x; t < NB; t += TRSV_NT) ys[t] = yin[t];
-  __syncthreads();
-  int r_begin, r_end;
   const int bn = N - j1 < NB ? N - j1 : NB;  // size of block J+1
-  if (blockIdx.x == 0) {
-    r_begin = j1;
-    r_end = j1 + bn;
-  } else {
-    r_begin = j1 + bn + (blockIdx.x - 1) * rows_per_wg;
-    r_end = r_begin + rows_per_wg < N ? r_begin + rows_per_wg : N;
+  if (blockIdx.x == 0) stage_block<NB>(LinvNext, Ls);  // overlaps the row updates
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
+    ys[t] = yin[t];
+    vs[t] = 0.0;
   }
-  // each wave takes a row: NB doubles = NB/64 per lane (coalesced)
-  for (int i = r_begin + wave; i < r_end; i += TRSV_NT / 64) {
-    const double* Lr = K + (int64_t)i * ld + j0;
-    double s = 0.0;
-#pragma unroll
-    for (int q = 0; q < NB / 64; ++q) s += Lr[lane + 64 * q] * ys[lane + 64 * q];
-    s = wave_sum(s);
-    if (lane == 0) {
-      const double v = b[i] - s;
-      b[i] = v;
-      if (blockIdx.x == 0) vs[i - j1] = v;
-    }
+  __syncthreads();
+  if (blockIdx.x != 0) {
+    const int r_begin = j1 + bn + (blockIdx.x - 1) * rows_per_wg;
+    const int r_end = r_begin + rows_per_wg < N ? r_begin + rows_per_wg : N;
+    rows_update<NB>(K, ld, j0, r_begin, r_end, ys, b, nullptr);
+    return;
   }
-  if (blockIdx.x != 0) return;
+  rows_update<NB>(K, ld, j0, j1, j1 + bn, ys, b, vs);
   __syncthreads();
-  block_lower_apply<NB>(LinvNext, vs, yn, bn, false);
-  __syncthreads();
+  block_apply<NB>(Ls, vs, yn, part, false);
   for (int t = threadIdx.x; t < bn; t += TRSV_NT) {
     yout[t] = yn[t];
     b[j1 + t] = yn[t] / D[j1 + t];
@@ -101,11 +136,12 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_fwd_step(const double* __restric
 template <int NB>
 __global__ __launch_bounds__(TRSV_NT) void trsv_bwd_first(const double* __restrict__ Linv, double* __restrict__ b,
                                                           double* __restrict__ xbuf, int jl, int bj) {
-  __shared__ double vs[NB], xs[NB];
-  for (int t = threadIdx.x; t < bj; t += TRSV_NT) vs[t] = b[jl + t];
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double vs[NB], xs[NB], part[4][NB];
+  stage_block<NB>(Linv, Ls);
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) vs[t] = t < bj ? b[jl + t] : 0.0;
   __syncthreads();
-  block_lower_apply<NB>(Linv, vs, xs, bj, true);
-  __syncthreads();
+  block_apply<NB>(Ls, vs, xs, part, true);
   for (int t = threadIdx.x; t < bj; t += TRSV_NT) {
     xbuf[t] = xs[t];
     b[jl + t] = xs[t];
@@ -113,31 +149,26 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_bwd_first(const double* __restri
 }
 
 // backward step J (block rows [j0, j0+bj)): z_i -= sum_r L[r][i] x_r for
-// i < j0.  Each workgroup owns 64 columns; its 4 waves split the nb rows and
+// i < j0.  Each workgroup owns NB columns; its 4 waves split the rows and
 // reduce through LDS.  Workgroup 0 owns block J-1 and solves it afterwards.
 template <int NB>
 __global__ __launch_bounds__(TRSV_NT) void trsv_bwd_step(const double* __restrict__ K, int64_t ld, int j0, int bj,
                                                          const double* __restrict__ LinvPrev,
                                                          double* __restrict__ b, const double* __restrict__ xin,
                                                          double* __restrict__ xout) {
+  __shared__ double Ls[NB][NB + 1];
   __shared__ double xs[NB], part[4][NB], vs[NB], xn[NB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int jp = j0 - NB;  // block J-1 start (j0 is a multiple of NB, >= NB)
+  if (blockIdx.x == 0) stage_block<NB>(LinvPrev, Ls);
   for (int t = threadIdx.x; t < NB; t += TRSV_NT) xs[t] = t < bj ? xin[t] : 0.0;
   __syncthreads();
-  const int jp = j0 - NB;  // block J-1 start (j0 is a multiple of NB, >= NB)
-  int c_begin, c_end;
-  if (blockIdx.x == 0) {
-    c_begin = jp;
-    c_end = j0;
-  } else {
-    c_begin = (blockIdx.x - 1) * NB;
-    c_end = c_begin + NB;
-  }
-  // NB columns per workgroup: lane handles column c_begin + lane + 64*q
+  const int c_begin = blockIdx.x == 0 ? jp : (blockIdx.x - 1) * NB;
   constexpr int CQ = NB / 64;
   double s[CQ];
 #pragma unroll
   for (int q = 0; q < CQ; ++q) s[q] = 0.0;
+#pragma unroll 4
   for (int r = wave; r < bj; r += 4) {
     const double* Lr = K + (int64_t)(j0 + r) * ld + c_begin;
     const double xr = xs[r];
@@ -153,11 +184,9 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_bwd_step(const double* __restric
     b[c_begin + c] = v;
     vs[c] = v;
   }
-  (void)c_end;
   if (blockIdx.x != 0) return;
   __syncthreads();
-  block_lower_apply<NB>(LinvPrev, vs, xn, NB, true);
-  __syncthreads();
+  block_apply<NB>(Ls, vs, xn, part, true);
   for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
     xout[t] = xn[t];
     b[jp + t] = xn[t];
@@ -168,7 +197,7 @@ template <int NB>
 static hipError_t ldlt_solve_nb(const double* K, int64_t ld, int N, const double* D, const double* Linv, double* b,
                                 double* side, hipStream_t st) {
   const int nblk = (N + NB - 1) / NB;
-  double* y0 = side;       // ping-pong block-solution buffers
+  double* y0 = side;  // ping-pong block-solution buffers
   double* y1 = side + NB;
   const int64_t LB = (int64_t)NB * NB;
   const int bj0 = N < NB ? N : NB;

@@ -56,6 +56,14 @@ class _QPConfig(ctypes.Structure):
 
 
 def _load():
+    # One HIP runtime per process: PyTorch-ROCm ships its own libamdhip64, and
+    # a second copy loaded next to it cannot open the device.  Loading torch
+    # first makes libipmz bind to torch's copy (same soname), so device
+    # pointers and streams are shared.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"libipmz not built: {LIB_PATH} missing (run __graft_entry__.build()); "
                           "there is no CPU fallback")

@@ -36,9 +36,9 @@ def test_ldlt_decomposition_golden(ctx, N, tag):
     D_ref = load(f"{tag}_D.bin")
     L, D, info = I.LinearSolvers.ldlt_decomposition(K, ctx)
     assert info == 0
-    if N <= 128:  # one diagonal block: reference arithmetic order, bitwise
-        assert np.array_equal(L, L_ref)
-        assert np.array_equal(D, D_ref)
+    if N <= 64:  # one diagonal block: the reference's k-order of updates (fused multiply-adds)
+        np.testing.assert_allclose(D, D_ref, rtol=1e-15, atol=0)
+        assert np.abs(L - L_ref).max() < 1e-15 * max(1.0, np.abs(L_ref).max())
     else:
         np.testing.assert_allclose(D, D_ref, rtol=1e-13, atol=0)
         assert np.abs(L - L_ref).max() < 1e-13 * max(1.0, np.abs(L_ref).max())
@@ -94,7 +94,7 @@ def test_ldlt_ragged_vs_oracle(ctx, N, blocking):
         x = I.LinearSolvers.overwriting_solve_ldlt(L, D, b.copy(), ctx)
         assert np.abs(x - x_o).max() < 1e-10
     finally:
-        ctx.set_blocking(256, 128)
+        ctx.set_blocking(256, 64)
 
 
 # ---------------------------------------------------------------------------

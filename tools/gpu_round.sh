@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: smoke -> GPU tests -> bench -> rocprof kernel stats.
+# Every GPU step has its own time limit; a crash/abort/timeout ends the run
+# (exit codes 124/134/137/139 or negative), plain test failures (1) do not.
+set -u
+OUT=${OUT:-gpurun_out}
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+step() {  # name timeout cmd...
+  local name=$1 t=$2; shift 2
+  echo "=== $name ($(date +%T))"
+  timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"
+  tail -5 "$OUT/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "ABORT after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for s in ${STEPS:-smoke tests bench prof}; do
+  case $s in
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    tests) step tests 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider ;;
+    bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    *) step "$s" 600 bash -c "$s" ;;
+  esac
+done
+echo ALL DONE

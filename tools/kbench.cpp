@@ -1,0 +1,97 @@
+// Kernel micro-benchmark for libipmz (MI355X): times the factor pieces with
+// HIP events.  Build: make -C ipm-zoo_amd kbench ; run: ipm-zoo_amd/build/kbench
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+#define CK(x)                                                                              \
+  do {                                                                                     \
+    hipError_t e = (x);                                                                    \
+    if (e != hipSuccess) {                                                                 \
+      std::fprintf(stderr, "%s:%d %s: %s\n", __FILE__, __LINE__, #x, hipGetErrorString(e)); \
+      std::exit(1);                                                                        \
+    }                                                                                      \
+  } while (0)
+
+__global__ void fill_qd(double* K, int64_t ld, int N, unsigned long long seed) {
+  const int64_t total = (int64_t)N * N;
+  for (int64_t t = blockIdx.x * 256ll + threadIdx.x; t < total; t += (int64_t)gridDim.x * 256) {
+    const int64_t i = t / N, j = t % N;
+    const int64_t a = i > j ? i : j, b = i > j ? j : i;
+    double v = (2.0 * ipmz_u01(seed, 9, a, b) - 1.0) / (double)N;
+    if (i == j) v = (i < 3 * N / 4) ? 1.0 + ipmz_u01(seed, 9, i, i) : -(0.5 + ipmz_u01(seed, 9, i, i));
+    K[i * ld + j] = v;
+  }
+}
+
+struct Timer {
+  hipEvent_t a, b;
+  Timer() {
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+  }
+  void start(hipStream_t s) { CK(hipEventRecord(a, s)); }
+  float stop(hipStream_t s) {
+    CK(hipEventRecord(b, s));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms;
+  }
+};
+
+int main(int argc, char** argv) {
+  const int N = argc > 1 ? std::atoi(argv[1]) : 11264;
+  hipStream_t st;
+  CK(hipStreamCreate(&st));
+  const int64_t ld = (N + 63) / 64 * 64;
+  double *K, *D, *Linv, *W, *b, *side;
+  int* info;
+  CK(hipMalloc(&K, ld * N * 8));
+  CK(hipMalloc(&D, N * 8));
+  CK(hipMalloc(&Linv, (int64_t)(N + 127) / 64 * 128 * 128 * 8));
+  CK(hipMalloc(&W, (int64_t)N * 512 * 8));
+  CK(hipMalloc(&b, N * 8));
+  CK(hipMalloc(&side, 1024 * 8));
+  CK(hipMalloc(&info, 64));
+  Timer t;
+  // 1. trailing GEMM alone: rank-nbo update of an R x R lower region
+  for (int nbo : {128, 256, 512}) {
+    for (int R : {2048, 5632, 11008}) {
+      if (R + nbo > N) continue;
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+      CK(ipmz::gemm_nt_sub(R, R, nbo, W, nbo, K, ld, K + (int64_t)nbo * ld + nbo, ld, 0, 0, true, st));
+      t.start(st);
+      const int reps = 5;
+      for (int r = 0; r < reps; ++r)
+        CK(ipmz::gemm_nt_sub(R, R, nbo, W, nbo, K, ld, K + (int64_t)nbo * ld + nbo, ld, 0, 0, true, st));
+      const float ms = t.stop(st) / reps;
+      const double fl = (double)R * (R + 1) * nbo;
+      std::printf("trailing nbo=%d R=%d: %.3f ms  %.2f TFLOP/s (algorithmic)\n", nbo, R, ms, fl / ms / 1e9);
+    }
+  }
+  // 2. full factor + solve per blocking
+  const int cfg[][2] = {{256, 64}, {256, 128}, {512, 64}, {512, 128}, {128, 64}};
+  for (auto& c : cfg) {
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+    CK(hipMemsetAsync(info, 0x7f, 4, st));
+    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st));  // warm
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+    t.start(st);
+    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st));
+    const float fms = t.stop(st);
+    CK(hipMemsetAsync(b, 0, N * 8, st));
+    t.start(st);
+    for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve(K, ld, N, D, Linv, c[1], b, side, st));
+    const float sms = t.stop(st) / 5;
+    std::printf("factor N=%d nbo=%d nbi=%d: %.3f ms = %.2f TFLOP/s (N^3/3); solve %.3f ms\n", N, c[0], c[1], fms,
+                (double)N * N * N / 3.0 / fms / 1e9, sms);
+  }
+  std::printf("done\n");
+  return 0;
+}
