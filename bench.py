@@ -105,17 +105,17 @@ def main():
     qp.generate(1234 + rank)
     timing = not args.no_timing
     flags = I.STEP_RESTART_IF_CONVERGED | (0 if timing else I.STEP_GRAPH)
-    red = torch.zeros(3, dtype=torch.float64, device="cuda")
+    from ipmz_amd.dist import pack_summary, reduce_summary
+
     sc = torch.zeros(I.SC_COUNT, dtype=torch.float64, device="cuda")
 
     def one_step():
         qp.step(flags)
         if world > 1:
-            # RCCL all-reduce of the convergence scalars only
+            # RCCL all-reduce of the convergence scalars only,
+            # enqueued on the solver's stream: no host round trip
             qp.copy_scalars(sc.data_ptr())
-            red[0] = sc[I.SC["res"]]
-            red[1] = sc[I.SC["mu"]]
-            dist.all_reduce(red[:2], op=dist.ReduceOp.MAX)
+            reduce_summary(pack_summary(sc[I.SC["res"]], sc[I.SC["mu"]], sc[I.SC["converged"]], "cuda"))
 
     for _ in range(args.warmup):
         one_step()
