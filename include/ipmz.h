@@ -87,9 +87,12 @@ typedef struct ipmz_qp ipmz_qp;
 /* ---- context ---------------------------------------------------------- */
 int ipmz_ctx_create(ipmz_ctx** out, int device);
 int ipmz_ctx_destroy(ipmz_ctx* ctx);
-/* Use an external HIP stream (e.g. torch.cuda.current_stream().cuda_stream);
- * NULL restores the context's own stream. */
+/* Enqueue on an external HIP stream, e.g. torch.cuda.current_stream().cuda_stream.
+ * NULL selects the HIP null (legacy default) stream -- what PyTorch's
+ * default stream is -- NOT the context's own stream. */
 int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* hip_stream);
+/* Go back to the context's own (non-blocking) stream. */
+int ipmz_ctx_reset_stream(ipmz_ctx* ctx);
 int ipmz_ctx_sync(ipmz_ctx* ctx);
 const char* ipmz_last_error(void);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512),

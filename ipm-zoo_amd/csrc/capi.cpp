@@ -87,7 +87,13 @@ int ipmz_ctx_destroy(ipmz_ctx* ctx) {
 
 int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* s) {
   if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
-  ctx->stream = s ? static_cast<hipStream_t>(s) : ctx->own;
+  ctx->stream = static_cast<hipStream_t>(s);  // NULL = the legacy default stream
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_reset_stream(ipmz_ctx* ctx) {
+  if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
+  ctx->stream = ctx->own;
   return IPMZ_OK;
 }
 

@@ -33,7 +33,7 @@ STEP_GRAPH = 2
 SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"]
 
 EXPORTS = [
-    "ipmz_ctx_create", "ipmz_ctx_destroy", "ipmz_ctx_set_stream", "ipmz_ctx_sync", "ipmz_last_error",
+    "ipmz_ctx_create", "ipmz_ctx_destroy", "ipmz_ctx_set_stream", "ipmz_ctx_reset_stream", "ipmz_ctx_sync", "ipmz_last_error",
     "ipmz_ctx_set_blocking", "ipmz_ldlt_workspace_bytes", "ipmz_ldlt_factor", "ipmz_ldlt_solve",
     "ipmz_ldlt_prepare_solve", "ipmz_ldlt_decomposition", "ipmz_overwriting_solve_ldlt", "ipmz_qp_create",
     "ipmz_qp_destroy", "ipmz_qp_load_host", "ipmz_qp_generate", "ipmz_qp_step", "ipmz_qp_scalars",
@@ -72,6 +72,7 @@ def _load():
         "ipmz_ctx_create": ([ctypes.POINTER(_VP), _I], _I),
         "ipmz_ctx_destroy": ([_VP], _I),
         "ipmz_ctx_set_stream": ([_VP, _VP], _I),
+        "ipmz_ctx_reset_stream": ([_VP], _I),
         "ipmz_ctx_sync": ([_VP], _I),
         "ipmz_last_error": ([], ctypes.c_char_p),
         "ipmz_ctx_set_blocking": ([_VP, _I, _I], _I),
@@ -133,7 +134,12 @@ class Context:
             self.set_blocking(nbo or 256, nbi or 128)
 
     def set_stream(self, stream):
-        _check(lib.ipmz_ctx_set_stream(self.h, _VP(stream)), "ipmz_ctx_set_stream")
+        """Enqueue on an external HIP stream handle (0 = the null stream,
+        which is PyTorch's default stream); None = the context's own stream."""
+        if stream is None:
+            _check(lib.ipmz_ctx_reset_stream(self.h), "ipmz_ctx_reset_stream")
+        else:
+            _check(lib.ipmz_ctx_set_stream(self.h, _VP(stream)), "ipmz_ctx_set_stream")
 
     def set_blocking(self, nbo, nbi):
         _check(lib.ipmz_ctx_set_blocking(self.h, nbo, nbi), "ipmz_ctx_set_blocking")

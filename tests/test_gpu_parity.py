@@ -79,7 +79,7 @@ def _qd(N, seed):
 
 
 @pytest.mark.parametrize("N", [127, 129, 300, 513, 1000])
-@pytest.mark.parametrize("blocking", [(256, 128), (128, 64), (512, 128)])
+@pytest.mark.parametrize("blocking", [(256, 64), (256, 128), (128, 64), (512, 128), (512, 64)])
 def test_ldlt_ragged_vs_oracle(ctx, N, blocking):
     ctx.set_blocking(*blocking)
     try:

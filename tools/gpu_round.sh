@@ -7,7 +7,7 @@ OUT=${OUT:-gpurun_out}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 step() {  # name timeout cmd...
-  local name=$1 t=$2; shift 2
+  local name=$(basename "$1") t=$2; shift 2
   echo "=== $name ($(date +%T))"
   timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
   local rc=$?
@@ -22,7 +22,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     tests) step tests 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
-    *) step "$s" 600 bash -c "$s" ;;
+    *) step "$s" 600 $s ;;
   esac
 done
 echo ALL DONE
