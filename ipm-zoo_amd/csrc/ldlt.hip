@@ -212,21 +212,21 @@ struct GemmArgs {
 // Tile pipeline: one LDS buffer is computed while the next k-chunk sits in
 // registers (loads issued before the MFMAs, written to the other buffer
 // after them): one barrier per 16-deep k-chunk.
-template <int BM, int BN>
+template <int BM, int BN, int NTH>
 struct TileLoader {
   static constexpr int BK = 16, PAD = 18;
-  static constexpr int QA = BM * BK / 2 / 256, QB = BN * BK / 2 / 256;  // double2 per thread
+  static constexpr int QA = BM * BK / 2 / NTH, QB = BN * BK / 2 / NTH;  // double2 per thread
   double2 ra[QA], rb[QB];
   __device__ __forceinline__ void load(const GemmArgs& g, int i0, int j0, int kk) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
       ra[q] = fetch(g.A, g.lda, i0 + r, g.M, kk + c, g.Kd);
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
       rb[q] = fetch(g.B, g.ldb, j0 + r, g.N, kk + c, g.Kd);
     }
   }
@@ -234,12 +234,12 @@ struct TileLoader {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
       *reinterpret_cast<double2*>(&As[r * PAD + c]) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int ch = tid + 256 * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
       *reinterpret_cast<double2*>(&Bs[r * PAD + c]) = rb[q];
     }
   }
@@ -254,10 +254,10 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, int EPI>
-__global__ __launch_bounds__(256) void gemm_nt_f64_kernel(GemmArgs g) {
-  constexpr int BK = 16, PAD = 18;
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 16, TN = WN / 16;
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
+__global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g) {
+  constexpr int BK = 16, PAD = 18, NTH = 64 * WGM * WGN;
+  constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) double As[2][BM * PAD];
   __shared__ __attribute__((aligned(16))) double Bs[2][BN * PAD];
 
@@ -285,14 +285,14 @@ __global__ __launch_bounds__(256) void gemm_nt_f64_kernel(GemmArgs g) {
   if (g.lower == 1 && g.row0 + i0 + BM - 1 < g.col0 + j0) return;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
+  const int wr = wave / WGN, wc = wave % WGN;
   double4_t acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
 
-  TileLoader<BM, BN> ld;
+  TileLoader<BM, BN, NTH> ld;
   const int nch = (g.Kd + BK - 1) / BK;
   ld.load(g, i0, j0, 0);
   ld.store(As[0], Bs[0]);
@@ -344,14 +344,65 @@ __global__ __launch_bounds__(256) void gemm_nt_f64_kernel(GemmArgs g) {
     }
 }
 
-template <int BM, int BN, int EPI>
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
 static hipError_t launch_gemm(GemmArgs g, hipStream_t st) {
   g.ntm = (g.M + BM - 1) / BM;
   g.ntn = (g.N + BN - 1) / BN;
   if (g.ntm == 0 || g.ntn == 0 || g.Kd == 0) return hipSuccess;
   int64_t nblk = (int64_t)g.ntm * g.ntn;
-  if (g.lower == 2) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
-  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI>), dim3((unsigned)nblk), dim3(256), 0, st, g);
+  if (g.lower == 2) {
+    // triangular enumeration needs square tiles; BM = k * BN tiles use a
+    // rectangular grid with upper-tile skipping instead
+    if (BM == BN) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
+    else g.lower = 1;
+  }
+  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN>), dim3((unsigned)nblk), dim3(64 * WGM * WGN), 0, st,
+                     g);
+  return hipGetLastError();
+}
+
+// experiment hook (kbench): trailing update with a chosen tile variant
+hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
+                               int64_t ldb, double* C, int64_t ldc, hipStream_t st) {
+  GemmArgs g{};
+  g.M = M;
+  g.N = N;
+  g.Kd = Kd;
+  g.A = A;
+  g.lda = lda;
+  g.B = B;
+  g.ldb = ldb;
+  g.C = C;
+  g.ldc = ldc;
+  g.lower = 2;
+  switch (variant) {
+    case 0: return launch_gemm<128, 128, EPI_SUB>(g, st);
+    case 1: return launch_gemm<256, 128, EPI_SUB, 4, 2>(g, st);
+    case 2: return launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st);
+    case 3: return launch_gemm<128, 64, EPI_SUB, 2, 1>(g, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// f64 MFMA throughput probe: each wave runs `iters` x 16 independent
+// v_mfma_f64_16x16x4 on register data.
+__global__ __launch_bounds__(256) void mfma_probe_kernel(double* out, int iters) {
+  double4_t acc[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) acc[i] = (double4_t){0.0, 0.0, 0.0, 0.0};
+  double a = threadIdx.x * 1e-3, b = blockIdx.x * 1e-3;
+  for (int it = 0; it < iters; ++it) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = mfma_f64_16x16x4(a, b, acc[i]);
+    a += 1e-9;
+  }
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  if (s == 12345.678) out[0] = s;
+}
+hipError_t mfma_probe(double* out, int blocks, int iters, hipStream_t st) {
+  hipLaunchKernelGGL(mfma_probe_kernel, dim3(blocks), dim3(256), 0, st, out, iters);
   return hipGetLastError();
 }
 

@@ -60,6 +60,25 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&side, 1024 * 8));
   CK(hipMalloc(&info, 64));
   Timer t;
+  {  // 0. f64 MFMA peak probe
+    const int iters = 20000, blocks = 1024;
+    CK(ipmz::mfma_probe(D, blocks, 10, st));
+    t.start(st);
+    CK(ipmz::mfma_probe(D, blocks, iters, st));
+    const float ms = t.stop(st);
+    const double fl = (double)blocks * 4 * iters * 16 * 2048.0;
+    std::printf("mfma_f64_16x16x4 probe: %.2f TFLOP/s (%d blocks x 4 waves)\n", fl / ms / 1e9, blocks);
+  }
+  for (int var = 0; var < 4; ++var) {
+    for (int R : {5632, 11008}) {
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+      CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+      t.start(st);
+      for (int r = 0; r < 5; ++r) CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+      const float ms = t.stop(st) / 5;
+      std::printf("gemm variant %d R=%d K=256: %.3f ms %.2f TFLOP/s\n", var, R, ms, (double)R * (R + 1) * 256 / ms / 1e9);
+    }
+  }
   // 1. trailing GEMM alone: rank-nbo update of an R x R lower region
   for (int nbo : {128, 256, 512}) {
     for (int R : {2048, 5632, 11008}) {
