@@ -22,7 +22,7 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
                        int* info, hipStream_t st, TrailTimer* timer = nullptr);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
-hipError_t mfma_probe(double* out, int blocks, int iters, hipStream_t st);
+hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st);

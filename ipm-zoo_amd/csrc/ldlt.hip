@@ -380,29 +380,36 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 1: return launch_gemm<256, 128, EPI_SUB, 4, 2>(g, st);
     case 2: return launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st);
     case 3: return launch_gemm<128, 64, EPI_SUB, 2, 1>(g, st);
+    case 4: return launch_gemm<256, 128, EPI_SUB, 4, 4>(g, st);
+    case 5: return launch_gemm<128, 128, EPI_SUB, 4, 4>(g, st);
+    case 6: return launch_gemm<128, 256, EPI_SUB, 2, 8>(g, st);
+    case 7: return launch_gemm<256, 256, EPI_SUB, 4, 4>(g, st);
     default: return hipErrorInvalidValue;
   }
 }
 
 // f64 MFMA throughput probe: each wave runs `iters` x 16 independent
 // v_mfma_f64_16x16x4 on register data.
-__global__ __launch_bounds__(256) void mfma_probe_kernel(double* out, int iters) {
-  double4_t acc[16];
+template <int NACC>
+__global__ __launch_bounds__(512) void mfma_probe_kernel(double* out, int iters) {
+  double4_t acc[NACC];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i] = (double4_t){0.0, 0.0, 0.0, 0.0};
+  for (int i = 0; i < NACC; ++i) acc[i] = (double4_t){0.0, 0.0, 0.0, 0.0};
   double a = threadIdx.x * 1e-3, b = blockIdx.x * 1e-3;
   for (int it = 0; it < iters; ++it) {
 #pragma unroll
-    for (int i = 0; i < 16; ++i) acc[i] = mfma_f64_16x16x4(a, b, acc[i]);
-    a += 1e-9;
+    for (int i = 0; i < NACC; ++i) acc[i] = mfma_f64_16x16x4(a, b, acc[i]);
   }
   double s = 0.0;
 #pragma unroll
-  for (int i = 0; i < 16; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
+  for (int i = 0; i < NACC; ++i) s += acc[i][0] + acc[i][1] + acc[i][2] + acc[i][3];
   if (s == 12345.678) out[0] = s;
 }
-hipError_t mfma_probe(double* out, int blocks, int iters, hipStream_t st) {
-  hipLaunchKernelGGL(mfma_probe_kernel, dim3(blocks), dim3(256), 0, st, out, iters);
+// waves_per_simd in {1, 2}: 256- or 512-thread blocks, one block per CU
+hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st) {
+  if (nacc == 16) hipLaunchKernelGGL(mfma_probe_kernel<16>, dim3(blocks), dim3(threads), 0, st, out, iters);
+  else if (nacc == 8) hipLaunchKernelGGL(mfma_probe_kernel<8>, dim3(blocks), dim3(threads), 0, st, out, iters);
+  else hipLaunchKernelGGL(mfma_probe_kernel<4>, dim3(blocks), dim3(threads), 0, st, out, iters);
   return hipGetLastError();
 }
 

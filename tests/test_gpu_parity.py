@@ -68,10 +68,10 @@ def _qd(N, seed):
     rng = np.random.default_rng(seed)
     n1 = (3 * N + 3) // 4
     K = rng.uniform(-1, 1, (N, N))
-    K = (K + K.T) / 2
     K[:n1, :n1] /= n1
     K[n1:, :n1] /= np.sqrt(n1)
     K[n1:, n1:] = 0
+    K = np.tril(K) + np.tril(K, -1).T  # symmetric
     d = rng.uniform(0.5, 1.5, N)
     K[np.arange(n1), np.arange(n1)] = 1 + d[:n1]
     K[np.arange(n1, N), np.arange(n1, N)] = -d[n1:]

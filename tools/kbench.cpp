@@ -60,16 +60,18 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&side, 1024 * 8));
   CK(hipMalloc(&info, 64));
   Timer t;
-  {  // 0. f64 MFMA peak probe
-    const int iters = 20000, blocks = 1024;
-    CK(ipmz::mfma_probe(D, blocks, 10, st));
-    t.start(st);
-    CK(ipmz::mfma_probe(D, blocks, iters, st));
-    const float ms = t.stop(st);
-    const double fl = (double)blocks * 4 * iters * 16 * 2048.0;
-    std::printf("mfma_f64_16x16x4 probe: %.2f TFLOP/s (%d blocks x 4 waves)\n", fl / ms / 1e9, blocks);
+  for (int threads : {256, 512}) {  // 0. f64 MFMA peak probe
+    for (int nacc : {4, 8, 16}) {
+      const int iters = 20000, blocks = 2048;
+      CK(ipmz::mfma_probe(D, blocks, 10, threads, nacc, st));
+      t.start(st);
+      CK(ipmz::mfma_probe(D, blocks, iters, threads, nacc, st));
+      const float ms = t.stop(st);
+      const double fl = (double)blocks * (threads / 64) * iters * nacc * 2048.0;
+      std::printf("mfma_f64_16x16x4 probe: threads=%d nacc=%d: %.2f TFLOP/s\n", threads, nacc, fl / ms / 1e9);
+    }
   }
-  for (int var = 0; var < 4; ++var) {
+  for (int var = 0; var < 8; ++var) {
     for (int R : {5632, 11008}) {
       hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
       CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
@@ -80,7 +82,7 @@ int main(int argc, char** argv) {
     }
   }
   // 1. trailing GEMM alone: rank-nbo update of an R x R lower region
-  for (int nbo : {128, 256, 512}) {
+  for (int nbo : {256}) {
     for (int R : {2048, 5632, 11008}) {
       if (R + nbo > N) continue;
       hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
