@@ -76,13 +76,14 @@ __global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restri
             __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v[kb][kb]), diag_lane),
                              __builtin_amdgcn_readlane(__double2loint(v[kb][kb]), diag_lane));
         const double dk = draw == 0.0 ? 1e-8 : draw;
+        const double rdk = 1.0 / dk;
         if (tc == kk) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
             const int r = tr + T * a;
             const double w = v[a][kb];
             if (r > k) {
-              const double l = w / dk;
+              const double l = w * rdk;
               v[a][kb] = l;
               wsh[buf][r] = w;
               lsh[buf][r] = l;
@@ -431,7 +432,11 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   g.lower = square_lower ? 2 : 1;
   // the trailing update (square, triangular grid) and the strip update are
   // separate instantiations so kernel traces attribute them separately
-  return square_lower ? launch_gemm<128, 128, EPI_SUB>(g, st) : launch_gemm<128, 128, EPI_SUB_STRIP>(g, st);
+  // 128x128 tile, 8 waves as 2 x 4 (64 x 32 per wave, 128 VGPRs), 72 KB LDS:
+  // two workgroups per CU = 4 waves per SIMD (kbench: 47 TFLOP/s = 60 % of
+  // the fp64 MFMA peak at R = 11008, vs 25 with 4 waves of 64 x 64)
+  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st)
+                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st);
 }
 
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
@@ -447,7 +452,7 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
   g.C = C;
   g.ldc = ldc;
   g.lower = 0;
-  return launch_gemm<128, 128, EPI_STORE>(g, st);
+  return launch_gemm<128, 128, EPI_STORE, 2, 4>(g, st);
 }
 
 // ---------------------------------------------------------------------------
@@ -484,7 +489,7 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
       g.ldw = nbo;
       g.dvec = D + j0;
       g.lower = 0;
-      e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL>(g, st) : launch_gemm<128, 64, EPI_PANEL>(g, st);
+      e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL, 2, 4>(g, st) : launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st);
       if (e != hipSuccess) return e;
       // strip update of the remaining columns of this outer panel
       const int c1 = k0 + bo;

@@ -63,67 +63,67 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_fwd_first(const double* __restri
   }
 }
 
-// rows [r_begin, r_end): b_i -= L[i, j0:j0+NB] . y  (wave per row, 4 rows in
-// flight per wave).  If vout, the updated values are also written to
-// vout[i - r_begin] (LDS).
+// Forward row update of one workgroup: rows [r_begin, r_begin + NB) (clipped
+// to r_end): b_i -= L[i, j0:j0+NB] . y_J.  Each wave owns NB/4 rows; every
+// global load (L rows, b, y) is issued before the first use so the step
+// pays one memory latency, then wave dot products with DPP reductions.
 template <int NB>
 __device__ __forceinline__ void rows_update(const double* __restrict__ K, int64_t ld, int j0, int r_begin, int r_end,
-                                            const double* ys, double* __restrict__ b, double* vout) {
+                                            const double* __restrict__ yin, double* __restrict__ b, double* ys,
+                                            double* bs, double* vout) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  constexpr int Q = NB / 64, R = 4;
+  constexpr int Q = NB / 64, RW = NB / 4;
+  double lv[RW][Q];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int i = r_begin + wave + 4 * j;
+#pragma unroll
+    for (int q = 0; q < Q; ++q) lv[j][q] = i < r_end ? K[(int64_t)i * ld + j0 + lane + 64 * q] : 0.0;
+  }
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
+    ys[t] = yin[t];
+    const int i = r_begin + t;
+    bs[t] = i < r_end ? b[i] : 0.0;
+  }
+  __syncthreads();
   double yl[Q];
 #pragma unroll
   for (int q = 0; q < Q; ++q) yl[q] = ys[lane + 64 * q];
-  for (int i0 = r_begin + wave * R; i0 < r_end; i0 += (TRSV_NT / 64) * R) {
-    double s[R];
 #pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-      s[rr] = 0.0;
-      const int i = i0 + rr;
-      if (i < r_end) {
-        const double* Lr = K + (int64_t)i * ld + j0;
+  for (int j = 0; j < RW; ++j) {
+    double s = 0.0;
 #pragma unroll
-        for (int q = 0; q < Q; ++q) s[rr] += Lr[lane + 64 * q] * yl[q];
-      }
-    }
-#pragma unroll
-    for (int rr = 0; rr < R; ++rr) {
-      const int i = i0 + rr;
-      const double t = wave_sum(s[rr]);
-      if (lane == 0 && i < r_end) {
-        const double v = b[i] - t;
-        b[i] = v;
-        if (vout) vout[i - r_begin] = v;
-      }
+    for (int q = 0; q < Q; ++q) s += lv[j][q] * yl[q];
+    s = wave_sum(s);
+    const int t = wave + 4 * j, i = r_begin + t;
+    if (lane == 0 && i < r_end) {
+      const double v = bs[t] - s;
+      b[i] = v;
+      if (vout) vout[t] = v;
     }
   }
 }
 
 // forward step J: rows below block J: b_i -= L[i, J] . y_J.  Workgroup 0
-// owns block J+1 (rows [j1, j1+bn)) and solves it afterwards.
+// owns block J+1 (rows [j1, j1+bn)) and solves it afterwards; workgroup
+// w > 0 owns rows [j1 + bn + (w-1) NB, +NB).
 template <int NB>
 __global__ __launch_bounds__(TRSV_NT) void trsv_fwd_step(const double* __restrict__ K, int64_t ld, int N, int j0,
                                                          const double* __restrict__ LinvNext,
                                                          const double* __restrict__ D, double* __restrict__ b,
-                                                         const double* __restrict__ yin, double* __restrict__ yout,
-                                                         int rows_per_wg) {
+                                                         const double* __restrict__ yin, double* __restrict__ yout) {
   __shared__ double Ls[NB][NB + 1];
-  __shared__ double ys[NB], vs[NB], yn[NB], part[4][NB];
+  __shared__ double ys[NB], bs[NB], vs[NB], yn[NB], part[4][NB];
   const int j1 = j0 + NB;
   const int bn = N - j1 < NB ? N - j1 : NB;  // size of block J+1
-  if (blockIdx.x == 0) stage_block<NB>(LinvNext, Ls);  // overlaps the row updates
-  for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
-    ys[t] = yin[t];
-    vs[t] = 0.0;
-  }
-  __syncthreads();
   if (blockIdx.x != 0) {
-    const int r_begin = j1 + bn + (blockIdx.x - 1) * rows_per_wg;
-    const int r_end = r_begin + rows_per_wg < N ? r_begin + rows_per_wg : N;
-    rows_update<NB>(K, ld, j0, r_begin, r_end, ys, b, nullptr);
+    const int r_begin = j1 + bn + (blockIdx.x - 1) * NB;
+    rows_update<NB>(K, ld, j0, r_begin, N, yin, b, ys, bs, nullptr);
     return;
   }
-  rows_update<NB>(K, ld, j0, j1, j1 + bn, ys, b, vs);
+  stage_block<NB>(LinvNext, Ls);  // in flight with the row loads
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) vs[t] = 0.0;
+  rows_update<NB>(K, ld, j0, j1, j1 + bn, yin, b, ys, bs, vs);
   __syncthreads();
   block_apply<NB>(Ls, vs, yn, part, false);
   for (int t = threadIdx.x; t < bn; t += TRSV_NT) {
@@ -157,30 +157,40 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_bwd_step(const double* __restric
                                                          double* __restrict__ b, const double* __restrict__ xin,
                                                          double* __restrict__ xout) {
   __shared__ double Ls[NB][NB + 1];
-  __shared__ double xs[NB], part[4][NB], vs[NB], xn[NB];
+  __shared__ double xs[NB], part[4][NB], vs[NB], xn[NB], bs[NB];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int jp = j0 - NB;  // block J-1 start (j0 is a multiple of NB, >= NB)
   if (blockIdx.x == 0) stage_block<NB>(LinvPrev, Ls);
-  for (int t = threadIdx.x; t < NB; t += TRSV_NT) xs[t] = t < bj ? xin[t] : 0.0;
-  __syncthreads();
   const int c_begin = blockIdx.x == 0 ? jp : (blockIdx.x - 1) * NB;
-  constexpr int CQ = NB / 64;
+  // issue every load first: this wave's rows of the block-row panel, x_J, b
+  constexpr int CQ = NB / 64, RW = NB / 4;
+  double lv[RW][CQ];
+#pragma unroll
+  for (int j = 0; j < RW; ++j) {
+    const int r = wave + 4 * j;
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) lv[j][q] = r < bj ? K[(int64_t)(j0 + r) * ld + c_begin + lane + 64 * q] : 0.0;
+  }
+  for (int t = threadIdx.x; t < NB; t += TRSV_NT) {
+    xs[t] = t < bj ? xin[t] : 0.0;
+    bs[t] = b[c_begin + t];
+  }
+  __syncthreads();
   double s[CQ];
 #pragma unroll
   for (int q = 0; q < CQ; ++q) s[q] = 0.0;
-#pragma unroll 4
-  for (int r = wave; r < bj; r += 4) {
-    const double* Lr = K + (int64_t)(j0 + r) * ld + c_begin;
-    const double xr = xs[r];
 #pragma unroll
-    for (int q = 0; q < CQ; ++q) s[q] += Lr[lane + 64 * q] * xr;
+  for (int j = 0; j < RW; ++j) {
+    const double xr = xs[wave + 4 * j];
+#pragma unroll
+    for (int q = 0; q < CQ; ++q) s[q] += lv[j][q] * xr;
   }
 #pragma unroll
   for (int q = 0; q < CQ; ++q) part[wave][lane + 64 * q] = s[q];
   __syncthreads();
   for (int c = threadIdx.x; c < NB; c += TRSV_NT) {
     const double t = (part[0][c] + part[1][c]) + (part[2][c] + part[3][c]);
-    const double v = b[c_begin + c] - t;
+    const double v = bs[c] - t;
     b[c_begin + c] = v;
     vs[c] = v;
   }
@@ -204,16 +214,15 @@ static hipError_t ldlt_solve_nb(const double* K, int64_t ld, int N, const double
   hipLaunchKernelGGL((trsv_fwd_first<NB>), dim3(1), dim3(TRSV_NT), 0, st, Linv, D, b, y0, bj0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const int rows_per_wg = 64;
   for (int J = 0; J + 1 < nblk; ++J) {
     const int j0 = J * NB, j1 = j0 + NB;
     const int bn = N - j1 < NB ? N - j1 : NB;
     const int rest = N - j1 - bn;
-    const int nwg = 1 + (rest + rows_per_wg - 1) / rows_per_wg;
+    const int nwg = 1 + (rest + NB - 1) / NB;
     double* yin = (J & 1) ? y1 : y0;
     double* yout = (J & 1) ? y0 : y1;
     hipLaunchKernelGGL((trsv_fwd_step<NB>), dim3(nwg), dim3(TRSV_NT), 0, st, K, ld, N, j0, Linv + (J + 1) * LB, D,
-                       b, yin, yout, rows_per_wg);
+                       b, yin, yout);
     if ((e = hipGetLastError()) != hipSuccess) return e;
   }
   // backward
