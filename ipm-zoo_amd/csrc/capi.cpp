@@ -8,6 +8,7 @@
 #include <climits>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -114,9 +115,10 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
 
 // ---------------------------------------------------------------------------
 // Workspace: [info int (256 B)] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
+//            [ybuf N] [zbuf N] [ctrl 2 + 2*nblk64 uint]
 namespace {
 struct WsLayout {
-  int64_t info_off, side_off, linv_off, w_off, total;
+  int64_t info_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
 };
 WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
@@ -125,8 +127,27 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   l.side_off = 256;
   l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
-  l.total = l.w_off + round_up((int64_t)N * nbo * 8, 256);
+  l.y_off = l.w_off + round_up((int64_t)N * nbo * 8, 256);
+  l.z_off = l.y_off + round_up((int64_t)N * 8, 256);
+  l.ctrl_off = l.z_off + round_up((int64_t)N * 8, 256);
+  l.total = l.ctrl_off + round_up((2 + 2 * ((int64_t)N + 63) / 64) * 4, 256);
   return l;
+}
+bool use_persistent_solve(int nbi) {
+  static const char* env = std::getenv("IPMZ_SOLVE");
+  return nbi == 64 && !(env && std::strcmp(env, "blocked") == 0);
+}
+// the solve (persistent single launch for nbi == 64, else block-step chain)
+hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const char* ws, int nbo, int nbi, double* b,
+                    hipStream_t st) {
+  const WsLayout l = ws_layout(N, nbo, nbi);
+  char* w = const_cast<char*>(ws);
+  const double* Linv = reinterpret_cast<const double*>(w + l.linv_off);
+  if (use_persistent_solve(nbi))
+    return ldlt_solve_persistent(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.y_off),
+                                 reinterpret_cast<double*>(w + l.z_off), reinterpret_cast<unsigned*>(w + l.ctrl_off),
+                                 st);
+  return ldlt_solve(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.side_off), st);
 }
 }  // namespace
 
@@ -166,10 +187,7 @@ int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const dou
   if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_solve: bad arguments");
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
-  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
-  const char* w = static_cast<const char*>(ws);
-  HIP_OK(ldlt_solve(K, ld, N, D, reinterpret_cast<const double*>(w + l.linv_off), ctx->nbi, b,
-                    reinterpret_cast<double*>(const_cast<char*>(w) + l.side_off), ctx->stream));
+  HIP_OK(solve_ws(K, ld, N, D, static_cast<const char*>(ws), ctx->nbo, ctx->nbi, b, ctx->stream));
   return IPMZ_OK;
 }
 
@@ -330,13 +348,10 @@ int run_step(ipmz_qp* s, int flags) {
   int rc = factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, t ? &tt : nullptr);
   if (rc) return rc;
   mark(2);
-  const WsLayout l = ws_layout(s->N, s->ctx->nbo, s->ctx->nbi);
-  const double* Linv = reinterpret_cast<const double*>(s->ws + l.linv_off);
-  double* side = reinterpret_cast<double*>(s->ws + l.side_off);
-  const int nbi = s->ctx->nbi;
+  const int nbo = s->ctx->nbo, nbi = s->ctx->nbi;
   // predictor (affine scaling) direction
   HIP_OK(qp_rhs(q, st));
-  HIP_OK(ldlt_solve(s->K, s->ldk, s->N, s->D, Linv, nbi, q.b, side, st));
+  HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, nbo, nbi, q.b, st));
   mark(3);
   HIP_OK(qp_backsub(q, q.daff, st));
   HIP_OK(qp_ratio(q, q.daff, SC_ALPHA_AFF, st));
@@ -345,7 +360,7 @@ int run_step(ipmz_qp* s, int flags) {
   HIP_OK(qp_corrector_residuals(q, st));
   HIP_OK(qp_rhs(q, st));
   mark(4);
-  HIP_OK(ldlt_solve(s->K, s->ldk, s->N, s->D, Linv, nbi, q.b, side, st));
+  HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, nbo, nbi, q.b, st));
   mark(5);
   HIP_OK(qp_backsub(q, q.dir, st));
   HIP_OK(qp_ratio(q, q.dir, SC_ALPHA, st));

@@ -34,6 +34,11 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,
                       double* side, hipStream_t st);
 
+// trsv_persist.hip: the same solve as ONE persistent launch (nbi == 64);
+// ybuf, zbuf: N doubles; ctrl: 2 + 2*ceil(N/64) unsigned (zeroed inside).
+hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
+                                 double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st);
+
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
 

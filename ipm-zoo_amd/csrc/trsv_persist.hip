@@ -1,0 +1,213 @@
+// Single-launch, sync-free triangular solve with the LDL^T factor:
+//   x = L^{-T} D^{-1} L^{-1} b   (LinearSolvers.cpp:44-74)
+//
+// The forward sweep (Ly = b, z = y / D) and the backward sweep (L^T x = z)
+// are 2 * nblk "tickets" of NB-row blocks, claimed in dependency order from
+// a device counter by whichever workgroup is running (dequeue pattern): a
+// ticket only ever waits on LOWER tickets, all of which belong to running
+// workgroups, so the grid cannot deadlock whatever the dispatch order.
+//
+//   forward block J  : v = b_J - sum_{K<J} L_JK y_K ; y_J = Linv_J v ;
+//                      z_J = y_J / D_J                      -> flag F[J]
+//   backward block J : u = z_J - sum_{K>J} L_KJ^T x_K ; x_J = Linv_J^T u
+//                                                          -> flag B[J]
+// Every off-diagonal tile is streamed into registers BEFORE the flag it
+// needs is polled, so the critical path per block is one hand-off plus one
+// NB x NB tile product plus the diagonal-block apply.
+//
+// Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, "Valid forms"
+// row 1): block vectors are stored write-through (sc1: relaxed agent-scope
+// atomic stores), every storing wave drains vmcnt(0), a workgroup barrier,
+// then ONE lane stores the flag with a relaxed agent-scope atomic; consumers
+// poll the flag with relaxed agent-scope loads and read the vectors with sc1
+// loads only.  Flags are zeroed by a memset node before every launch.  Spins
+// are bounded: on timeout the kernel records an error word and gives up.
+#include "common.h"
+#include "kernels.h"
+
+namespace ipmz {
+
+namespace {
+constexpr int PNT = 256;                 // threads per workgroup
+constexpr unsigned SPIN_LIMIT = 1u << 24;  // ~ seconds at s_sleep(2): far beyond any legitimate wait
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane of the workgroup polls; everyone leaves together
+__device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned* err, unsigned* sh_ok) {
+  if (threadIdx.x == 0) {
+    unsigned spins = 0, ok = 1;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > SPIN_LIMIT ||
+          __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *sh_ok = ok;
+  }
+  __syncthreads();
+  return *sh_ok != 0;
+}
+
+__device__ __forceinline__ void publish(unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// quad (4-lane) all-reduce on the VALU
+__device__ __forceinline__ double quad_sum(double v) {
+  v += dpp_double<0xb1>(v);
+  v += dpp_double<0x4e>(v);
+  return v;
+}
+}  // namespace
+
+// NB = 64: forward tiles are read row-wise (thread t: row t>>2, 16 columns
+// (t&3)*16..+16 -> 8 x 16-byte loads), backward tiles column-wise (thread t:
+// column t&63, rows (t>>6)*16..+16).
+template <int NB>
+__global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __restrict__ K, int64_t ld, int N,
+                                                              const double* __restrict__ D,
+                                                              const double* __restrict__ Linv, double* b,
+                                                              double* ybuf, double* zbuf, unsigned* ctrl, int nblk) {
+  static_assert(NB == 64, "persistent solve is written for 64-row blocks");
+  __shared__ double vec[NB];      // y_K / x_K of the tile being applied, then v / u
+  __shared__ double red[4][NB];   // cross-wave reduction (backward)
+  __shared__ unsigned sh_ticket, sh_ok;
+  unsigned* counter = ctrl;
+  unsigned* err = ctrl + 1;
+  unsigned* fflag = ctrl + 2;
+  unsigned* bflag = ctrl + 2 + nblk;
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+
+  for (;;) {
+    if (tid == 0) sh_ticket = atomicAdd(counter, 1u);
+    __syncthreads();
+    const int ticket = (int)sh_ticket;
+    __syncthreads();
+    if (ticket >= 2 * nblk) return;
+
+    if (ticket < nblk) {
+      // ------------------------------------------------------------ forward
+      const int J = ticket, J0 = J * NB;
+      const int rows = N - J0 < NB ? N - J0 : NB;
+      const int r = tid >> 2, c0 = (tid & 3) * 16;
+      // diagonal-block inverse row r (Linv_J, NB x NB) and b_J[r]
+      double li[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) li[q] = Linv[(int64_t)J * NB * NB + r * NB + c0 + q];
+      double acc = 0.0;
+      double tile[16];
+      auto load_tile = [&](int Kb) {
+        const bool in = r < rows;
+        const double* p = K + (int64_t)(J0 + (in ? r : 0)) * ld + Kb * NB + c0;
+#pragma unroll
+        for (int q = 0; q < 16; q += 2) {
+          const double2 v2 = *reinterpret_cast<const double2*>(p + q);
+          tile[q] = in ? v2.x : 0.0;
+          tile[q + 1] = in ? v2.y : 0.0;
+        }
+      };
+      if (J > 0) load_tile(0);
+      for (int Kb = 0; Kb < J; ++Kb) {
+        if (!wait_flag(&fflag[Kb], err, &sh_ok)) return;
+        if (tid < NB) vec[tid] = ld_sc1(&ybuf[Kb * NB + tid]);
+        __syncthreads();
+        double cur[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cur[q] = tile[q];
+        if (Kb + 1 < J) load_tile(Kb + 1);  // next tile in flight during this product
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = fma(cur[q], vec[c0 + q], acc);
+        __syncthreads();
+      }
+      acc = quad_sum(acc);
+      const double bv = r < rows ? b[J0 + r] : 0.0;
+      if ((tid & 3) == 0) vec[r] = bv - acc;  // v = b_J - L_J,<J y
+      __syncthreads();
+      double y = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) y = fma(li[q], vec[c0 + q], y);
+      y = quad_sum(y);
+      if ((tid & 3) == 0 && r < rows) {
+        st_sc1(&ybuf[J0 + r], y);
+        st_sc1(&zbuf[J0 + r], y / D[J0 + r]);
+      }
+      publish(&fflag[J]);
+    } else {
+      // ----------------------------------------------------------- backward
+      const int J = nblk - 1 - (ticket - nblk), J0 = J * NB;
+      const int rows = N - J0 < NB ? N - J0 : NB;
+      const int c = lane, rq = wave * 16;
+      // Linv_J^T column c: Linv_J[rq + q][c]
+      double li[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) li[q] = Linv[(int64_t)J * NB * NB + (rq + q) * NB + c];
+      double acc = 0.0;
+      double tile[16];
+      auto load_tile = [&](int Kb) {  // L_KJ rows Kb*NB + rq.., column J0 + c
+        const int R0 = Kb * NB + rq;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int row = R0 + q;
+          tile[q] = (row < N && c < rows) ? K[(int64_t)row * ld + J0 + c] : 0.0;
+        }
+      };
+      if (J + 1 < nblk) load_tile(nblk - 1);
+      if (!wait_flag(&fflag[J], err, &sh_ok)) return;  // z_J ready
+      for (int Kb = nblk - 1; Kb > J; --Kb) {
+        if (!wait_flag(&bflag[Kb], err, &sh_ok)) return;
+        if (tid < NB) vec[tid] = (Kb * NB + tid < N) ? ld_sc1(&b[Kb * NB + tid]) : 0.0;
+        __syncthreads();
+        double cur[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) cur[q] = tile[q];
+        if (Kb - 1 > J) load_tile(Kb - 1);
+#pragma unroll
+        for (int q = 0; q < 16; ++q) acc = fma(cur[q], vec[rq + q], acc);
+        __syncthreads();
+      }
+      red[wave][c] = acc;
+      __syncthreads();
+      if (tid < NB) {
+        const double t = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        vec[tid] = tid < rows ? ld_sc1(&zbuf[J0 + tid]) - t : 0.0;  // u = z_J - sum L_KJ^T x_K
+      }
+      __syncthreads();
+      double x = 0.0;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) x = fma(li[q], vec[rq + q], x);
+      red[wave][c] = x;
+      __syncthreads();
+      if (tid < rows) st_sc1(&b[J0 + tid], (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]));
+      publish(&bflag[J]);
+    }
+  }
+}
+
+hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
+                                 double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st) {
+  if (N <= 0) return hipSuccess;
+  if (nbi != 64) return hipErrorInvalidValue;
+  const int nblk = (N + 63) / 64;
+  hipError_t e = hipMemsetAsync(ctrl, 0, (size_t)(2 + 2 * nblk) * sizeof(unsigned), st);
+  if (e != hipSuccess) return e;
+  // resident grid: 3 workgroups per CU fit (LDS ~2.6 KB, < 128 VGPRs); the
+  // dequeue makes residency a performance matter only
+  int grid = 2 * nblk < 512 ? 2 * nblk : 512;
+  hipLaunchKernelGGL((trsv_persistent_kernel<64>), dim3(grid), dim3(PNT), 0, st, K, ld, N, D, Linv, b, ybuf, zbuf,
+                     ctrl, nblk);
+  return hipGetLastError();
+}
+
+}  // namespace ipmz
