@@ -42,7 +42,22 @@ struct ipmz_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   int nbo = 256, nbi = 64;
+  // factorization look-ahead: panel path on sA (high priority), trailing
+  // updates on sB; forked from / joined to `stream` with events
+  hipStream_t sA = nullptr, sB = nullptr;
+  std::vector<hipEvent_t> evpool;
+  bool lookahead = true;
 };
+
+static int ensure_events(ipmz_ctx* ctx, size_t n) {
+  while (ctx->evpool.size() < n) {
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+      return fail(IPMZ_ERR_HIP, "hipEventCreate failed");
+    ctx->evpool.push_back(e);
+  }
+  return IPMZ_OK;
+}
 
 static int check_device(int device) {
   int count = 0;
@@ -73,6 +88,15 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
     return fail(IPMZ_ERR_HIP, "hipStreamCreate failed");
   }
   c->stream = c->own;
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (hipStreamCreateWithPriority(&c->sA, hipStreamNonBlocking, greatest) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess) {
+    ipmz_ctx_destroy(c);
+    return fail(IPMZ_ERR_HIP, "hipStreamCreateWithPriority failed");
+  }
+  const char* la = std::getenv("IPMZ_LOOKAHEAD");
+  c->lookahead = !(la && la[0] == '0');
   *out = c;
   return IPMZ_OK;
 }
@@ -80,8 +104,13 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
 int ipmz_ctx_destroy(ipmz_ctx* ctx) {
   if (!ctx) return IPMZ_OK;
   hipSetDevice(ctx->device);
-  hipStreamSynchronize(ctx->stream);
-  if (ctx->own) hipStreamDestroy(ctx->own);
+  if (ctx->stream) hipStreamSynchronize(ctx->stream);
+  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB})
+    if (s) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
+  for (auto e : ctx->evpool) hipEventDestroy(e);
   delete ctx;
   return IPMZ_OK;
 }
@@ -127,7 +156,7 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   l.side_off = 256;
   l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
-  l.y_off = l.w_off + round_up((int64_t)N * nbo * 8, 256);
+  l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)
   l.z_off = l.y_off + round_up((int64_t)N * 8, 256);
   l.ctrl_off = l.z_off + round_up((int64_t)N * 8, 256);
   l.total = l.ctrl_off + round_up((2 + 2 * ((int64_t)N + 63) / 64) * 4, 256);
@@ -159,9 +188,26 @@ int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N) {
 static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, char* ws, TrailTimer* timer) {
   const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
   int* info = reinterpret_cast<int*>(ws + l.info_off);
+  double* Linv = reinterpret_cast<double*>(ws + l.linv_off);
+  double* W = reinterpret_cast<double*>(ws + l.w_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
-  HIP_OK(ldlt_factor(K, ld, N, D, reinterpret_cast<double*>(ws + l.linv_off), reinterpret_cast<double*>(ws + l.w_off),
-                     ctx->nbo, ctx->nbi, info, ctx->stream, timer));
+  const int npan = (N + ctx->nbo - 1) / ctx->nbo;
+  if (!ctx->lookahead || npan < 3) {
+    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->stream, timer));
+    return IPMZ_OK;
+  }
+  const int nev = 2 * npan + 4;
+  int rc = ensure_events(ctx, (size_t)nev);
+  if (rc) return rc;
+  hipEvent_t* ev = ctx->evpool.data();
+  // fork: A (panel path) and B (trailing updates) start after the caller's stream
+  HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
+  HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
+  HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
+  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2));
+  // join (A has already waited for B's tail)
+  HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
+  HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
   return IPMZ_OK;
 }
 

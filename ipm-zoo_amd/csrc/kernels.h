@@ -18,8 +18,11 @@ struct TrailTimer {  // HIP-event pairs around every trailing-update launch
   double flops = 0.0;
   hipEvent_t* next() { return used < cap ? pairs[used++] : nullptr; }
 };
+// Two-stream look-ahead when st2 and ev (>= 2*ceil(N/nbo)+2 events) are
+// given; W must then hold 3 * N * nbo doubles (else N * nbo).
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
-                       int* info, hipStream_t st, TrailTimer* timer = nullptr);
+                       int* info, hipStream_t st, TrailTimer* timer = nullptr, hipStream_t st2 = nullptr,
+                       hipEvent_t* ev = nullptr, int nev = 0);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
 hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st);

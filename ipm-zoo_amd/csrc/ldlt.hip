@@ -456,64 +456,131 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 }
 
 // ---------------------------------------------------------------------------
-hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
-                       int* info, hipStream_t st, TrailTimer* timer) {
-  if (N <= 0) return hipSuccess;
-  if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
-  if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
+// Factor the outer panel [k0, k0 + bo): inner diag / TRSM / strip steps, all
+// on stream st.  Writes L (in K), D, the L11^{-1} blocks and W = L D for
+// the panel's rows below each inner block (W: N x nbo, this panel's buffer).
+static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo,
+                               int nbo, int nbi, int* info, hipStream_t st) {
   hipError_t e = hipSuccess;
-  for (int k0 = 0; k0 < N; k0 += nbo) {
-    const int bo = N - k0 < nbo ? N - k0 : nbo;
-    for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
-      const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
-      double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
-      if (nbi == 128)
-        hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info);
-      else
-        hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info);
-      if ((e = hipGetLastError()) != hipSuccess) return e;
-      const int r1 = j0 + bi;
-      if (r1 >= N) continue;
-      // panel: rows [r1, N), output W[:, j0-k0 ..], L21 in place
-      GemmArgs g{};
-      g.M = N - r1;
-      g.N = bi;
-      g.Kd = bi;
-      g.A = K + (int64_t)r1 * ld + j0;
-      g.lda = ld;
-      g.B = Lb;
-      g.ldb = nbi;
-      g.C = K + (int64_t)r1 * ld + j0;
-      g.ldc = ld;
-      g.W = W + (int64_t)r1 * nbo + (j0 - k0);
-      g.ldw = nbo;
-      g.dvec = D + j0;
-      g.lower = 0;
-      e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL, 2, 4>(g, st) : launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st);
-      if (e != hipSuccess) return e;
-      // strip update of the remaining columns of this outer panel
-      const int c1 = k0 + bo;
-      if (r1 < c1) {
-        e = gemm_nt_sub(N - r1, c1 - r1, bi, W + (int64_t)r1 * nbo + (j0 - k0), nbo, K + (int64_t)r1 * ld + j0,
-                        ld, K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st);
-        if (e != hipSuccess) return e;
-      }
-    }
-    const int t0 = k0 + bo;
-    if (t0 < N) {
-      hipEvent_t* ev = timer ? timer->next() : nullptr;
-      if (ev) hipEventRecord(ev[0], st);
-      e = gemm_nt_sub(N - t0, N - t0, bo, W + (int64_t)t0 * nbo, nbo, K + (int64_t)t0 * ld + k0, ld,
-                      K + (int64_t)t0 * ld + t0, ld, t0, t0, true, st);
-      if (ev) hipEventRecord(ev[1], st);
-      if (timer) {
-        const double R = (double)(N - t0);
-        timer->flops += R * (R + 1.0) * (double)bo;  // lower triangle incl. diagonal, 2 flops per FMA
-      }
+  for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
+    const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
+    double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
+    if (nbi == 128)
+      hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info);
+    else
+      hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const int r1 = j0 + bi;
+    if (r1 >= N) continue;
+    // panel TRSM: rows [r1, N): T = A21 L11^{-T}, W21 = T, L21 = T / D1
+    GemmArgs g{};
+    g.M = N - r1;
+    g.N = bi;
+    g.Kd = bi;
+    g.A = K + (int64_t)r1 * ld + j0;
+    g.lda = ld;
+    g.B = Lb;
+    g.ldb = nbi;
+    g.C = K + (int64_t)r1 * ld + j0;
+    g.ldc = ld;
+    g.W = W + (int64_t)r1 * nbo + (j0 - k0);
+    g.ldw = nbo;
+    g.dvec = D + j0;
+    g.lower = 0;
+    e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL, 2, 4>(g, st) : launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st);
+    if (e != hipSuccess) return e;
+    // strip update of the remaining columns of this outer panel
+    const int c1 = k0 + bo;
+    if (r1 < c1) {
+      e = gemm_nt_sub(N - r1, c1 - r1, bi, W + (int64_t)r1 * nbo + (j0 - k0), nbo, K + (int64_t)r1 * ld + j0, ld,
+                      K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st);
       if (e != hipSuccess) return e;
     }
   }
   return hipSuccess;
+}
+
+// Rank-bo update of the column block [c0, c1) (rows >= c0) with outer panel
+// k (W_k rows, L_k = K[:, k0:k0+bo)); square = the whole trailing triangle.
+static hipError_t panel_update(double* K, int64_t ld, int N, const double* Wk, int nbo, int k0, int bo, int c0,
+                               int c1, bool square, hipStream_t st) {
+  if (c0 >= c1 || c0 >= N) return hipSuccess;
+  return gemm_nt_sub(N - c0, c1 - c0, bo, Wk + (int64_t)c0 * nbo, nbo, K + (int64_t)c0 * ld + k0, ld,
+                     K + (int64_t)c0 * ld + c0, ld, c0, c0, square, st);
+}
+
+// Blocked LDL^T with depth-1 look-ahead on two streams (Ws: 3 buffers of
+// N x nbo).  With P_k the k-th outer panel:
+//   stream A (st): [wait N_{k-1}] update P_{k+1} with P_k ; factor P_{k+1}
+//   stream B (st2): [wait P_k] update P_{k+2} with P_k -> event N_k ;
+//                   update everything beyond P_{k+2} with P_k (the big
+//                   trailing GEMM, overlapping A's panel factorization)
+// Correctness: P_{k+1}'s columns get panel j <= k-1 contributions from B
+// (ordered on B before N_{k-1}) and panel k's from A; B never touches the
+// columns A is factoring; W is triple-buffered so A's P_{k+1} never
+// overwrites the W_{k-2} a late B_{k-2} could still read (B_{k-2} precedes
+// N_{k-1} on B).  A waits for B's tail at the end.
+hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
+                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev) {
+  if (N <= 0) return hipSuccess;
+  if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
+  if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
+  const int npan = (N + nbo - 1) / nbo;
+  const bool two = st2 != nullptr && ev != nullptr && nev >= 2 * npan + 2;
+  const int64_t wsz = (int64_t)N * nbo;
+  auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };
+  auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
+  hipError_t e = factor_panel(K, ld, N, D, Linv, Wb(0), 0, pw(0), nbo, nbi, info, st);
+  if (e != hipSuccess) return e;
+  if (!two) {  // single stream: factor, then the whole trailing update
+    for (int k = 0; k < npan; ++k) {
+      const int k0 = k * nbo, bo = pw(k), t0 = k0 + bo;
+      if (t0 < N) {
+        hipEvent_t* te = timer ? timer->next() : nullptr;
+        if (te) hipEventRecord(te[0], st);
+        e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, t0, N, true, st);
+        if (te) hipEventRecord(te[1], st);
+        if (timer) timer->flops += (double)(N - t0) * (double)(N - t0 + 1) * (double)bo;
+        if (e != hipSuccess) return e;
+        if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), t0, pw(k + 1), nbo, nbi, info, st)) != hipSuccess)
+          return e;
+      }
+    }
+    return hipSuccess;
+  }
+  hipEvent_t* evP = ev;         // panel k factored (A)
+  hipEvent_t* evN = ev + npan;  // P_{k+2} updated with P_k (B)
+  hipEvent_t evJoin = ev[2 * npan];
+  for (int k = 0; k < npan; ++k) {
+    const int k0 = k * nbo, bo = pw(k);
+    const int p1 = k0 + bo;                          // start of P_{k+1}
+    const int p2 = p1 < N ? p1 + pw(k + 1) : N;      // start of P_{k+2}
+    const int p3 = p2 < N ? p2 + pw(k + 2) : N;      // start of P_{k+3}
+    if (p1 >= N) break;
+    if ((e = hipEventRecord(evP[k], st)) != hipSuccess) return e;
+    // ---- stream B: P_{k+2} columns first, then the rest
+    if ((e = hipStreamWaitEvent(st2, evP[k], 0)) != hipSuccess) return e;
+    if (p2 < N) {
+      if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p2, p3, false, st2)) != hipSuccess) return e;
+    }
+    if ((e = hipEventRecord(evN[k], st2)) != hipSuccess) return e;
+    if (p3 < N) {
+      hipEvent_t* te = timer ? timer->next() : nullptr;
+      if (te) hipEventRecord(te[0], st2);
+      e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p3, N, true, st2);
+      if (te) hipEventRecord(te[1], st2);
+      if (timer) timer->flops += (double)(N - p3) * (double)(N - p3 + 1) * (double)bo;
+      if (e != hipSuccess) return e;
+    }
+    // ---- stream A: update P_{k+1} with P_k, factor P_{k+1}
+    if (k >= 1) {
+      if ((e = hipStreamWaitEvent(st, evN[k - 1], 0)) != hipSuccess) return e;
+    }
+    if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
+    if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), p1, pw(k + 1), nbo, nbi, info, st)) != hipSuccess) return e;
+  }
+  if ((e = hipEventRecord(evJoin, st2)) != hipSuccess) return e;
+  return hipStreamWaitEvent(st, evJoin, 0);
 }
 
 }  // namespace ipmz

@@ -55,7 +55,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&K, ld * N * 8));
   CK(hipMalloc(&D, N * 8));
   CK(hipMalloc(&Linv, (int64_t)(N + 127) / 64 * 128 * 128 * 8));
-  CK(hipMalloc(&W, (int64_t)N * 512 * 8));
+  CK(hipMalloc(&W, 3ll * N * 512 * 8));
   CK(hipMalloc(&b, N * 8));
   CK(hipMalloc(&side, 1024 * 8));
   CK(hipMalloc(&info, 64));
@@ -101,8 +101,25 @@ int main(int argc, char** argv) {
       std::printf("trailing nbo=%d R=%d: %.3f ms  %.2f TFLOP/s (algorithmic)\n", nbo, R, ms, fl / ms / 1e9);
     }
   }
-  // 2. full factor + solve per blocking
-  const int cfg[][2] = {{256, 64}, {256, 128}, {512, 64}, {512, 128}, {128, 64}};
+  // 2. full factor + solve per blocking, single stream and look-ahead
+  hipStream_t sB;
+  CK(hipStreamCreateWithFlags(&sB, hipStreamNonBlocking));
+  std::vector<hipEvent_t> ev(2 * (N / 64 + 2) + 8);
+  for (size_t i = 0; i < ev.size(); ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+  for (int nbo : {128, 256, 512}) {
+    for (int nbi : {64}) {
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, nbi, info, st, nullptr, sB, ev.data(), (int)ev.size()));
+      CK(hipStreamSynchronize(st));
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+      t.start(st);
+      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, nbi, info, st, nullptr, sB, ev.data(), (int)ev.size()));
+      const float fms = t.stop(st);
+      std::printf("look-ahead factor N=%d nbo=%d nbi=%d: %.3f ms = %.2f TFLOP/s (N^3/3)\n", N, nbo, nbi, fms,
+                  (double)N * N * N / 3.0 / fms / 1e9);
+    }
+  }
+  const int cfg[][2] = {{256, 64}, {512, 64}, {128, 64}};
   for (auto& c : cfg) {
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     CK(hipMemsetAsync(info, 0x7f, 4, st));
