@@ -165,6 +165,26 @@ int ipmz_qp_set_state(ipmz_qp* qp, const double* host_vars);
 int ipmz_qp_get_kkt(ipmz_qp* qp, double* host_K);
 int ipmz_qp_kkt_dim(ipmz_qp* qp);
 
+/* ---- batches of independent QPs (config C4) ------------------------------
+ * A batch is an ipmz_qp holding `batch` QPs of identical (n, m, p); every
+ * kernel launch serves the whole batch.  ipmz_qp_step / _generate (QP i gets
+ * seed + i) / _destroy / _set_timing / _phase_times apply to batches; the
+ * ipmz_qp_* state accessors address QP 0. */
+int ipmz_batch_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int batch, ipmz_qp** out);
+int ipmz_batch_size(ipmz_qp* qp);
+/* Copy QP `index`'s data (build_environment's validation); call
+ * ipmz_batch_initialize once every QP is loaded. */
+int ipmz_batch_load_host(ipmz_qp* qp, int index, const double* Q, const double* c, const double* A,
+                         const double* l_A, const double* u_A, const double* C, const double* d, const double* l_x,
+                         const double* u_x);
+int ipmz_batch_initialize(ipmz_qp* qp);
+/* out: host, batch * IPMZ_SC_COUNT doubles */
+int ipmz_batch_scalars(ipmz_qp* qp, double* out);
+int ipmz_batch_get_state(ipmz_qp* qp, int index, int which, double* host_out);
+int ipmz_batch_set_state(ipmz_qp* qp, int index, const double* host_vars);
+/* Step until every QP converged (converged QPs keep their iterate). */
+int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
+
 /* Phase timing (HIP events on the context stream; eager launches only).
  * ms: host array of IPMZ_PH_COUNT floats, cumulative since enable. */
 enum ipmz_phase {

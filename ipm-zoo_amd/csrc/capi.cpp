@@ -322,18 +322,27 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
 }  // extern "C"
 
 // ===========================================================================
-// Newton-step solver
+// Newton-step solver: B QPs with identical dimensions (B = 1 for ipmz_qp_*).
+// Every per-QP array lives in one allocation with a per-QP stride; the
+// kernels take a device array of QPDev descriptors and index it with
+// blockIdx.y, so one launch serves the whole batch.
 struct ipmz_qp {
   ipmz_ctx* ctx = nullptr;
-  int n = 0, m = 0, p = 0, N = 0;
+  int n = 0, m = 0, p = 0, N = 0, B = 1;
   int64_t ldn = 0, ldk = 0, state_len = 0;
   double delta = 1e-4;
   std::vector<void*> allocs;
-  QPDev q{};
+  std::vector<QPDev> hq;   // host copies of the descriptors
+  QPDev* dq = nullptr;     // device array of B descriptors
+  QPBatch qb{};
+  // factor storage
   double *K = nullptr, *D = nullptr;
-  char* ws = nullptr;
+  int64_t sK = 0, sD = 0, sb = 0;
+  char* ws = nullptr;      // B == 1: ws_layout(N) ; B > 1: see batch_ws
   int64_t ws_bytes = 0;
-  double *v0 = nullptr, *r0 = nullptr, *scal0 = nullptr;
+  double *bLinv = nullptr, *bW = nullptr;  // batched factor workspace (B > 1)
+  int* binfo = nullptr;
+  int64_t sL = 0, sW = 0;
   bool loaded = false;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
@@ -357,14 +366,14 @@ int64_t slot_len(const ipmz_qp* s, int slot) {
   }
 }
 
-template <typename T>
-int dev_alloc(ipmz_qp* s, T** p, int64_t count) {
+// one allocation of B x stride doubles (stride = per-QP count rounded to 64 B)
+double* dev_array(ipmz_qp* s, int64_t count, int64_t* stride_out = nullptr) {
+  const int64_t stride = round_up(count < 1 ? 1 : count, 8);
   void* ptr = nullptr;
-  const size_t bytes = (size_t)round_up(count < 1 ? 1 : count, 8) * sizeof(T);
-  if (hipMalloc(&ptr, bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "hipMalloc failed");
+  if (hipMalloc(&ptr, (size_t)(stride * s->B) * sizeof(double)) != hipSuccess) return nullptr;
   s->allocs.push_back(ptr);
-  *p = static_cast<T*>(ptr);
-  return IPMZ_OK;
+  if (stride_out) *stride_out = stride;
+  return static_cast<double*>(ptr);
 }
 
 // slot pointers into one contiguous Newton-order vector
@@ -376,43 +385,68 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
   }
 }
 
+QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
+
+int solve_batch(ipmz_qp* s, hipStream_t st) {
+  if (s->B == 1) {
+    HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, s->ctx->nbo, s->ctx->nbi, q0(s).b, st));
+  } else {
+    HIP_OK(ldlt_solve_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->ctx->nbi, q0(s).b, s->B, s->sK, s->sD, s->sL,
+                              s->sb, st));
+  }
+  return IPMZ_OK;
+}
+
+int factor_batch(ipmz_qp* s, TrailTimer* tt) {
+  if (s->B == 1) return factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, tt);
+  BatchStrides bs;
+  bs.B = s->B;
+  bs.sK = s->sK;
+  bs.sD = s->sD;
+  bs.sL = s->sL;
+  bs.sW = s->sW;
+  HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
+  HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, s->ctx->nbo, s->ctx->nbi, s->binfo,
+                             s->ctx->stream, bs));
+  return IPMZ_OK;
+}
+
 int run_step(ipmz_qp* s, int flags) {
   hipStream_t st = s->ctx->stream;
-  QPDev& q = s->q;
+  const QPBatch& qb = s->qb;
   const bool t = s->timing;
   auto mark = [&](int i) {
     if (t) hipEventRecord(s->ev[i], st);
   };
-  if (flags & IPMZ_STEP_RESTART_IF_CONVERGED)
-    HIP_OK(qp_restart_if_converged(q, s->v0, s->r0, s->scal0, s->state_len, st));
+  if (flags & IPMZ_STEP_RESTART_IF_CONVERGED) HIP_OK(qp_restart_if_converged(qb, st));
+  const int freeze = (flags & IPMZ_STEP_RESTART_IF_CONVERGED) ? 0 : 1;
   mark(0);
-  HIP_OK(qp_assemble(q, s->K, s->ldk, st));
+  HIP_OK(qp_assemble(qb, st));
   mark(1);
   TrailTimer tt;
   tt.pairs = s->tr_pairs;
   tt.cap = t ? s->tr_cap : 0;
-  int rc = factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, t ? &tt : nullptr);
+  int rc = factor_batch(s, t ? &tt : nullptr);
   if (rc) return rc;
   mark(2);
-  const int nbo = s->ctx->nbo, nbi = s->ctx->nbi;
   // predictor (affine scaling) direction
-  HIP_OK(qp_rhs(q, st));
-  HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, nbo, nbi, q.b, st));
+  HIP_OK(qp_rhs(qb, st));
+  if ((rc = solve_batch(s, st))) return rc;
   mark(3);
-  HIP_OK(qp_backsub(q, q.daff, st));
-  HIP_OK(qp_ratio(q, q.daff, SC_ALPHA_AFF, st));
-  HIP_OK(qp_mu_aff(q, st));
+  HIP_OK(qp_backsub(qb, 0, st));
+  HIP_OK(qp_ratio(qb, 0, SC_ALPHA_AFF, st));
+  HIP_OK(qp_mu_aff(qb, st));
   // centering-corrector direction
-  HIP_OK(qp_corrector_residuals(q, st));
-  HIP_OK(qp_rhs(q, st));
+  HIP_OK(qp_corrector_residuals(qb, st));
+  HIP_OK(qp_rhs(qb, st));
   mark(4);
-  HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, nbo, nbi, q.b, st));
+  if ((rc = solve_batch(s, st))) return rc;
   mark(5);
-  HIP_OK(qp_backsub(q, q.dir, st));
-  HIP_OK(qp_ratio(q, q.dir, SC_ALPHA, st));
-  HIP_OK(qp_update(q, st));
+  HIP_OK(qp_backsub(qb, 1, st));
+  HIP_OK(qp_ratio(qb, 1, SC_ALPHA, st));
+  HIP_OK(qp_update(qb, freeze, st));
   mark(6);
-  HIP_OK(qp_evaluate(q, st));
+  HIP_OK(qp_evaluate(qb, st));
   mark(7);
   if (t) {
     HIP_OK(hipStreamSynchronize(st));
@@ -431,31 +465,28 @@ int run_step(ipmz_qp* s, int flags) {
       s->ph_ms[IPMZ_PH_TRAILING] += ms;
     }
     s->tr_launches += tt.used;
-    s->tr_flops += tt.flops;
+    s->tr_flops += tt.flops * s->B;
   }
   return IPMZ_OK;
 }
 
 int evaluate_and_save(ipmz_qp* s) {
   hipStream_t st = s->ctx->stream;
-  HIP_OK(qp_evaluate(s->q, st));
-  HIP_OK(hipMemcpyAsync(s->v0, s->q.v[0], s->state_len * 8, hipMemcpyDeviceToDevice, st));
-  HIP_OK(hipMemcpyAsync(s->r0, s->q.r[0], s->state_len * 8, hipMemcpyDeviceToDevice, st));
-  HIP_OK(hipMemcpyAsync(s->scal0, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToDevice, st));
+  HIP_OK(qp_evaluate(s->qb, st));
+  HIP_OK(qp_save_initial(s->qb, st));
   s->loaded = true;
   return IPMZ_OK;
 }
-}  // namespace
 
-extern "C" {
-
-int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out) {
+int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out) {
   if (!ctx || !cfg || !out) return fail(IPMZ_ERR_INVALID, "null argument");
   *out = nullptr;
-  if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0) return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0");
+  if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0 || B <= 0)
+    return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
   HIP_OK(hipSetDevice(ctx->device));
   auto* s = new ipmz_qp();
   s->ctx = ctx;
+  s->B = B;
   s->n = cfg->n;
   s->m = cfg->m;
   s->p = cfg->p;
@@ -463,100 +494,130 @@ int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out) {
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->ldn = round_up(s->n, 8);
   s->ldk = round_up(s->N, 64);
-  s->state_len = 2 * (int64_t)s->n * 2 + s->n + 6 * (int64_t)s->m + 2 * (int64_t)s->p;  // 5n + 6m + 2p
   s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + 2 * (int64_t)s->p;
-  QPDev& q = s->q;
-  q.n = s->n;
-  q.m = s->m;
-  q.p = s->p;
-  q.N = s->N;
-  q.ldn = s->ldn;
-  q.delta = s->delta;
-  int rc = 0;
-  double *Q, *A, *C, *c, *lA, *uA, *d, *lx, *ux, *v, *r, *da, *di;
-  rc |= dev_alloc(s, &Q, (int64_t)s->n * s->ldn);
-  rc |= dev_alloc(s, &A, (int64_t)s->m * s->ldn);
-  rc |= dev_alloc(s, &C, (int64_t)s->p * s->ldn);
-  rc |= dev_alloc(s, &c, s->n);
-  rc |= dev_alloc(s, &lA, s->m);
-  rc |= dev_alloc(s, &uA, s->m);
-  rc |= dev_alloc(s, &d, s->p);
-  rc |= dev_alloc(s, &lx, s->n);
-  rc |= dev_alloc(s, &ux, s->n);
-  rc |= dev_alloc(s, &v, s->state_len);
-  rc |= dev_alloc(s, &r, s->state_len);
-  rc |= dev_alloc(s, &da, s->state_len);
-  rc |= dev_alloc(s, &di, s->state_len);
-  rc |= dev_alloc(s, &q.Qx, s->n);
-  rc |= dev_alloc(s, &q.ATl, s->n);
-  rc |= dev_alloc(s, &q.CTl, s->n);
-  rc |= dev_alloc(s, &q.Ax, s->m);
-  rc |= dev_alloc(s, &q.Cx, s->p);
-  rc |= dev_alloc(s, &q.b, s->N);
-  rc |= dev_alloc(s, &q.scal, SC_COUNT);
-  rc |= dev_alloc(s, &q.part, 4 * 1024);
-  rc |= dev_alloc(s, &q.tpart, (int64_t)((s->m > s->p ? s->m : s->p) + 127) / 128 * s->n + 8);
-  rc |= dev_alloc(s, &s->K, (int64_t)s->N * s->ldk);
-  rc |= dev_alloc(s, &s->D, s->N);
-  s->ws_bytes = ws_layout(s->N, ctx->nbo, ctx->nbi).total;
-  rc |= dev_alloc(s, &s->ws, s->ws_bytes);
-  rc |= dev_alloc(s, &s->v0, s->state_len);
-  rc |= dev_alloc(s, &s->r0, s->state_len);
-  rc |= dev_alloc(s, &s->scal0, SC_COUNT);
-  if (rc) {
+  const int n = s->n, m = s->m, p = s->p, N = s->N;
+  int64_t sQ, sA, sC, sn, sm, sp, sS, sNb, sScal, sPart, sT;
+  double* Q = dev_array(s, (int64_t)n * s->ldn, &sQ);
+  double* A = dev_array(s, (int64_t)m * s->ldn, &sA);
+  double* C = dev_array(s, (int64_t)p * s->ldn, &sC);
+  double* c = dev_array(s, n, &sn);
+  double* lx = dev_array(s, n);
+  double* ux = dev_array(s, n);
+  double* Qx = dev_array(s, n);
+  double* ATl = dev_array(s, n);
+  double* CTl = dev_array(s, n);
+  double* lA = dev_array(s, m, &sm);
+  double* uA = dev_array(s, m);
+  double* Ax = dev_array(s, m);
+  double* d = dev_array(s, p, &sp);
+  double* Cx = dev_array(s, p);
+  double* v = dev_array(s, s->state_len, &sS);
+  double* r = dev_array(s, s->state_len);
+  double* da = dev_array(s, s->state_len);
+  double* di = dev_array(s, s->state_len);
+  double* v0 = dev_array(s, s->state_len);
+  double* r0 = dev_array(s, s->state_len);
+  double* bvec = dev_array(s, N, &sNb);
+  double* scal = dev_array(s, SC_COUNT, &sScal);
+  double* scal0 = dev_array(s, SC_COUNT);
+  double* part = dev_array(s, 4 * 1024, &sPart);
+  double* tpart = dev_array(s, (int64_t)((m > p ? m : p) + 127) / 128 * n + 8, &sT);
+  s->K = dev_array(s, (int64_t)N * s->ldk, &s->sK);
+  s->D = dev_array(s, N, &s->sD);
+  s->sb = sNb;
+  bool ok = Q && A && C && c && lx && ux && Qx && ATl && CTl && lA && uA && Ax && d && Cx && v && r && da && di &&
+            v0 && r0 && bvec && scal && scal0 && part && tpart && s->K && s->D;
+  if (ok && B == 1) {
+    s->ws_bytes = ws_layout(N, ctx->nbo, ctx->nbi).total;
+    void* w = nullptr;
+    ok = hipMalloc(&w, (size_t)s->ws_bytes) == hipSuccess;
+    if (ok) s->allocs.push_back(w);
+    s->ws = static_cast<char*>(w);
+  } else if (ok) {
+    const int64_t nblk = (N + ctx->nbi - 1) / ctx->nbi;
+    s->bLinv = dev_array(s, nblk * ctx->nbi * ctx->nbi, &s->sL);
+    s->bW = dev_array(s, (int64_t)N * ctx->nbo, &s->sW);
+    void* w = nullptr;
+    ok = s->bLinv && s->bW && hipMalloc(&w, 256) == hipSuccess;
+    if (ok) s->allocs.push_back(w);
+    s->binfo = static_cast<int*>(w);
+  }
+  if (!ok) {
     ipmz_qp_destroy(s);
     return fail(IPMZ_ERR_NOMEM, "device allocation failed");
   }
-  q.Q = Q;
-  q.A = A;
-  q.C = C;
-  q.c = c;
-  q.lA = lA;
-  q.uA = uA;
-  q.d = d;
-  q.lx = lx;
-  q.ux = ux;
-  carve(s, v, q.v);
-  carve(s, r, q.r);
-  carve(s, da, q.daff);
-  carve(s, di, q.dir);
-  HIP_OK(hipMemsetAsync(q.scal, 0, SC_COUNT * 8, ctx->stream));
-  HIP_OK(hipMemsetAsync(s->K, 0, (size_t)s->N * s->ldk * 8, ctx->stream));
+  s->hq.resize(B);
+  for (int i = 0; i < B; ++i) {
+    QPDev& q = s->hq[i];
+    q = QPDev{};
+    q.n = n;
+    q.m = m;
+    q.p = p;
+    q.N = N;
+    q.ldn = s->ldn;
+    q.ldk = s->ldk;
+    q.state_len = s->state_len;
+    q.delta = s->delta;
+    q.Q = Q + i * sQ;
+    q.A = A + i * sA;
+    q.C = C + i * sC;
+    q.c = c + i * sn;
+    q.lx = lx + i * sn;
+    q.ux = ux + i * sn;
+    q.Qx = Qx + i * sn;
+    q.ATl = ATl + i * sn;
+    q.CTl = CTl + i * sn;
+    q.lA = lA + i * sm;
+    q.uA = uA + i * sm;
+    q.Ax = Ax + i * sm;
+    q.d = d + i * sp;
+    q.Cx = Cx + i * sp;
+    carve(s, v + i * sS, q.v);
+    carve(s, r + i * sS, q.r);
+    carve(s, da + i * sS, q.daff);
+    carve(s, di + i * sS, q.dir);
+    q.v0 = v0 + i * sS;
+    q.r0 = r0 + i * sS;
+    q.b = bvec + i * sNb;
+    q.scal = scal + i * sScal;
+    q.scal0 = scal0 + i * sScal;
+    q.part = part + i * sPart;
+    q.tpart = tpart + i * sT;
+    q.K = s->K + i * s->sK;
+  }
+  void* dqp = nullptr;
+  if (hipMalloc(&dqp, sizeof(QPDev) * B) != hipSuccess) {
+    ipmz_qp_destroy(s);
+    return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  }
+  s->allocs.push_back(dqp);
+  s->dq = static_cast<QPDev*>(dqp);
+  HIP_OK(hipMemcpy(s->dq, s->hq.data(), sizeof(QPDev) * B, hipMemcpyHostToDevice));
+  s->qb = QPBatch{s->dq, s->hq[0], B};
+  HIP_OK(hipMemsetAsync(scal, 0, (size_t)sScal * B * 8, ctx->stream));
+  HIP_OK(hipMemsetAsync(s->K, 0, (size_t)s->sK * B * 8, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
   *out = s;
   return IPMZ_OK;
 }
 
-int ipmz_qp_destroy(ipmz_qp* s) {
-  if (!s) return IPMZ_OK;
-  hipSetDevice(s->ctx->device);
-  hipStreamSynchronize(s->ctx->stream);
-  if (s->gexec) hipGraphExecDestroy(s->gexec);
-  if (s->graph) hipGraphDestroy(s->graph);
-  for (auto e : s->ev) hipEventDestroy(e);
-  if (s->tr_pairs) {
-    for (int i = 0; i < s->tr_cap; ++i) {
-      hipEventDestroy(s->tr_pairs[i][0]);
-      hipEventDestroy(s->tr_pairs[i][1]);
-    }
-    delete[] s->tr_pairs;
-  }
-  for (void* p : s->allocs) hipFree(p);
-  delete s;
+int check_index(ipmz_qp* s, int i) {
+  if (!s || i < 0 || i >= s->B) return fail(IPMZ_ERR_INVALID, "QP index out of range");
   return IPMZ_OK;
 }
 
-int ipmz_qp_load_host(ipmz_qp* s, const double* Q, const double* c, const double* A, const double* lA,
-                      const double* uA, const double* C, const double* d, const double* lx, const double* ux) {
-  if (!s || !Q || !c || !lx || !ux || (s->m && (!A || !lA || !uA)) || (s->p && (!C || !d)))
-    return fail(IPMZ_ERR_INVALID, "ipmz_qp_load_host: missing data block");
+int load_one(ipmz_qp* s, int i, const double* Q, const double* c, const double* A, const double* lA, const double* uA,
+             const double* C, const double* d, const double* lx, const double* ux) {
+  if (!Q || !c || !lx || !ux || (s->m && (!A || !lA || !uA)) || (s->p && (!C || !d)))
+    return fail(IPMZ_ERR_INVALID, "load: missing data block");
   // EnvironmentBuilder.cpp:12-17 (the reference ASSERTs; here an error code)
-  for (int i = 0; i < s->n; ++i)
-    if (!(lx[i] < ux[i])) return fail(IPMZ_ERR_INVALID, "l_x < u_x violated at " + std::to_string(i));
-  for (int i = 0; i < s->m; ++i)
-    if (!(lA[i] <= uA[i])) return fail(IPMZ_ERR_INVALID, "l_A <= u_A violated at " + std::to_string(i));
+  for (int k = 0; k < s->n; ++k)
+    if (!(lx[k] < ux[k])) return fail(IPMZ_ERR_INVALID, "l_x < u_x violated at " + std::to_string(k));
+  for (int k = 0; k < s->m; ++k)
+    if (!(lA[k] <= uA[k])) return fail(IPMZ_ERR_INVALID, "l_A <= u_A violated at " + std::to_string(k));
   HIP_OK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  QPDev& q = s->q;
+  const QPDev& q = s->hq[i];
   const size_t rowb = (size_t)s->n * 8, ldb = (size_t)s->ldn * 8;
   HIP_OK(hipMemcpy2DAsync((void*)q.Q, ldb, Q, rowb, rowb, s->n, hipMemcpyHostToDevice, st));
   if (s->m) HIP_OK(hipMemcpy2DAsync((void*)q.A, ldb, A, rowb, rowb, s->m, hipMemcpyHostToDevice, st));
@@ -569,28 +630,11 @@ int ipmz_qp_load_host(ipmz_qp* s, const double* Q, const double* c, const double
     HIP_OK(hipMemcpyAsync((void*)q.uA, uA, (size_t)s->m * 8, hipMemcpyHostToDevice, st));
   }
   if (s->p) HIP_OK(hipMemcpyAsync((void*)q.d, d, (size_t)s->p * 8, hipMemcpyHostToDevice, st));
-  HIP_OK(qp_init_iterate(q, st));
-  int rc = evaluate_and_save(s);
-  if (rc) return rc;
   HIP_OK(hipStreamSynchronize(st));
   return IPMZ_OK;
 }
 
-int ipmz_qp_generate(ipmz_qp* s, uint64_t seed) {
-  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
-  HIP_OK(hipSetDevice(s->ctx->device));
-  hipStream_t st = s->ctx->stream;
-  QPDev& q = s->q;
-  HIP_OK(qp_generate(s->n, s->m, s->p, s->ldn, seed, (double*)q.Q, (double*)q.c, (double*)q.A, (double*)q.lA,
-                     (double*)q.uA, (double*)q.C, (double*)q.d, (double*)q.lx, (double*)q.ux, st));
-  HIP_OK(qp_init_iterate(q, st));
-  int rc = evaluate_and_save(s);
-  if (rc) return rc;
-  HIP_OK(hipStreamSynchronize(st));
-  return IPMZ_OK;
-}
-
-int ipmz_qp_step(ipmz_qp* s, int flags) {
+int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (!(flags & IPMZ_STEP_GRAPH) || s->timing) return run_step(s, flags);
@@ -617,31 +661,99 @@ int ipmz_qp_step(ipmz_qp* s, int flags) {
   return IPMZ_OK;
 }
 
-int ipmz_qp_scalars(ipmz_qp* s, double* out) {
-  if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+int scalars_impl(ipmz_qp* s, double* out) {
   HIP_OK(hipSetDevice(s->ctx->device));
-  HIP_OK(hipMemcpyAsync(out, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+  for (int i = 0; i < s->B; ++i)
+    HIP_OK(hipMemcpyAsync(out + (int64_t)i * SC_COUNT, s->hq[i].scal, SC_COUNT * 8, hipMemcpyDeviceToHost,
+                          s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   return IPMZ_OK;
 }
 
+int get_state_impl(ipmz_qp* s, int i, int which, double* out) {
+  if (which < 0 || which > 3 || !out) return fail(IPMZ_ERR_INVALID, "bad arguments");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  const QPDev& q = s->hq[i];
+  const double* src = which == 0 ? q.v[0] : which == 1 ? q.daff[0] : which == 2 ? q.dir[0] : q.r[0];
+  HIP_OK(hipMemcpyAsync(out, src, s->state_len * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out) { return create_solver(ctx, cfg, 1, out); }
+
+int ipmz_qp_destroy(ipmz_qp* s) {
+  if (!s) return IPMZ_OK;
+  hipSetDevice(s->ctx->device);
+  hipStreamSynchronize(s->ctx->stream);
+  if (s->gexec) hipGraphExecDestroy(s->gexec);
+  if (s->graph) hipGraphDestroy(s->graph);
+  for (auto e : s->ev) hipEventDestroy(e);
+  if (s->tr_pairs) {
+    for (int i = 0; i < s->tr_cap; ++i) {
+      hipEventDestroy(s->tr_pairs[i][0]);
+      hipEventDestroy(s->tr_pairs[i][1]);
+    }
+    delete[] s->tr_pairs;
+  }
+  for (void* p : s->allocs) hipFree(p);
+  delete s;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_load_host(ipmz_qp* s, const double* Q, const double* c, const double* A, const double* lA,
+                      const double* uA, const double* C, const double* d, const double* lx, const double* ux) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  for (int i = 0; i < s->B; ++i) {
+    int rc = load_one(s, i, Q, c, A, lA, uA, C, d, lx, ux);
+    if (rc) return rc;
+  }
+  HIP_OK(qp_init_iterate(s->qb, s->ctx->stream));
+  int rc = evaluate_and_save(s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_generate(ipmz_qp* s, uint64_t seed) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  hipStream_t st = s->ctx->stream;
+  HIP_OK(qp_generate(s->qb, seed, st));
+  HIP_OK(qp_init_iterate(s->qb, st));
+  int rc = evaluate_and_save(s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(st));
+  return IPMZ_OK;
+}
+
+int ipmz_qp_step(ipmz_qp* s, int flags) { return step_impl(s, flags); }
+
+int ipmz_qp_scalars(ipmz_qp* s, double* out) {
+  if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+  return scalars_impl(s, out);
+}
+
 int ipmz_qp_device_scalars(ipmz_qp* s, double** out) {
   if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
-  *out = s->q.scal;
+  *out = s->hq[0].scal;
   return IPMZ_OK;
 }
 
 int ipmz_qp_copy_scalars(ipmz_qp* s, double* dst) {
   if (!s || !dst) return fail(IPMZ_ERR_INVALID, "null argument");
   HIP_OK(hipSetDevice(s->ctx->device));
-  HIP_OK(hipMemcpyAsync(dst, s->q.scal, SC_COUNT * 8, hipMemcpyDeviceToDevice, s->ctx->stream));
+  HIP_OK(hipMemcpyAsync(dst, s->hq[0].scal, SC_COUNT * 8, hipMemcpyDeviceToDevice, s->ctx->stream));
   return IPMZ_OK;
 }
 
 int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   double sc[SC_COUNT];
-  int rc = ipmz_qp_scalars(s, sc);
+  int rc = scalars_impl(s, sc);
   if (rc) return rc;
   int it = 0;
   for (; it < max_iter; ++it) {  // Optimizer.cpp:127-135
@@ -654,9 +766,9 @@ int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
       row[3] = row[4] = row[5] = row[6] = 0.0;
     }
     if (sc[SC_CONVERGED] != 0.0) break;
-    rc = ipmz_qp_step(s, 0);
+    rc = step_impl(s, 0);
     if (rc) return rc;
-    rc = ipmz_qp_scalars(s, sc);
+    rc = scalars_impl(s, sc);
     if (rc) return rc;
     if (row) {
       row[3] = sc[SC_ALPHA_AFF];
@@ -672,19 +784,16 @@ int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
 int64_t ipmz_qp_state_len(ipmz_qp* s) { return s ? s->state_len : 0; }
 
 int ipmz_qp_get_state(ipmz_qp* s, int which, double* out) {
-  if (!s || !out || which < 0 || which > 3) return fail(IPMZ_ERR_INVALID, "bad arguments");
-  HIP_OK(hipSetDevice(s->ctx->device));
-  const double* src = which == 0 ? s->q.v[0] : which == 1 ? s->q.daff[0] : which == 2 ? s->q.dir[0] : s->q.r[0];
-  HIP_OK(hipMemcpyAsync(out, src, s->state_len * 8, hipMemcpyDeviceToHost, s->ctx->stream));
-  HIP_OK(hipStreamSynchronize(s->ctx->stream));
-  return IPMZ_OK;
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  return get_state_impl(s, 0, which, out);
 }
 
 int ipmz_qp_set_state(ipmz_qp* s, const double* in) {
   if (!s || !in) return fail(IPMZ_ERR_INVALID, "bad arguments");
   HIP_OK(hipSetDevice(s->ctx->device));
-  HIP_OK(hipMemcpyAsync(s->q.v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
-  HIP_OK(qp_evaluate(s->q, s->ctx->stream));
+  for (int i = 0; i < s->B; ++i)
+    HIP_OK(hipMemcpyAsync(s->hq[i].v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  HIP_OK(qp_evaluate(s->qb, s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   s->loaded = true;
   return IPMZ_OK;
@@ -696,7 +805,7 @@ int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
   if (!s || !out) return fail(IPMZ_ERR_INVALID, "bad arguments");
   HIP_OK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
-  HIP_OK(qp_assemble(s->q, s->K, s->ldk, st));
+  HIP_OK(qp_assemble(s->qb, st));
   HIP_OK(hipMemcpy2DAsync(out, (size_t)s->N * 8, s->K, s->ldk * 8, (size_t)s->N * 8, s->N, hipMemcpyDeviceToHost,
                           st));
   HIP_OK(hipStreamSynchronize(st));
@@ -711,7 +820,7 @@ int ipmz_qp_set_timing(ipmz_qp* s, int enable) {
   s->timing = enable != 0;
   if (s->timing && s->ev.empty()) {
     s->ev.resize(8);
-    for (auto& e : s->ev) HIP_OK(hipEventCreate(&e));
+    for (size_t i = 0; i < s->ev.size(); ++i) HIP_OK(hipEventCreate(&s->ev[i]));
     s->tr_cap = (s->N + 63) / 64 + 8;
     s->tr_pairs = new hipEvent_t[s->tr_cap][2];
     for (int i = 0; i < s->tr_cap; ++i) {
@@ -731,6 +840,65 @@ int ipmz_qp_phase_times(ipmz_qp* s, double* ms, double* flops, int64_t* launches
     for (int i = 0; i < IPMZ_PH_COUNT; ++i) ms[i] = s->ph_ms[i];
   if (flops) *flops = s->tr_flops;
   if (launches) *launches = s->tr_launches;
+  return IPMZ_OK;
+}
+
+// ---- batches of independent QPs (config C4) ---------------------------------
+int ipmz_batch_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int batch, ipmz_qp** out) {
+  return create_solver(ctx, cfg, batch, out);
+}
+int ipmz_batch_size(ipmz_qp* s) { return s ? s->B : 0; }
+int ipmz_batch_load_host(ipmz_qp* s, int index, const double* Q, const double* c, const double* A, const double* lA,
+                         const double* uA, const double* C, const double* d, const double* lx, const double* ux) {
+  int rc = check_index(s, index);
+  if (rc) return rc;
+  if ((rc = load_one(s, index, Q, c, A, lA, uA, C, d, lx, ux))) return rc;
+  return IPMZ_OK;
+}
+int ipmz_batch_initialize(ipmz_qp* s) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(qp_init_iterate(s->qb, s->ctx->stream));
+  int rc = evaluate_and_save(s);
+  if (rc) return rc;
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+int ipmz_batch_scalars(ipmz_qp* s, double* out) {
+  if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
+  return scalars_impl(s, out);
+}
+int ipmz_batch_get_state(ipmz_qp* s, int index, int which, double* out) {
+  int rc = check_index(s, index);
+  if (rc) return rc;
+  return get_state_impl(s, index, which, out);
+}
+int ipmz_batch_set_state(ipmz_qp* s, int index, const double* in) {
+  int rc = check_index(s, index);
+  if (rc) return rc;
+  if (!in) return fail(IPMZ_ERR_INVALID, "null state");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(hipMemcpyAsync(s->hq[index].v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  HIP_OK(qp_evaluate(s->qb, s->ctx->stream));
+  HIP_OK(hipStreamSynchronize(s->ctx->stream));
+  return IPMZ_OK;
+}
+// Steps until every QP converged or max_iter; a converged QP keeps its
+// iterate.  converged_count: host, may be NULL.
+int ipmz_batch_solve(ipmz_qp* s, int max_iter, int* iterations, int* converged_count) {
+  if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the batch first");
+  std::vector<double> sc((size_t)s->B * SC_COUNT);
+  int it = 0, nconv = 0;
+  for (;; ++it) {
+    int rc = scalars_impl(s, sc.data());
+    if (rc) return rc;
+    nconv = 0;
+    for (int i = 0; i < s->B; ++i) nconv += sc[(size_t)i * SC_COUNT + SC_CONVERGED] != 0.0;
+    if (nconv == s->B || it >= max_iter) break;
+    if ((rc = step_impl(s, 0))) return rc;
+  }
+  if (iterations) *iterations = it;
+  if (converged_count) *converged_count = nconv;
   return IPMZ_OK;
 }
 

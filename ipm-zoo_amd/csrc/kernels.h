@@ -8,6 +8,14 @@
 namespace ipmz {
 
 // ldlt.hip -------------------------------------------------------------------
+// Batched factorization: element strides between consecutive QPs' K, D,
+// L^{-1} blocks and W panels.
+struct BatchStrides {
+  int B = 1;
+  int64_t sK = 0, sD = 0, sL = 0, sW = 0;
+};
+hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
+                               int* info, hipStream_t st, const BatchStrides& bs);
 // In-place blocked LDL^T of the lower triangle of K (row-major, ld).
 // Linv: (ceil(N/nbi)) blocks of nbi x nbi (inverse unit-lower diagonal
 // blocks, consumed by ldlt_solve); W: N x nbo workspace.  info: device int,
@@ -28,7 +36,8 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
 hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st);
+                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
+                       const BatchStrides* bs = nullptr);
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                          double* C, int64_t ldc, hipStream_t st);
 
@@ -36,6 +45,10 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 // In-place b <- L^{-T} D^{-1} L^{-1} b; side: 2*nbi doubles of scratch.
 hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,
                       double* side, hipStream_t st);
+
+// one workgroup per QP of a batch (small N); b: batch of rhs, stride sb
+hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
+                              double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st);
 
 // trsv_persist.hip: the same solve as ONE persistent launch (nbi == 64);
 // ybuf, zbuf: N doubles; ctrl: 2 + 2*ceil(N/64) unsigned (zeroed inside).
@@ -64,6 +77,8 @@ struct QPDev {
   int n, m, p;
   int N;
   int64_t ldn;  // leading dimension of Q, A, C (multiple of 8)
+  int64_t ldk;  // leading dimension of K
+  int64_t state_len;
   double delta;
   // problem data (row-major, ld = ldn)
   const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;
@@ -76,23 +91,32 @@ struct QPDev {
   double* scal;   // SC_COUNT doubles
   double* part;   // reduction partials
   double* tpart;  // transposed-GEMV partials
+  double* K;      // KKT / factor (N x ldk)
+  double *v0, *r0, *scal0;  // initial iterate snapshot (benchmark restarts)
 };
 
-hipError_t qp_generate(int n, int m, int p, int64_t ld, uint64_t seed, double* Q, double* c, double* A, double* lA,
-                       double* uA, double* C, double* d, double* lx, double* ux, hipStream_t st);
-hipError_t qp_init_iterate(const QPDev& q, hipStream_t st);
+// A batch of QPs with identical (n, m, p): d = device array of B
+// descriptors (kernels index it with blockIdx.y), h = host copy of QP 0.
+struct QPBatch {
+  const QPDev* d;
+  QPDev h;
+  int B;
+};
+
+hipError_t qp_generate(const QPBatch& qb, uint64_t seed0, hipStream_t st);  // QP b: seed0 + b
+hipError_t qp_init_iterate(const QPBatch& qb, hipStream_t st);
 // residual vectors of the current iterate at mu = 0, plus f, res, mu,
 // converged into scal (the head of Optimizer.cpp:127-135)
-hipError_t qp_evaluate(const QPDev& q, hipStream_t st);
-hipError_t qp_assemble(const QPDev& q, double* K, int64_t ld, hipStream_t st);
-// predictor / corrector pieces
-hipError_t qp_rhs(const QPDev& q, hipStream_t st);
-hipError_t qp_backsub(const QPDev& q, double* const* dslots, hipStream_t st);
-hipError_t qp_ratio(const QPDev& q, double* const* dslots, int out_index, hipStream_t st);
-hipError_t qp_mu_aff(const QPDev& q, hipStream_t st);
-hipError_t qp_corrector_residuals(const QPDev& q, hipStream_t st);
-hipError_t qp_update(const QPDev& q, hipStream_t st);
-hipError_t qp_restart_if_converged(const QPDev& q, const double* saved_v, const double* saved_r,
-                                   const double* saved_scal, int64_t state_len, hipStream_t st);
+hipError_t qp_evaluate(const QPBatch& qb, hipStream_t st);
+hipError_t qp_assemble(const QPBatch& qb, hipStream_t st);
+// predictor / corrector pieces; which: 0 = affine direction, 1 = corrector
+hipError_t qp_rhs(const QPBatch& qb, hipStream_t st);
+hipError_t qp_backsub(const QPBatch& qb, int which, hipStream_t st);
+hipError_t qp_ratio(const QPBatch& qb, int which, int out_index, hipStream_t st);
+hipError_t qp_mu_aff(const QPBatch& qb, hipStream_t st);
+hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st);
+hipError_t qp_update(const QPBatch& qb, int freeze, hipStream_t st);
+hipError_t qp_restart_if_converged(const QPBatch& qb, hipStream_t st);
+hipError_t qp_save_initial(const QPBatch& qb, hipStream_t st);
 
 }  // namespace ipmz

@@ -44,8 +44,12 @@ namespace ipmz {
 template <int NB>
 __global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
                                                                 double* __restrict__ D, double* __restrict__ Linv,
-                                                                int* __restrict__ info) {
+                                                                int* __restrict__ info, int64_t sK, int64_t sD,
+                                                                int64_t sL) {
   constexpr int T = NB / 4, NT = T * T;
+  K += blockIdx.x * sK;  // batch: one workgroup per QP
+  D += blockIdx.x * sD;
+  Linv += blockIdx.x * sL;
   __shared__ double M[NB][NB + 1];  // coalesced staging in/out
   __shared__ double wsh[2][NB], lsh[2][NB], xsh[2][NB];
   __shared__ double dsh[NB];
@@ -208,6 +212,8 @@ struct GemmArgs {
   int64_t row0, col0;
   int lower;  // 0: full rectangle, 1: skip strictly-upper tiles, 2: triangular grid (row0==col0, BM==BN)
   int ntm, ntn;
+  // batch (blockIdx.y = QP): element strides between the QPs' operands
+  int64_t sA, sB, sC, sW, sD;
 };
 
 // Tile pipeline: one LDS buffer is computed while the next k-chunk sits in
@@ -258,6 +264,16 @@ struct TileLoader {
 template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
 __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g) {
   constexpr int BK = 16, PAD = 18, NTH = 64 * WGM * WGN;
+  if (blockIdx.y) {
+    const int64_t z = blockIdx.y;
+    g.A += z * g.sA;
+    g.B += z * g.sB;
+    g.C += z * g.sC;
+    if (EPI == EPI_PANEL) {
+      g.W += z * g.sW;
+      g.dvec += z * g.sD;
+    }
+  }
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
   __shared__ __attribute__((aligned(16))) double As[2][BM * PAD];
   __shared__ __attribute__((aligned(16))) double Bs[2][BN * PAD];
@@ -346,7 +362,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g)
 }
 
 template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
-static hipError_t launch_gemm(GemmArgs g, hipStream_t st) {
+static hipError_t launch_gemm(GemmArgs g, hipStream_t st, int batch = 1) {
   g.ntm = (g.M + BM - 1) / BM;
   g.ntn = (g.N + BN - 1) / BN;
   if (g.ntm == 0 || g.ntn == 0 || g.Kd == 0) return hipSuccess;
@@ -357,8 +373,8 @@ static hipError_t launch_gemm(GemmArgs g, hipStream_t st) {
     if (BM == BN) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
     else g.lower = 1;
   }
-  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN>), dim3((unsigned)nblk), dim3(64 * WGM * WGN), 0, st,
-                     g);
+  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN>), dim3((unsigned)nblk, (unsigned)batch),
+                     dim3(64 * WGM * WGN), 0, st, g);
   return hipGetLastError();
 }
 
@@ -416,8 +432,16 @@ hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc,
 
 // C[i][j] -= sum_k A[i][k] B[j][k] over the lower part of a trailing region.
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st) {
+                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
+                       const BatchStrides* bs) {
   GemmArgs g{};
+  int batch = 1;
+  if (bs && bs->B > 1) {
+    batch = bs->B;
+    g.sA = bs->sW;  // A is a W panel, B and C live in K
+    g.sB = bs->sK;
+    g.sC = bs->sK;
+  }
   g.M = M;
   g.N = N;
   g.Kd = Kd;
@@ -435,8 +459,8 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   // 128x128 tile, 8 waves as 2 x 4 (64 x 32 per wave, 128 VGPRs), 72 KB LDS:
   // two workgroups per CU = 4 waves per SIMD (kbench: 47 TFLOP/s = 60 % of
   // the fp64 MFMA peak at R = 11008, vs 25 with 4 waves of 64 x 64)
-  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st)
-                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st);
+  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st, batch)
+                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st, batch);
 }
 
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
@@ -460,15 +484,17 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 // on stream st.  Writes L (in K), D, the L11^{-1} blocks and W = L D for
 // the panel's rows below each inner block (W: N x nbo, this panel's buffer).
 static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo,
-                               int nbo, int nbi, int* info, hipStream_t st) {
+                               int nbo, int nbi, int* info, hipStream_t st, const BatchStrides* bs = nullptr) {
   hipError_t e = hipSuccess;
+  const int B = bs ? bs->B : 1;
+  const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
     double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
     if (nbi == 128)
-      hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info);
+      hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(B), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     else
-      hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info);
+      hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int r1 = j0 + bi;
     if (r1 >= N) continue;
@@ -487,13 +513,18 @@ static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* 
     g.ldw = nbo;
     g.dvec = D + j0;
     g.lower = 0;
-    e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL, 2, 4>(g, st) : launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st);
+    g.sA = sK;
+    g.sB = sL;
+    g.sC = sK;
+    g.sW = sW;
+    g.sD = sD;
+    e = nbi == 128 ? launch_gemm<128, 128, EPI_PANEL, 2, 4>(g, st, B) : launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st, B);
     if (e != hipSuccess) return e;
     // strip update of the remaining columns of this outer panel
     const int c1 = k0 + bo;
     if (r1 < c1) {
       e = gemm_nt_sub(N - r1, c1 - r1, bi, W + (int64_t)r1 * nbo + (j0 - k0), nbo, K + (int64_t)r1 * ld + j0, ld,
-                      K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st);
+                      K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st, bs);
       if (e != hipSuccess) return e;
     }
   }
@@ -503,10 +534,26 @@ static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* 
 // Rank-bo update of the column block [c0, c1) (rows >= c0) with outer panel
 // k (W_k rows, L_k = K[:, k0:k0+bo)); square = the whole trailing triangle.
 static hipError_t panel_update(double* K, int64_t ld, int N, const double* Wk, int nbo, int k0, int bo, int c0,
-                               int c1, bool square, hipStream_t st) {
+                               int c1, bool square, hipStream_t st, const BatchStrides* bs = nullptr) {
   if (c0 >= c1 || c0 >= N) return hipSuccess;
   return gemm_nt_sub(N - c0, c1 - c0, bo, Wk + (int64_t)c0 * nbo, nbo, K + (int64_t)c0 * ld + k0, ld,
-                     K + (int64_t)c0 * ld + c0, ld, c0, c0, square, st);
+                     K + (int64_t)c0 * ld + c0, ld, c0, c0, square, st, bs);
+}
+
+// Batch of B independent factorizations (same N), single stream: each
+// launch covers every QP (grid.y / grid.x = QP).  For small N (C4: 320).
+hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
+                               int* info, hipStream_t st, const BatchStrides& bs) {
+  if (N <= 0 || bs.B <= 0) return hipSuccess;
+  if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
+  if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
+  hipError_t e = hipSuccess;
+  for (int k0 = 0; k0 < N; k0 += nbo) {
+    const int bo = N - k0 < nbo ? N - k0 : nbo, t0 = k0 + bo;
+    if ((e = factor_panel(K, ld, N, D, Linv, W, k0, bo, nbo, nbi, info, st, &bs)) != hipSuccess) return e;
+    if (t0 < N && (e = panel_update(K, ld, N, W, nbo, k0, bo, t0, N, true, st, &bs)) != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // Blocked LDL^T with depth-1 look-ahead on two streams (Ws: 3 buffers of

@@ -49,7 +49,12 @@ __device__ __forceinline__ double block_min(double v, double* sh) {
 // ---------------------------------------------------------------------------
 // Generator, bit-identical to the oracle's generator.  Matrices are
 // written row-major with leading dimension n.
-__global__ void k_gen_Q(int n, int64_t ld, uint64_t seed, double* Q) {
+__global__ void k_gen_Q(const QPDev* __restrict__ qs, uint64_t seed0) {
+  const QPDev& q = qs[blockIdx.y];
+  const int n = q.n;
+  const int64_t ld = q.ldn;
+  const uint64_t seed = seed0 + blockIdx.y;
+  double* Q = const_cast<double*>(q.Q);
   const int64_t total = (int64_t)n * n;
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
     const int64_t i = t / n, j = t % n;
@@ -60,7 +65,12 @@ __global__ void k_gen_Q(int n, int64_t ld, uint64_t seed, double* Q) {
     Q[i * ld + j] = v;
   }
 }
-__global__ void k_gen_rect(int rows, int n, int64_t ld, uint64_t seed, uint64_t tag, double* M) {
+__global__ void k_gen_rect(const QPDev* __restrict__ qs, uint64_t seed0, int which) {
+  const QPDev& q = qs[blockIdx.y];
+  const int n = q.n, rows = which ? q.p : q.m;
+  const int64_t ld = q.ldn;
+  const uint64_t seed = seed0 + blockIdx.y, tag = which ? TAG_C_EQ : TAG_A;
+  double* M = const_cast<double*>(which ? q.C : q.A);
   const int64_t total = (int64_t)rows * n;
   const double sn = sqrt((double)n);
   for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < total; t += (int64_t)gridDim.x * NT) {
@@ -68,8 +78,12 @@ __global__ void k_gen_rect(int rows, int n, int64_t ld, uint64_t seed, uint64_t 
     M[i * ld + j] = (2.0 * ipmz_u01(seed, tag, i, j) - 1.0) / sn;
   }
 }
-__global__ void k_gen_vec(int n, int m, int p, uint64_t seed, double* c, double* lA, double* uA, double* d,
-                          double* lx, double* ux) {
+__global__ void k_gen_vec(const QPDev* __restrict__ qs, uint64_t seed0) {
+  const QPDev& q = qs[blockIdx.y];
+  const int n = q.n, m = q.m, p = q.p;
+  const uint64_t seed = seed0 + blockIdx.y;
+  double *c = const_cast<double*>(q.c), *lA = const_cast<double*>(q.lA), *uA = const_cast<double*>(q.uA);
+  double *d = const_cast<double*>(q.d), *lx = const_cast<double*>(q.lx), *ux = const_cast<double*>(q.ux);
   const int t = blockIdx.x * NT + threadIdx.x;
   if (t < n) {
     c[t] = 2.0 * ipmz_u01(seed, TAG_C, t, 0) - 1.0;
@@ -83,20 +97,32 @@ __global__ void k_gen_vec(int n, int m, int p, uint64_t seed, double* c, double*
   if (t < p) d[t] = (2.0 * ipmz_u01(seed, TAG_D, t, 0) - 1.0) * 0.1;
 }
 
-hipError_t qp_generate(int n, int m, int p, int64_t ld, uint64_t seed, double* Q, double* c, double* A, double* lA,
-                       double* uA, double* C, double* d, double* lx, double* ux, hipStream_t st) {
-  hipLaunchKernelGGL(k_gen_Q, dim3(2048), dim3(NT), 0, st, n, ld, seed, Q);
-  if (m) hipLaunchKernelGGL(k_gen_rect, dim3(1024), dim3(NT), 0, st, m, n, ld, seed, (uint64_t)TAG_A, A);
-  if (p) hipLaunchKernelGGL(k_gen_rect, dim3(1024), dim3(NT), 0, st, p, n, ld, seed, (uint64_t)TAG_C_EQ, C);
-  const int mx = n > m ? (n > p ? n : p) : (m > p ? m : p);
-  hipLaunchKernelGGL(k_gen_vec, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, n, m, p, seed, c, lA, uA, d, lx, ux);
+static inline int max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
+
+static dim3 grid2(int64_t x, int B) { return dim3((unsigned)(x < 1 ? 1 : x), (unsigned)B); }
+
+hipError_t qp_generate(const QPBatch& qb, uint64_t seed0, hipStream_t st) {
+  const QPDev& h = qb.h;
+  const int64_t gq = ((int64_t)h.n * h.n + NT - 1) / NT;
+  hipLaunchKernelGGL(k_gen_Q, grid2(gq < 2048 ? gq : 2048, qb.B), dim3(NT), 0, st, qb.d, seed0);
+  if (h.m) {
+    const int64_t g = ((int64_t)h.m * h.n + NT - 1) / NT;
+    hipLaunchKernelGGL(k_gen_rect, grid2(g < 1024 ? g : 1024, qb.B), dim3(NT), 0, st, qb.d, seed0, 0);
+  }
+  if (h.p) {
+    const int64_t g = ((int64_t)h.p * h.n + NT - 1) / NT;
+    hipLaunchKernelGGL(k_gen_rect, grid2(g < 1024 ? g : 1024, qb.B), dim3(NT), 0, st, qb.d, seed0, 1);
+  }
+  const int mx = max3(h.n, h.m, h.p);
+  hipLaunchKernelGGL(k_gen_vec, grid2((mx + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d, seed0);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // build_environment (EnvironmentBuilder.cpp:34-73): x = (l+u)/2, s = (l_A+u_A)/2,
 // every other slack and dual 1.
-__global__ void k_init_iterate(QPDev q) {
+__global__ void k_init_iterate(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
   const int t = blockIdx.x * NT + threadIdx.x;
   if (t < q.n) {
     q.v[X][t] = 0.5 * (q.lx[t] + q.ux[t]);
@@ -119,23 +145,29 @@ __global__ void k_init_iterate(QPDev q) {
   }
 }
 
-static inline int max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
-
-hipError_t qp_init_iterate(const QPDev& q, hipStream_t st) {
-  const int mx = max3(q.n, q.m, q.p);
-  hipLaunchKernelGGL(k_init_iterate, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, q);
+hipError_t qp_init_iterate(const QPBatch& qb, hipStream_t st) {
+  const int mx = max3(qb.h.n, qb.h.m, qb.h.p);
+  hipLaunchKernelGGL(k_init_iterate, grid2((mx + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // Dense matvecs (Evaluation.cpp:35-41 and the materialised transpose at
-// :126-140): out[i] = M[i,:] . x, one wave per row, 16-byte loads.
-__global__ __launch_bounds__(NT) void k_matvec_rows(const double* __restrict__ M, int rows, int cols, int64_t ld,
-                                                    const double* __restrict__ x, double* __restrict__ out) {
+// :126-140).  MV selects Q x -> Qx, A x -> Ax, C x -> Cx; one wave per row,
+// 16-byte loads; blockIdx.y = QP of the batch.
+enum { MV_Q = 0, MV_A = 1, MV_C = 2 };
+template <int MV>
+__global__ __launch_bounds__(NT) void k_matvec_rows(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  const int rows = MV == MV_Q ? q.n : MV == MV_A ? q.m : q.p;
+  const double* M = MV == MV_Q ? q.Q : MV == MV_A ? q.A : q.C;
+  double* out = MV == MV_Q ? q.Qx : MV == MV_A ? q.Ax : q.Cx;
+  const double* x = q.v[X];
+  const int cols = q.n;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const double* r = M + (int64_t)row * ld;
+  const double* r = M + (int64_t)row * q.ldn;
   double s0 = 0.0, s1 = 0.0;
   int j = lane * 2;
   for (; j + 1 < cols; j += 128) {
@@ -149,41 +181,51 @@ __global__ __launch_bounds__(NT) void k_matvec_rows(const double* __restrict__ M
   if (lane == 0) out[row] = s;
 }
 
-// out[j] = sum_i M[i][j] y[i]: column blocks of NT x row chunks of 128,
-// deterministic two-pass (chunk partials, then an ordered sum).
+// A^T lambda_A -> ATl, C^T lambda_C -> CTl: column blocks of NT x row chunks
+// of 128, deterministic two-pass (chunk partials, then an ordered sum).
 constexpr int TCHUNK = 128;
-__global__ __launch_bounds__(NT) void k_matvec_t_part(const double* __restrict__ M, int rows, int cols, int64_t ld,
-                                                      const double* __restrict__ y, double* __restrict__ part) {
+template <int MV>
+__global__ __launch_bounds__(NT) void k_matvec_t_part(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.z];
+  const int rows = MV == MV_A ? q.m : q.p, cols = q.n;
+  const double* M = MV == MV_A ? q.A : q.C;
+  const double* y = MV == MV_A ? q.v[LA] : q.v[LC];
   const int j = blockIdx.x * NT + threadIdx.x;
   const int i0 = blockIdx.y * TCHUNK;
   if (j >= cols) return;
   const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
   double s = 0.0;
-  for (int i = i0; i < i1; ++i) s += M[(int64_t)i * ld + j] * y[i];
-  part[(int64_t)blockIdx.y * cols + j] = s;
+  for (int i = i0; i < i1; ++i) s += M[(int64_t)i * q.ldn + j] * y[i];
+  q.tpart[(int64_t)blockIdx.y * cols + j] = s;
 }
-__global__ void k_sum_chunks(const double* __restrict__ part, int nchunk, int cols, double* __restrict__ out) {
+template <int MV>
+__global__ void k_sum_chunks(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  const int rows = MV == MV_A ? q.m : q.p, cols = q.n;
+  const int nchunk = (rows + TCHUNK - 1) / TCHUNK;
+  double* out = MV == MV_A ? q.ATl : q.CTl;
   const int j = blockIdx.x * NT + threadIdx.x;
   if (j >= cols) return;
   double s = 0.0;
-  for (int c = 0; c < nchunk; ++c) s += part[(int64_t)c * cols + j];
+  for (int c = 0; c < nchunk; ++c) s += q.tpart[(int64_t)c * cols + j];
   out[j] = s;
 }
 
-static hipError_t matvec_t(const double* M, int rows, int cols, int64_t ld, const double* y, double* out,
-                           double* tpart, hipStream_t st) {
+template <int MV>
+static void matvec_t(const QPBatch& qb, hipStream_t st) {
+  const QPDev& h = qb.h;
+  const int rows = MV == MV_A ? h.m : h.p;
   const int nchunk = (rows + TCHUNK - 1) / TCHUNK;
-  hipLaunchKernelGGL(k_matvec_t_part, dim3((cols + NT - 1) / NT, nchunk), dim3(NT), 0, st, M, rows, cols, ld, y,
-                     tpart);
-  hipLaunchKernelGGL(k_sum_chunks, dim3((cols + NT - 1) / NT), dim3(NT), 0, st, tpart, nchunk, cols, out);
-  return hipGetLastError();
+  hipLaunchKernelGGL((k_matvec_t_part<MV>), dim3((h.n + NT - 1) / NT, nchunk, qb.B), dim3(NT), 0, st, qb.d);
+  hipLaunchKernelGGL((k_sum_chunks<MV>), grid2((h.n + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
 }
 
 // ---------------------------------------------------------------------------
 // Shorthand residuals r_v := -rhs_v at mu (SymbolicOptimization.cpp:480-492),
 // plus per-block partials of ||rhs||^2, sum |complementarity|, and the two
 // objective sums (Optimizer.cpp:128-130).
-__global__ __launch_bounds__(NT) void k_residuals(QPDev q, double mu, int with_stats) {
+__global__ __launch_bounds__(NT) void k_residuals(const QPDev* __restrict__ qs, double mu, int with_stats) {
+  const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   double res2 = 0.0, comp = 0.0, fa = 0.0, fb = 0.0;
   const int n = q.n, m = q.m, p = q.p;
@@ -245,7 +287,8 @@ __global__ __launch_bounds__(NT) void k_residuals(QPDev q, double mu, int with_s
   if (threadIdx.x == 0) q.part[4 * blockIdx.x + 3] = a;
 }
 
-__global__ void k_stats_final(QPDev q, int nblocks) {
+__global__ void k_stats_final(const QPDev* __restrict__ qs, int nblocks) {
+  const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[4][NT];
   double s[4] = {0.0, 0.0, 0.0, 0.0};
   for (int b = threadIdx.x; b < nblocks; b += NT)
@@ -271,20 +314,20 @@ static int red_blocks(int total) {
   return b < 1 ? 1 : (b > RED_BLOCKS ? RED_BLOCKS : b);
 }
 
-hipError_t qp_evaluate(const QPDev& q, hipStream_t st) {
-  const int64_t ld = q.ldn;
-  hipLaunchKernelGGL(k_matvec_rows, dim3((q.n + 3) / 4), dim3(NT), 0, st, q.Q, q.n, q.n, ld, q.v[X], q.Qx);
-  if (q.m) {
-    hipLaunchKernelGGL(k_matvec_rows, dim3((q.m + 3) / 4), dim3(NT), 0, st, q.A, q.m, q.n, ld, q.v[X], q.Ax);
-    matvec_t(q.A, q.m, q.n, ld, q.v[LA], q.ATl, q.tpart, st);
+hipError_t qp_evaluate(const QPBatch& qb, hipStream_t st) {
+  const QPDev& h = qb.h;
+  hipLaunchKernelGGL((k_matvec_rows<MV_Q>), grid2((h.n + 3) / 4, qb.B), dim3(NT), 0, st, qb.d);
+  if (h.m) {
+    hipLaunchKernelGGL((k_matvec_rows<MV_A>), grid2((h.m + 3) / 4, qb.B), dim3(NT), 0, st, qb.d);
+    matvec_t<MV_A>(qb, st);
   }
-  if (q.p) {
-    hipLaunchKernelGGL(k_matvec_rows, dim3((q.p + 3) / 4), dim3(NT), 0, st, q.C, q.p, q.n, ld, q.v[X], q.Cx);
-    matvec_t(q.C, q.p, q.n, ld, q.v[LC], q.CTl, q.tpart, st);
+  if (h.p) {
+    hipLaunchKernelGGL((k_matvec_rows<MV_C>), grid2((h.p + 3) / 4, qb.B), dim3(NT), 0, st, qb.d);
+    matvec_t<MV_C>(qb, st);
   }
-  const int nb = red_blocks(q.n + q.m + q.p);
-  hipLaunchKernelGGL(k_residuals, dim3(nb), dim3(NT), 0, st, q, 0.0, 1);
-  hipLaunchKernelGGL(k_stats_final, dim3(1), dim3(NT), 0, st, q, nb);
+  const int nb = red_blocks(h.n + h.m + h.p);
+  hipLaunchKernelGGL(k_residuals, grid2(nb, qb.B), dim3(NT), 0, st, qb.d, 0.0, 1);
+  hipLaunchKernelGGL(k_stats_final, grid2(1, qb.B), dim3(NT), 0, st, qb.d, nb);
   return hipGetLastError();
 }
 
@@ -295,7 +338,10 @@ __device__ __forceinline__ double ds_inv(const QPDev& q, int i) {
   return ipmz_inv(ipmz_inv(q.v[G][i]) * q.v[LG][i] + ipmz_inv(q.v[H][i]) * q.v[LH][i]);
 }
 
-__global__ __launch_bounds__(NT) void k_assemble(QPDev q, double* __restrict__ K, int64_t ld) {
+__global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  double* __restrict__ K = q.K;
+  const int64_t ld = q.ldk;
   const int i = blockIdx.x;
   const int n = q.n, m = q.m;
   double* Kr = K + (int64_t)i * ld;
@@ -321,14 +367,15 @@ __global__ __launch_bounds__(NT) void k_assemble(QPDev q, double* __restrict__ K
   }
 }
 
-hipError_t qp_assemble(const QPDev& q, double* K, int64_t ld, hipStream_t st) {
-  hipLaunchKernelGGL(k_assemble, dim3(q.N), dim3(NT), 0, st, q, K, ld);
+hipError_t qp_assemble(const QPBatch& qb, hipStream_t st) {
+  hipLaunchKernelGGL(k_assemble, grid2(qb.h.N, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
 // Augmented rhs (formulations.txt, augmented system rhs rows 0..2).
-__global__ void k_rhs(QPDev q) {
+__global__ void k_rhs(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
   const int t = blockIdx.x * NT + threadIdx.x;
   const int n = q.n, m = q.m;
   if (t < n) {
@@ -347,17 +394,21 @@ __global__ void k_rhs(QPDev q) {
   }
 }
 
-hipError_t qp_rhs(const QPDev& q, hipStream_t st) {
-  hipLaunchKernelGGL(k_rhs, dim3((q.N + NT - 1) / NT), dim3(NT), 0, st, q);
+hipError_t qp_rhs(const QPBatch& qb, hipStream_t st) {
+  hipLaunchKernelGGL(k_rhs, grid2((qb.h.N + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 
 // Back-substitution of the eliminated variables (delta_definitions,
-// Optimizer.cpp:373-378).  dslots: the 13 output vectors.
-struct DSlots {
-  double* d[NSLOT];
+// Optimizer.cpp:373-378) into the affine (which = 0) or corrector (1) slots.
+struct DSel {
+  double* const* d;
 };
-__global__ void k_backsub(QPDev q, DSlots D) {
+__device__ __forceinline__ DSel dsel(const QPDev& q, int which) { return DSel{which ? q.dir : q.daff}; }
+
+__global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
+  const QPDev& q = qs[blockIdx.y];
+  const DSel D = dsel(q, which);
   const int t = blockIdx.x * NT + threadIdx.x;
   const int n = q.n, m = q.m;
   if (t < n) {
@@ -394,10 +445,8 @@ __global__ void k_backsub(QPDev q, DSlots D) {
   }
 }
 
-hipError_t qp_backsub(const QPDev& q, double* const* dslots, hipStream_t st) {
-  DSlots D;
-  for (int s = 0; s < NSLOT; ++s) D.d[s] = dslots[s];
-  hipLaunchKernelGGL(k_backsub, dim3((q.N + NT - 1) / NT), dim3(NT), 0, st, q, D);
+hipError_t qp_backsub(const QPBatch& qb, int which, hipStream_t st) {
+  hipLaunchKernelGGL(k_backsub, grid2((qb.h.N + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d, which);
   return hipGetLastError();
 }
 
@@ -405,7 +454,9 @@ hipError_t qp_backsub(const QPDev& q, double* const* dslots, hipStream_t st) {
 // get_max_step_ (Optimizer.cpp:270-342): fraction-to-boundary over the
 // non-negative Newton variables, plus explicit x bounds when neither g nor h
 // is a Newton variable (m == 0).
-__global__ __launch_bounds__(NT) void k_ratio_part(QPDev q, DSlots D) {
+__global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs, int which) {
+  const QPDev& q = qs[blockIdx.y];
+  const DSel D = dsel(q, which);
   __shared__ double sh[NT / 64];
   double a = 1.0;
   const int n = q.n, m = q.m;
@@ -437,7 +488,8 @@ __global__ __launch_bounds__(NT) void k_ratio_part(QPDev q, DSlots D) {
   a = block_min(a, sh);
   if (threadIdx.x == 0) q.part[blockIdx.x] = a;
 }
-__global__ void k_min_final(QPDev q, int nblocks, int out_index) {
+__global__ void k_min_final(const QPDev* __restrict__ qs, int nblocks, int out_index) {
+  const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   double a = 1.0;
   for (int b = threadIdx.x; b < nblocks; b += NT) a = fmin(a, q.part[b]);
@@ -445,17 +497,16 @@ __global__ void k_min_final(QPDev q, int nblocks, int out_index) {
   if (threadIdx.x == 0) q.scal[out_index] = a;
 }
 
-hipError_t qp_ratio(const QPDev& q, double* const* dslots, int out_index, hipStream_t st) {
-  DSlots D;
-  for (int s = 0; s < NSLOT; ++s) D.d[s] = dslots[s];
-  const int nb = red_blocks(q.n + q.m);
-  hipLaunchKernelGGL(k_ratio_part, dim3(nb), dim3(NT), 0, st, q, D);
-  hipLaunchKernelGGL(k_min_final, dim3(1), dim3(NT), 0, st, q, nb, out_index);
+hipError_t qp_ratio(const QPBatch& qb, int which, int out_index, hipStream_t st) {
+  const int nb = red_blocks(qb.h.n + qb.h.m);
+  hipLaunchKernelGGL(k_ratio_part, grid2(nb, qb.B), dim3(NT), 0, st, qb.d, which);
+  hipLaunchKernelGGL(k_min_final, grid2(1, qb.B), dim3(NT), 0, st, qb.d, nb, out_index);
   return hipGetLastError();
 }
 
 // mu at the affine trial point v + alpha_aff * daff (Optimizer.cpp:167-180).
-__global__ __launch_bounds__(NT) void k_mu_aff_part(QPDev q) {
+__global__ __launch_bounds__(NT) void k_mu_aff_part(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   const double al = q.scal[SC_ALPHA_AFF];
   double s = 0.0;
@@ -476,7 +527,8 @@ __global__ __launch_bounds__(NT) void k_mu_aff_part(QPDev q) {
   s = block_sum(s, sh);
   if (threadIdx.x == 0) q.part[blockIdx.x] = s;
 }
-__global__ void k_mu_aff_final(QPDev q, int nblocks) {
+__global__ void k_mu_aff_final(const QPDev* __restrict__ qs, int nblocks) {
+  const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   double s = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += NT) s += q.part[b];
@@ -492,15 +544,16 @@ __global__ void k_mu_aff_final(QPDev q, int nblocks) {
   }
 }
 
-hipError_t qp_mu_aff(const QPDev& q, hipStream_t st) {
-  const int nb = red_blocks(q.n + q.m);
-  hipLaunchKernelGGL(k_mu_aff_part, dim3(nb), dim3(NT), 0, st, q);
-  hipLaunchKernelGGL(k_mu_aff_final, dim3(1), dim3(NT), 0, st, q, nb);
+hipError_t qp_mu_aff(const QPBatch& qb, hipStream_t st) {
+  const int nb = red_blocks(qb.h.n + qb.h.m);
+  hipLaunchKernelGGL(k_mu_aff_part, grid2(nb, qb.B), dim3(NT), 0, st, qb.d);
+  hipLaunchKernelGGL(k_mu_aff_final, grid2(1, qb.B), dim3(NT), 0, st, qb.d, nb);
   return hipGetLastError();
 }
 
 // Corrector (Optimizer.cpp:183-209): r_v = (V lambda - mu_new e) + dV_aff dlambda_aff.
-__global__ void k_corrector(QPDev q) {
+__global__ void k_corrector(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
   const int t = blockIdx.x * NT + threadIdx.x;
   const double mu = q.scal[SC_MU_NEW];
   const int n = q.n, m = q.m;
@@ -518,13 +571,17 @@ __global__ void k_corrector(QPDev q) {
   q.r[c1][i] = (q.v[c1][i] * q.v[d1][i] + (-(mu * 1.0))) + (q.daff[c1][i] * q.daff[d1][i] + (-(0.0 * 1.0)));
 }
 
-hipError_t qp_corrector_residuals(const QPDev& q, hipStream_t st) {
-  hipLaunchKernelGGL(k_corrector, dim3((q.n + q.m + NT - 1) / NT), dim3(NT), 0, st, q);
+hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st) {
+  hipLaunchKernelGGL(k_corrector, grid2((qb.h.n + qb.h.m + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 
 // update_variables_(0.995 * alpha, ...) (Optimizer.cpp:216-231)
-__global__ void k_update(QPDev q) {
+// freeze != 0: a converged QP of a batch keeps its iterate (the reference
+// stops iterating it, Optimizer.cpp:133-135).
+__global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
+  const QPDev& q = qs[blockIdx.y];
+  if (freeze && q.scal[SC_CONVERGED] != 0.0) return;
   const int t = blockIdx.x * NT + threadIdx.x;
   const double s = 0.995 * q.scal[SC_ALPHA];
   const int n = q.n, m = q.m, p = q.p;
@@ -544,33 +601,49 @@ __global__ void k_update(QPDev q) {
   }
 }
 
-hipError_t qp_update(const QPDev& q, hipStream_t st) {
-  const int mx = max3(q.n, q.m, q.p);
-  hipLaunchKernelGGL(k_update, dim3((mx + NT - 1) / NT), dim3(NT), 0, st, q);
+hipError_t qp_update(const QPBatch& qb, int freeze, hipStream_t st) {
+  const int mx = max3(qb.h.n, qb.h.m, qb.h.p);
+  hipLaunchKernelGGL(k_update, grid2((mx + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d, freeze);
   return hipGetLastError();
 }
 
 // Benchmark restart: a converged iterate is reset (on device, no host sync)
 // to the saved initial state, so every timed step is a real Newton step.
-__global__ void k_restart_copy(const double* __restrict__ sv, const double* __restrict__ sr, double* v, double* r,
-                               const double* scal, int64_t len) {
-  if (scal[SC_CONVERGED] == 0.0) return;
-  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < len; t += (int64_t)gridDim.x * NT) {
-    v[t] = sv[t];
-    r[t] = sr[t];
+__global__ void k_restart_copy(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  if (q.scal[SC_CONVERGED] == 0.0) return;
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < q.state_len; t += (int64_t)gridDim.x * NT) {
+    q.v[0][t] = q.v0[t];
+    q.r[0][t] = q.r0[t];
   }
 }
-__global__ void k_restart_scal(const double* __restrict__ ss, double* scal) {
-  if (threadIdx.x != 0 || scal[SC_CONVERGED] == 0.0) return;
-  const double restarts = scal[SC_RESTARTS];
-  for (int k = 0; k < SC_RESTARTS; ++k) scal[k] = ss[k];
-  scal[SC_RESTARTS] = restarts + 1.0;
+__global__ void k_restart_scal(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  if (threadIdx.x != 0 || q.scal[SC_CONVERGED] == 0.0) return;
+  const double restarts = q.scal[SC_RESTARTS];
+  for (int k = 0; k < SC_RESTARTS; ++k) q.scal[k] = q.scal0[k];
+  q.scal[SC_RESTARTS] = restarts + 1.0;
 }
 
-hipError_t qp_restart_if_converged(const QPDev& q, const double* saved_v, const double* saved_r,
-                                   const double* saved_scal, int64_t state_len, hipStream_t st) {
-  hipLaunchKernelGGL(k_restart_copy, dim3(256), dim3(NT), 0, st, saved_v, saved_r, q.v[0], q.r[0], q.scal, state_len);
-  hipLaunchKernelGGL(k_restart_scal, dim3(1), dim3(64), 0, st, saved_scal, q.scal);
+hipError_t qp_restart_if_converged(const QPBatch& qb, hipStream_t st) {
+  const int64_t g = (qb.h.state_len + NT - 1) / NT;
+  hipLaunchKernelGGL(k_restart_copy, grid2(g < 256 ? g : 256, qb.B), dim3(NT), 0, st, qb.d);
+  hipLaunchKernelGGL(k_restart_scal, grid2(1, qb.B), dim3(64), 0, st, qb.d);
+  return hipGetLastError();
+}
+
+// snapshot of the initial iterate (restart source)
+__global__ void k_save_initial(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  for (int64_t t = blockIdx.x * (int64_t)NT + threadIdx.x; t < q.state_len; t += (int64_t)gridDim.x * NT) {
+    q.v0[t] = q.v[0][t];
+    q.r0[t] = q.r[0][t];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < SC_COUNT) q.scal0[threadIdx.x] = q.scal[threadIdx.x];
+}
+hipError_t qp_save_initial(const QPBatch& qb, hipStream_t st) {
+  const int64_t g = (qb.h.state_len + NT - 1) / NT;
+  hipLaunchKernelGGL(k_save_initial, grid2(g < 256 ? g : 256, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 

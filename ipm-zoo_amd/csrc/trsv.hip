@@ -250,4 +250,75 @@ hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const
   return hipErrorInvalidValue;
 }
 
+
+// ---------------------------------------------------------------------------
+// Batched solve for many small factors (config C4, N ~ 320): one workgroup
+// per QP walks its NB-row blocks itself (no inter-workgroup hand-offs):
+// forward  : y_J = Linv_J b_J ; z_J = y_J / D_J ; b_i -= L[i, J] y_J (i below J)
+// backward : x_J = Linv_J^T z_J ;                z_i -= L[J, i]^T x_J (i above J)
+template <int NB>
+__global__ __launch_bounds__(TRSV_NT) void trsv_batched_kernel(const double* __restrict__ K, int64_t ld, int N,
+                                                               const double* __restrict__ D,
+                                                               const double* __restrict__ Linv, double* b,
+                                                               int64_t sK, int64_t sD, int64_t sL, int64_t sb) {
+  __shared__ double Ls[NB][NB + 1];
+  __shared__ double vs[NB], ys[NB], part[4][NB];
+  const int64_t q = blockIdx.x;
+  K += q * sK;
+  D += q * sD;
+  Linv += q * sL;
+  b += q * sb;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nblk = (N + NB - 1) / NB;
+  for (int J = 0; J < nblk; ++J) {
+    const int J0 = J * NB, bj = N - J0 < NB ? N - J0 : NB;
+    stage_block<NB>(Linv + (int64_t)J * NB * NB, Ls);
+    for (int t = threadIdx.x; t < NB; t += TRSV_NT) vs[t] = t < bj ? b[J0 + t] : 0.0;
+    __syncthreads();
+    block_apply<NB>(Ls, vs, ys, part, false);  // ends with a barrier
+    for (int t = threadIdx.x; t < bj; t += TRSV_NT) b[J0 + t] = ys[t] / D[J0 + t];
+    // rows below: wave per row, DPP reduction
+    double yl[NB / 64];
+#pragma unroll
+    for (int qq = 0; qq < NB / 64; ++qq) yl[qq] = ys[lane + 64 * qq];
+    for (int i = J0 + NB + wave; i < N; i += 4) {
+      const double* Lr = K + (int64_t)i * ld + J0;
+      double s = 0.0;
+#pragma unroll
+      for (int qq = 0; qq < NB / 64; ++qq) s += Lr[lane + 64 * qq] * yl[qq];
+      s = wave_sum(s);
+      if (lane == 0) b[i] -= s;
+    }
+    __syncthreads();
+  }
+  for (int J = nblk - 1; J >= 0; --J) {
+    const int J0 = J * NB, bj = N - J0 < NB ? N - J0 : NB;
+    stage_block<NB>(Linv + (int64_t)J * NB * NB, Ls);
+    for (int t = threadIdx.x; t < NB; t += TRSV_NT) vs[t] = t < bj ? b[J0 + t] : 0.0;
+    __syncthreads();
+    block_apply<NB>(Ls, vs, ys, part, true);
+    for (int t = threadIdx.x; t < bj; t += TRSV_NT) b[J0 + t] = ys[t];
+    // columns above: thread per column, sum over the block's rows
+    for (int c = threadIdx.x; c < J0; c += TRSV_NT) {
+      double s = 0.0;
+      for (int r = 0; r < bj; ++r) s += K[(int64_t)(J0 + r) * ld + c] * ys[r];
+      b[c] -= s;
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
+                              double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st) {
+  if (N <= 0 || B <= 0) return hipSuccess;
+  if (nbi == 64)
+    hipLaunchKernelGGL((trsv_batched_kernel<64>), dim3(B), dim3(TRSV_NT), 0, st, K, ld, N, D, Linv, b, sK, sD, sL, sb);
+  else if (nbi == 128)
+    hipLaunchKernelGGL((trsv_batched_kernel<128>), dim3(B), dim3(TRSV_NT), 0, st, K, ld, N, D, Linv, b, sK, sD, sL,
+                       sb);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 }  // namespace ipmz

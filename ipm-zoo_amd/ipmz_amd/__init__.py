@@ -39,6 +39,8 @@ EXPORTS = [
     "ipmz_qp_destroy", "ipmz_qp_load_host", "ipmz_qp_generate", "ipmz_qp_step", "ipmz_qp_scalars",
     "ipmz_qp_device_scalars", "ipmz_qp_copy_scalars", "ipmz_qp_solve", "ipmz_qp_state_len", "ipmz_qp_get_state", "ipmz_qp_set_state",
     "ipmz_qp_get_kkt", "ipmz_qp_kkt_dim", "ipmz_qp_set_timing", "ipmz_qp_phase_times",
+    "ipmz_batch_create", "ipmz_batch_size", "ipmz_batch_load_host", "ipmz_batch_initialize", "ipmz_batch_scalars",
+    "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
 ]
 
 _P = ctypes.POINTER(ctypes.c_double)
@@ -98,6 +100,14 @@ def _load():
         "ipmz_qp_kkt_dim": ([_VP], _I),
         "ipmz_qp_set_timing": ([_VP, _I], _I),
         "ipmz_qp_phase_times": ([_VP, _P, _P, ctypes.POINTER(_I64)], _I),
+        "ipmz_batch_create": ([_VP, ctypes.POINTER(_QPConfig), _I, ctypes.POINTER(_VP)], _I),
+        "ipmz_batch_size": ([_VP], _I),
+        "ipmz_batch_load_host": ([_VP, _I] + [_P] * 9, _I),
+        "ipmz_batch_initialize": ([_VP], _I),
+        "ipmz_batch_scalars": ([_VP, _P], _I),
+        "ipmz_batch_get_state": ([_VP, _I, _I, _P], _I),
+        "ipmz_batch_set_state": ([_VP, _I, _P], _I),
+        "ipmz_batch_solve": ([_VP, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -333,3 +343,48 @@ class Optimizer:
             self.close()
         except Exception:
             pass
+
+
+class Batch(Optimizer):
+    """A batch of independent QPs with identical (n, m, p) (config C4): every
+    kernel launch serves the whole batch.  QP i of generate(seed) uses
+    seed + i."""
+
+    def __init__(self, n, m=0, p=0, batch=1, ctx=None, delta=1e-4):
+        self.ctx = ctx or default_context()
+        cfg = _QPConfig(n, m, p, delta)
+        h = _VP()
+        _check(lib.ipmz_batch_create(self.ctx.h, ctypes.byref(cfg), batch, ctypes.byref(h)), "ipmz_batch_create")
+        self.h = h
+        self.n, self.m, self.p = n, m, p
+        self.N = n + m + p
+        self.batch = batch
+        self.state_len = lib.ipmz_qp_state_len(h)
+
+    def load_one(self, index, data):
+        keep = [data.Q, data.c, data.A_ineq, data.l_A_ineq, data.u_A_ineq, data.A_eq, data.b_eq, data.l_x, data.u_x]
+        keep = [np.ascontiguousarray(a, dtype=np.float64).reshape(-1) if np.size(a) else np.zeros(1) for a in keep]
+        _check(lib.ipmz_batch_load_host(self.h, index, *[_dp(a) for a in keep]), "ipmz_batch_load_host")
+
+    def initialize(self):
+        _check(lib.ipmz_batch_initialize(self.h), "ipmz_batch_initialize")
+
+    def batch_scalars(self):
+        out = np.zeros(self.batch * SC_COUNT)
+        _check(lib.ipmz_batch_scalars(self.h, _dp(out)), "ipmz_batch_scalars")
+        return out.reshape(self.batch, SC_COUNT)
+
+    def state(self, index, which=0):
+        out = np.zeros(self.state_len)
+        _check(lib.ipmz_batch_get_state(self.h, index, which, _dp(out)), "ipmz_batch_get_state")
+        return out
+
+    def set_state(self, index, v):
+        v = np.ascontiguousarray(v, dtype=np.float64)
+        _check(lib.ipmz_batch_set_state(self.h, index, _dp(v)), "ipmz_batch_set_state")
+
+    def solve_all(self, max_iter=100):
+        it = ctypes.c_int(0)
+        nc = ctypes.c_int(0)
+        _check(lib.ipmz_batch_solve(self.h, max_iter, ctypes.byref(it), ctypes.byref(nc)), "ipmz_batch_solve")
+        return it.value, nc.value
