@@ -33,6 +33,9 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
                        hipEvent_t* ev = nullptr, int nev = 0);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
+hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st);
+hipError_t trsm_probe(double* K, int64_t ld, int N, int j0, double* D, const double* Linv, double* W, int nbo,
+                      hipStream_t st);
 hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,

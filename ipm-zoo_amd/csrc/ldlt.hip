@@ -405,6 +405,33 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
   }
 }
 
+// experiment hooks (kbench): one diag block, one panel TRSM
+hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st) {
+  if (nbi == 128)
+    hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
+  else
+    hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
+  return hipGetLastError();
+}
+hipError_t trsm_probe(double* K, int64_t ld, int N, int j0, double* D, const double* Linv, double* W, int nbo,
+                      hipStream_t st) {
+  const int r1 = j0 + 64;
+  GemmArgs g{};
+  g.M = N - r1;
+  g.N = 64;
+  g.Kd = 64;
+  g.A = K + (int64_t)r1 * ld + j0;
+  g.lda = ld;
+  g.B = Linv;
+  g.ldb = 64;
+  g.C = K + (int64_t)r1 * ld + j0;
+  g.ldc = ld;
+  g.W = W + (int64_t)r1 * nbo;
+  g.ldw = nbo;
+  g.dvec = D + j0;
+  return launch_gemm<128, 64, EPI_PANEL, 4, 2>(g, st);
+}
+
 // f64 MFMA throughput probe: each wave runs `iters` x 16 independent
 // v_mfma_f64_16x16x4 on register data.
 template <int NACC>

@@ -65,8 +65,35 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&zb, N * 8));
   CK(hipMalloc(&ctrl, (2 + 2 * (N + 63) / 64) * 4 + 256));
   Timer t;
-  for (int threads : {256, 512}) {  // 0. f64 MFMA peak probe
-    for (int nacc : {4, 8, 16}) {
+  {  // panel-path pieces
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+    for (int nbi : {64, 128}) {
+      CK(ipmz::diag_probe(K, ld, 0, nbi, D, Linv, info, st));
+      t.start(st);
+      for (int r = 0; r < 10; ++r) CK(ipmz::diag_probe(K, ld, 1024 * r, nbi, D, Linv, info, st));
+      std::printf("diag block nbi=%d: %.1f us\n", nbi, t.stop(st) / 10 * 1e3);
+    }
+    for (int j0 : {0, 5632, 10240}) {
+      CK(ipmz::trsm_probe(K, ld, N, j0, D, Linv, W, 256, st));
+      t.start(st);
+      for (int r = 0; r < 10; ++r) CK(ipmz::trsm_probe(K, ld, N, j0, D, Linv, W, 256, st));
+      std::printf("panel TRSM rows=%d x 64: %.1f us\n", N - j0 - 64, t.stop(st) / 10 * 1e3);
+    }
+    for (int cols : {64, 192, 256}) {
+      for (int kd : {64, 256}) {
+        const int M = N - 256;
+        CK(ipmz::gemm_nt_sub(M, cols, kd, W, 256, K, ld, K + 256 * ld + 256, ld, 256, 256, false, st));
+        t.start(st);
+        for (int r = 0; r < 10; ++r)
+          CK(ipmz::gemm_nt_sub(M, cols, kd, W, 256, K, ld, K + 256 * ld + 256, ld, 256, 256, false, st));
+        const float us = t.stop(st) / 10 * 1e3;
+        std::printf("strip update rows=%d cols=%d rank=%d: %.1f us (%.1f TFLOP/s)\n", M, cols, kd, us,
+                    2.0 * M * cols * kd / us / 1e6);
+      }
+    }
+  }
+  for (int threads : {256}) {  // 0. f64 MFMA peak probe
+    for (int nacc : {16}) {
       const int iters = 20000, blocks = 2048;
       CK(ipmz::mfma_probe(D, blocks, 10, threads, nacc, st));
       t.start(st);
