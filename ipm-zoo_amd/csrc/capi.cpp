@@ -147,12 +147,13 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
 //            [ybuf N] [zbuf N] [ctrl 2 + 2*nblk64 uint]
 namespace {
 struct WsLayout {
-  int64_t info_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
+  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
 };
 WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
   const int64_t nblk = (N + nbi - 1) / nbi;
   l.info_off = 0;
+  l.pctrl_off = 64;  // IPMZ_PANEL_CTRL_WORDS words, inside the first 256 bytes
   l.side_off = 256;
   l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
@@ -190,10 +191,13 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   int* info = reinterpret_cast<int*>(ws + l.info_off);
   double* Linv = reinterpret_cast<double*>(ws + l.linv_off);
   double* W = reinterpret_cast<double*>(ws + l.w_off);
+  unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
+  HIP_OK(hipMemsetAsync(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), ctx->stream));
   const int npan = (N + ctx->nbo - 1) / ctx->nbo;
   if (!ctx->lookahead || npan < 3) {
-    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->stream, timer));
+    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, 0,
+                       pctrl));
     return IPMZ_OK;
   }
   const int nev = 2 * npan + 4;
@@ -204,7 +208,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
   HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
   HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2));
+  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2, pctrl));
   // join (A has already waited for B's tail)
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));

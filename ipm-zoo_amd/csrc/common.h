@@ -11,6 +11,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+#include <utility>
+
 #define IPMZ_HOST_DEVICE __host__ __device__ __forceinline__
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -51,6 +54,23 @@ __device__ __forceinline__ double dpp_double(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xf, 0xf, false);
   return __hiloint2double(hi, lo);
 }
+// lane-broadcast DPP (row_newbcast etc.): no old value, so no v_mov of a
+// placeholder before every v_mov_dpp
+template <int CTRL>
+__device__ __forceinline__ double dpp_bcast(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xf, 0xf, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xf, 0xf, true);
+  return __hiloint2double(hi, lo);
+}
+// 1/d from v_rcp_f64 and two Newton steps (5 dependent ops instead of the
+// 10-op IEEE division sequence); finite nonzero d only
+__device__ __forceinline__ double fast_rcp(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  double e = fma(-d, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-d, r, 1.0);
+  return fma(r, e, r);
+}
 __device__ __forceinline__ void swap16(double v, double& a, double& b) {
   const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
   const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
@@ -84,4 +104,15 @@ __device__ __forceinline__ double wave_min(double v) {
   v = fmin(a, b);
   swap32(v, a, b);
   return fmin(a, b);
+}
+
+// compile-time loop: f(std::integral_constant<int, I>{}) for I in [0, N),
+// for bodies that must index register arrays with constants
+template <typename F, int... I>
+__device__ __forceinline__ void static_for_impl(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  static_for_impl(f, std::make_integer_sequence<int, N>{});
 }

@@ -4,6 +4,7 @@
 #include <stdint.h>
 
 #define IPMZ_NBO_MAX 512
+#define IPMZ_PANEL_CTRL_WORDS 16
 
 namespace ipmz {
 
@@ -28,11 +29,19 @@ struct TrailTimer {  // HIP-event pairs around every trailing-update launch
 };
 // Two-stream look-ahead when st2 and ev (>= 2*ceil(N/nbo)+2 events) are
 // given; W must then hold 3 * N * nbo doubles (else N * nbo).
+// pctrl: IPMZ_PANEL_CTRL_WORDS zeroed words for the fused panel-step kernel
+// (nbi == 64); nullptr selects the diag / TRSM / strip kernel chain.
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                        int* info, hipStream_t st, TrailTimer* timer = nullptr, hipStream_t st2 = nullptr,
-                       hipEvent_t* ev = nullptr, int nev = 0);
+                       hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr);
+// one fused diag + TRSM + strip launch for the inner block [j0, j0 + bi) of an
+// outer panel ending at column c1 (panel.hip); Wc = W + (j0 - k0), row-indexed
+hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
+                      int ldw, int* info, unsigned* ctrl, hipStream_t st);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
+hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,
+                            hipStream_t st);
 hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st);
 hipError_t trsm_probe(double* K, int64_t ld, int N, int j0, double* D, const double* Linv, double* W, int nbo,
                       hipStream_t st);

@@ -18,7 +18,11 @@
 // fits one block factors bit-identically to the reference.  Across blocks the
 // MFMA accumulates a block's contributions before subtracting them, which
 // changes rounding at the 1e-16 level (parity tolerance: tests/).
+#include <cstdlib>
+#include <cstring>
+
 #include "common.h"
+#include "diag64.h"
 #include "kernels.h"
 
 namespace ipmz {
@@ -144,6 +148,131 @@ __global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restri
     D[k0 + k] = dk;
     if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(info, k0 + k + 1);  // first non-finite pivot
   }
+}
+
+// ---------------------------------------------------------------------------
+// Diagonal block, NB = 64, ONE wave (the latency-critical kernel of the
+// factor: 176 of them sit back to back on the panel path at N = 11264).
+//
+// Lane r holds row r of the block in 64 registers.  Step k:
+//   w_r = A[r][k] goes to LDS (one ds_write per lane, double-buffered by k),
+//   d_k = readlane(A[k][k], k), the zero-pivot rule of LinearSolvers.cpp:26-28,
+//   l_r = w_r / d_k, then A[r][j] -= l_r w_j for j > k with w_j a broadcast
+//   LDS read.  No workgroup barrier anywhere in the 64 steps: a wave's LDS
+//   operations complete in order, so a wave-scope fence (no waitcnt) is all
+//   the write -> broadcast-read hand-off needs.
+// Upper-triangle registers (j > r) carry finite junk that is never read.
+// L^{-1} is built afterwards column-per-lane (lane c: L y = e_c, right-looking
+// so the 2016 FMAs are independent), reading L^T from LDS by broadcast.
+// Same arithmetic as ldlt_diag_kernel: A[r][c] -= l_r * w_c, l = w * (1/d).
+template <bool RL, bool INV = true>
+__global__ __launch_bounds__(64) void ldlt_diag64_wave_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
+                                                              double* __restrict__ D, double* __restrict__ Linv,
+                                                              int* __restrict__ info, int64_t sK, int64_t sD,
+                                                              int64_t sL) {
+  constexpr int S = 66;  // even row stride: M[j][2p..2p+1] is one aligned 16-byte broadcast read
+  K += blockIdx.x * sK;
+  D += blockIdx.x * sD;
+  Linv += blockIdx.x * sL;
+  __shared__ __attribute__((aligned(16))) double M[64 * S];
+  __shared__ __attribute__((aligned(16))) double wb[2][64];
+  const int r = threadIdx.x;
+  // coalesced load (lanes over columns): all 64 loads in flight, addresses
+  // clamped into the block's valid lower triangle, identity padding past b
+  {
+    double t[64];
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      const int ii = i < b ? i : 0, cc = r <= ii ? r : 0;
+      t[i] = K[(int64_t)(k0 + ii) * ld + k0 + cc];
+    }
+#pragma unroll
+    for (int i = 0; i < 64; ++i) M[i * S + r] = (i < b && r <= i) ? t[i] : (i == r ? 1.0 : 0.0);
+  }
+  __syncthreads();
+  double a[64];
+#pragma unroll
+  for (int j = 0; j < 64; ++j) a[j] = M[r * S + j];
+  double dreg = 1.0;
+  static_for<64>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const double wb_self = a[k];
+    if constexpr (!RL) wb[k & 1][r] = a[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    const double draw = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(a[k]), k),
+                                         __builtin_amdgcn_readlane(__double2loint(a[k]), k));
+    const double dk = draw == 0.0 ? 1e-8 : draw;
+    const double rdk = 1.0 / dk;
+    dreg = r == k ? dk : dreg;
+    const double l = a[k] * rdk;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if constexpr (RL) {  // broadcast w_j straight from lane j's register
+      static_for<63 - k>([&](auto jc) {
+        constexpr int j = k + 1 + decltype(jc)::value;
+        const double wj = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(wb_self), j),
+                                           __builtin_amdgcn_readlane(__double2loint(wb_self), j));
+        a[j] = fma(-l, wj, a[j]);
+      });
+      a[k] = l;
+      return;
+    }
+    const double2* w2 = reinterpret_cast<const double2*>(wb[k & 1]);
+    // 16 columns per batch: 8 broadcast b128 reads, then 16 independent FMAs
+    static_for<4 - (k + 1) / 16>([&](auto cc) {
+      constexpr int c0 = ((k + 1) / 16 + decltype(cc)::value) * 16;
+      double2 wv[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) wv[p] = w2[c0 / 2 + p];
+      static_for<16>([&](auto jc) {
+        constexpr int j = c0 + decltype(jc)::value;
+        if constexpr (j > k) a[j] = fma(-l, (j & 1) ? wv[(j - c0) / 2].y : wv[(j - c0) / 2].x, a[j]);
+      });
+    });
+    a[k] = l;
+  });
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 64; ++j) M[j * S + r] = a[j];  // M[j][i] = L[i][j] for i > j
+  __syncthreads();
+#pragma unroll 8
+  for (int i = 1; i < 64; ++i)
+    if (i < b && r < i) K[(int64_t)(k0 + i) * ld + k0 + r] = M[r * S + i];
+  if (r < b) {
+    D[k0 + r] = dreg;
+    if (!(fabs(dreg) <= 1.7976931348623157e308)) atomicMin(info, k0 + r + 1);  // first non-finite pivot
+  }
+  if constexpr (!INV) return;
+  // lane c: column c of L^{-1}, right-looking (y[i] -= L[i][j] y[j], i > j)
+  double y[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) y[i] = i == r ? 1.0 : 0.0;
+  static_for<63>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    const double2* l2 = reinterpret_cast<const double2*>(&M[j * S]);
+    static_for<4 - (j + 1) / 16>([&](auto cc) {
+      constexpr int c0 = ((j + 1) / 16 + decltype(cc)::value) * 16;
+      double2 lv[8];
+#pragma unroll
+      for (int p = 0; p < 8; ++p) lv[p] = l2[c0 / 2 + p];
+      static_for<16>([&](auto ic) {
+        constexpr int i = c0 + decltype(ic)::value;
+        if constexpr (i > j) y[i] = fma(-((i & 1) ? lv[(i - c0) / 2].y : lv[(i - c0) / 2].x), y[j], y[i]);
+      });
+    });
+  });
+#pragma unroll
+  for (int i = 0; i < 64; ++i) Linv[i * 64 + r] = y[i];
+}
+
+__device__ unsigned long long g_diag_clk[32];
+template <bool PROF = false>
+__global__ __launch_bounds__(256) void ldlt_diag64_blk_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
+                                                              double* __restrict__ D, double* __restrict__ Linv,
+                                                              int* __restrict__ info, int64_t sK, int64_t sD,
+                                                              int64_t sL) {
+  __shared__ double M[64 * DS], X[64 * DS], Wt[64 * DS], dsh[64];
+  diag64_body<false>(K + blockIdx.x * sK, ld, k0, b, D + blockIdx.x * sD, Linv + blockIdx.x * sL, info, M, X, Wt, dsh,
+                     PROF ? g_diag_clk : nullptr);
 }
 
 // Inverse of the unit-lower diagonal blocks of an explicit L (one workgroup
@@ -406,11 +535,52 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
 }
 
 // experiment hooks (kbench): one diag block, one panel TRSM
+// diag kernel choice for nbi = 64: 0 = 4-wave barrier-per-step (default),
+// 1 = one wave with LDS broadcasts, 2 = one wave with readlane broadcasts
+static int diag64_variant() {
+  static const int v = [] {
+    const char* e = std::getenv("IPMZ_DIAG");
+    if (!e) return 0;
+    if (!std::strcmp(e, "wave")) return 1;
+    if (!std::strcmp(e, "wave_rl")) return 2;
+    if (!std::strcmp(e, "blk")) return 5;
+    return 0;
+  }();
+  return v;
+}
+static void launch_diag64(int variant, int B, hipStream_t st, double* K, int64_t ld, int j0, int bi, double* D,
+                          double* Lb, int* info, int64_t sK, int64_t sD, int64_t sL) {
+  if (variant == 5)
+    hipLaunchKernelGGL(ldlt_diag64_blk_kernel<false>, dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+  else if (variant == 1)
+    hipLaunchKernelGGL(ldlt_diag64_wave_kernel<false>, dim3(B), dim3(64), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+  else if (variant == 2)
+    hipLaunchKernelGGL(ldlt_diag64_wave_kernel<true>, dim3(B), dim3(64), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+  else if (variant == 3)  // timing probes: no L^{-1}
+    hipLaunchKernelGGL((ldlt_diag64_wave_kernel<false, false>), dim3(B), dim3(64), 0, st, K, ld, j0, bi, D, Lb, info, sK,
+                       sD, sL);
+  else if (variant == 4)
+    hipLaunchKernelGGL((ldlt_diag64_wave_kernel<true, false>), dim3(B), dim3(64), 0, st, K, ld, j0, bi, D, Lb, info, sK,
+                       sD, sL);
+  else
+    hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+}
+
+// stage clock (s_memtime) of one ldlt_diag64_blk_kernel run, for kbench
+hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,
+                            hipStream_t st) {
+  hipLaunchKernelGGL(ldlt_diag64_blk_kernel<true>, dim3(1), dim3(256), 0, st, K, ld, 0, 64, D, Linv, info, 0, 0, 0);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_diag_clk), sizeof(unsigned long long) * 32, 0,
+                                  hipMemcpyDeviceToHost, st);
+}
+
 hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st) {
   if (nbi == 128)
     hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
-  else
-    hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(1), dim3(256), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
+  else  // nbi = -variant - 64 .. : kernel variants at 64
+    launch_diag64(nbi <= -64 ? -nbi - 64 : 0, 1, st, K, ld, k0, 64, D, Linv, info, 0, 0, 0);
   return hipGetLastError();
 }
 hipError_t trsm_probe(double* K, int64_t ld, int N, int j0, double* D, const double* Linv, double* W, int nbo,
@@ -510,18 +680,32 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 // Factor the outer panel [k0, k0 + bo): inner diag / TRSM / strip steps, all
 // on stream st.  Writes L (in K), D, the L11^{-1} blocks and W = L D for
 // the panel's rows below each inner block (W: N x nbo, this panel's buffer).
+static bool fused_panel_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("IPMZ_PANEL");
+    return !(e && !std::strcmp(e, "chain"));
+  }();
+  return on;
+}
+
 static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo,
-                               int nbo, int nbi, int* info, hipStream_t st, const BatchStrides* bs = nullptr) {
+                               int nbo, int nbi, int* info, hipStream_t st, const BatchStrides* bs = nullptr,
+                               unsigned* pctrl = nullptr) {
   hipError_t e = hipSuccess;
   const int B = bs ? bs->B : 1;
   const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
     double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
+    if (pctrl && B == 1 && nbi == 64 && fused_panel_enabled()) {
+      if ((e = panel_step(K, ld, N, j0, bi, k0 + bo, D, Lb, W + (j0 - k0), nbo, info, pctrl, st)) != hipSuccess)
+        return e;
+      continue;
+    }
     if (nbi == 128)
       hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(B), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     else
-      hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+      launch_diag64(diag64_variant(), B, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int r1 = j0 + bi;
     if (r1 >= N) continue;
@@ -595,7 +779,8 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 // overwrites the W_{k-2} a late B_{k-2} could still read (B_{k-2} precedes
 // N_{k-1} on B).  A waits for B's tail at the end.
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
-                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev) {
+                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
+                       unsigned* pctrl) {
   if (N <= 0) return hipSuccess;
   if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
@@ -604,7 +789,7 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
   const int64_t wsz = (int64_t)N * nbo;
   auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };
   auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
-  hipError_t e = factor_panel(K, ld, N, D, Linv, Wb(0), 0, pw(0), nbo, nbi, info, st);
+  hipError_t e = factor_panel(K, ld, N, D, Linv, Wb(0), 0, pw(0), nbo, nbi, info, st, nullptr, pctrl);
   if (e != hipSuccess) return e;
   if (!two) {  // single stream: factor, then the whole trailing update
     for (int k = 0; k < npan; ++k) {
@@ -616,7 +801,7 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
         if (te) hipEventRecord(te[1], st);
         if (timer) timer->flops += (double)(N - t0) * (double)(N - t0 + 1) * (double)bo;
         if (e != hipSuccess) return e;
-        if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), t0, pw(k + 1), nbo, nbi, info, st)) != hipSuccess)
+        if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), t0, pw(k + 1), nbo, nbi, info, st, nullptr, pctrl)) != hipSuccess)
           return e;
       }
     }
@@ -651,7 +836,8 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
       if ((e = hipStreamWaitEvent(st, evN[k - 1], 0)) != hipSuccess) return e;
     }
     if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
-    if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), p1, pw(k + 1), nbo, nbi, info, st)) != hipSuccess) return e;
+    if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), p1, pw(k + 1), nbo, nbi, info, st, nullptr, pctrl)) != hipSuccess)
+      return e;
   }
   if ((e = hipEventRecord(evJoin, st2)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, evJoin, 0);

@@ -1,0 +1,56 @@
+// Cross-workgroup hand-offs inside one launch (cdna_hip_programming.md §6
+// Guideline 16, "Valid forms" row 1): data is stored write-through with
+// relaxed agent-scope atomic stores (sc1) and read with agent-scope atomic
+// loads, every storing wave drains vmcnt(0), a workgroup barrier, then ONE
+// lane stores the flag with a relaxed agent-scope atomic.  The 8 XCDs have
+// private L2s, so plain loads/stores are not enough for data that another
+// workgroup of the same launch consumes.
+#pragma once
+#include <hip/hip_runtime.h>
+
+namespace ipmz {
+
+// a wait gives up after this long (s_memrealtime runs at a constant 100 MHz):
+// far beyond any legitimate hand-off, short enough that a bug surfaces as an
+// error word instead of a hung queue
+constexpr unsigned long long SPIN_TICKS = 50000000ull;  // 0.5 s
+
+__device__ __forceinline__ double ld_sc1(const double* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// one lane of the workgroup polls flag >= want; everyone leaves together.
+// Gives up (and raises *err) after SPIN_TICKS or when *err is raised.
+__device__ __forceinline__ bool wait_flag_ge(unsigned* flag, unsigned want, unsigned* err, unsigned* sh_ok) {
+  if (threadIdx.x == 0) {
+    unsigned ok = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < want) {
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+          __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    *sh_ok = ok;
+  }
+  __syncthreads();
+  return *sh_ok != 0;
+}
+__device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned* err, unsigned* sh_ok) {
+  return wait_flag_ge(flag, 1u, err, sh_ok);
+}
+
+// every storing wave drains its sc1 stores, then one lane raises the flag
+__device__ __forceinline__ void publish(unsigned* flag) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace ipmz

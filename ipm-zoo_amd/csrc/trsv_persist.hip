@@ -24,44 +24,12 @@
 // are bounded: on timeout the kernel records an error word and gives up.
 #include "common.h"
 #include "kernels.h"
+#include "sync.h"
 
 namespace ipmz {
 
 namespace {
 constexpr int PNT = 256;                 // threads per workgroup
-constexpr unsigned SPIN_LIMIT = 1u << 24;  // ~ seconds at s_sleep(2): far beyond any legitimate wait
-
-__device__ __forceinline__ double ld_sc1(const double* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// one lane of the workgroup polls; everyone leaves together
-__device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned* err, unsigned* sh_ok) {
-  if (threadIdx.x == 0) {
-    unsigned spins = 0, ok = 1;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > SPIN_LIMIT ||
-          __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        ok = 0;
-        break;
-      }
-    }
-    *sh_ok = ok;
-  }
-  __syncthreads();
-  return *sh_ok != 0;
-}
-
-__device__ __forceinline__ void publish(unsigned* flag) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its sc1 stores
-  __syncthreads();
-  if (threadIdx.x == 0) __hip_atomic_store(flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
 // quad (4-lane) all-reduce on the VALU
 __device__ __forceinline__ double quad_sum(double v) {

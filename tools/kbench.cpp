@@ -4,6 +4,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -46,6 +47,7 @@ struct Timer {
 };
 
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   const int N = argc > 1 ? std::atoi(argv[1]) : 11264;
   hipStream_t st;
   CK(hipStreamCreate(&st));
@@ -64,10 +66,13 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&yb, N * 8));
   CK(hipMalloc(&zb, N * 8));
   CK(hipMalloc(&ctrl, (2 + 2 * (N + 63) / 64) * 4 + 256));
+  unsigned* pctrl;
+  CK(hipMalloc(&pctrl, IPMZ_PANEL_CTRL_WORDS * 4));
+  CK(hipMemset(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * 4));
   Timer t;
   {  // panel-path pieces
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
-    for (int nbi : {64, 128}) {
+    for (int nbi : {64, -65, -69, 128}) {
       CK(ipmz::diag_probe(K, ld, 0, nbi, D, Linv, info, st));
       t.start(st);
       for (int r = 0; r < 10; ++r) CK(ipmz::diag_probe(K, ld, 1024 * r, nbi, D, Linv, info, st));
@@ -92,6 +97,17 @@ int main(int argc, char** argv) {
       }
     }
   }
+  {
+    unsigned long long clk[32];
+    for (int rep = 0; rep < 3; ++rep) {
+      CK(ipmz::diag_clock_probe(K, ld, D, Linv, info, clk, st));
+      CK(hipStreamSynchronize(st));
+    }
+    std::printf("diag64 blk stage clocks (s_memtime ticks from start):");
+    for (unsigned i = 1; i < clk[31] && i < 31; ++i) std::printf(" %llu", clk[i] - clk[0]);
+    std::printf("\n");
+  }
+  if (argc > 2 && std::string(argv[2]) == "pieces") return 0;
   for (int threads : {256}) {  // 0. f64 MFMA peak probe
     for (int nacc : {16}) {
       const int iters = 20000, blocks = 2048;
@@ -128,33 +144,73 @@ int main(int argc, char** argv) {
       std::printf("trailing nbo=%d R=%d: %.3f ms  %.2f TFLOP/s (algorithmic)\n", nbo, R, ms, fl / ms / 1e9);
     }
   }
-  // 2. full factor + solve per blocking, single stream and look-ahead
-  hipStream_t sB;
-  CK(hipStreamCreateWithFlags(&sB, hipStreamNonBlocking));
+  // 2. look-ahead factor: panel path on a high-priority stream, trailing
+  // updates on a stream whose CU mask leaves `reserve` CUs to the panel path
+  // (excl: the panel stream is confined to those CUs)
   std::vector<hipEvent_t> ev(2 * (N / 64 + 2) + 8);
   for (size_t i = 0; i < ev.size(); ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
-  for (int nbo : {128, 256, 512}) {
-    for (int nbi : {64}) {
-      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
-      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, nbi, info, st, nullptr, sB, ev.data(), (int)ev.size()));
-      CK(hipStreamSynchronize(st));
-      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
-      t.start(st);
-      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, nbi, info, st, nullptr, sB, ev.data(), (int)ev.size()));
-      const float fms = t.stop(st);
-      std::printf("look-ahead factor N=%d nbo=%d nbi=%d: %.3f ms = %.2f TFLOP/s (N^3/3)\n", N, nbo, nbi, fms,
-                  (double)N * N * N / 3.0 / fms / 1e9);
+  int lo = 0, hi = 0;
+  CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  int ncu = 0;
+  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
+  struct LA { int nbo, reserve; bool excl, fused; };
+  const LA las[] = {{256, 0, false, false}, {256, 0, false, true}, {256, 32, false, true},
+                    {512, 0, false, false}, {512, 0, false, true}, {512, 32, false, true}};
+  for (const LA& la : las) {
+    std::vector<uint32_t> mB((ncu + 31) / 32, 0u), mA((ncu + 31) / 32, 0u);
+    const int stride = la.reserve ? ncu / la.reserve : ncu + 1;
+    for (int c = 0; c < ncu; ++c) {
+      const bool res = la.reserve && c % stride == 0 && c / stride < la.reserve;
+      (res ? mA : mB)[c / 32] |= 1u << (c % 32);
     }
+    hipStream_t sA, sB;
+    CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+    if (la.reserve) CK(hipExtStreamCreateWithCUMask(&sB, (uint32_t)mB.size(), mB.data()));
+    else CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+    if (la.excl) {
+      CK(hipStreamDestroy(sA));
+      CK(hipExtStreamCreateWithCUMask(&sA, (uint32_t)mA.size(), mA.data()));
+    }
+    {
+      std::vector<uint32_t> got(mB.size(), 0u);
+      CK(hipExtStreamGetCUMask(sB, (uint32_t)got.size(), got.data()));
+      std::printf("config nbo=%d reserve=%d excl=%d: sB mask[0]=%08x\n", la.nbo, la.reserve, (int)la.excl, got[0]);
+    }
+    for (int rep = 0; rep < 2; ++rep) {
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, sA, K, ld, N, 7ull);
+      CK(hipStreamSynchronize(sA));
+      t.start(sA);
+      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, la.nbo, 64, info, sA, nullptr, sB, ev.data(), (int)ev.size(),
+                           la.fused ? pctrl : nullptr));
+      const float fms = t.stop(sA);
+      if (rep)
+        std::printf("look-ahead factor N=%d nbo=%d reserve=%d%s%s: %.3f ms = %.2f TFLOP/s (N^3/3)\n", N, la.nbo,
+                    la.reserve, la.excl ? " excl" : "", la.fused ? " fused" : "", fms,
+                    (double)N * N * N / 3.0 / fms / 1e9);
+    }
+    CK(hipStreamSynchronize(sB));
+    {
+      unsigned hc[IPMZ_PANEL_CTRL_WORDS];
+      CK(hipMemcpy(hc, pctrl, sizeof(hc), hipMemcpyDeviceToHost));
+      std::printf("  panel ctrl: ticket=%u done=%u err=%u diag=%u\n", hc[0], hc[1], hc[2], hc[3]);
+    }
+    CK(hipStreamDestroy(sA));
+    CK(hipStreamDestroy(sB));
   }
   const int cfg[][2] = {{256, 64}, {512, 64}, {128, 64}};
   for (auto& c : cfg) {
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     CK(hipMemsetAsync(info, 0x7f, 4, st));
-    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st));  // warm
+    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st, nullptr, nullptr, nullptr, 0, pctrl));  // warm
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     t.start(st);
-    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st));
+    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, c[0], c[1], info, st, nullptr, nullptr, nullptr, 0, pctrl));
     const float fms = t.stop(st);
+    {
+      unsigned hc[IPMZ_PANEL_CTRL_WORDS];
+      CK(hipMemcpy(hc, pctrl, sizeof(hc), hipMemcpyDeviceToHost));
+      std::printf("  panel ctrl after factor: ticket=%u done=%u err=%u diag=%u\n", hc[0], hc[1], hc[2], hc[3]);
+    }
     CK(hipMemsetAsync(b, 0, N * 8, st));
     t.start(st);
     for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve(K, ld, N, D, Linv, c[1], b, side, st));
