@@ -143,7 +143,7 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
 }
 
 // ---------------------------------------------------------------------------
-// Workspace: [info int (256 B)] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
+// Workspace: [info int (256 B)] [panel ctrl words] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
 //            [ybuf N] [zbuf N] [ctrl 2 + 2*nblk64 uint]
 namespace {
 struct WsLayout {
@@ -153,8 +153,8 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
   const int64_t nblk = (N + nbi - 1) / nbi;
   l.info_off = 0;
-  l.pctrl_off = 64;  // IPMZ_PANEL_CTRL_WORDS words, inside the first 256 bytes
-  l.side_off = 256;
+  l.pctrl_off = 256;  // IPMZ_PANEL_CTRL_WORDS words
+  l.side_off = l.pctrl_off + round_up(IPMZ_PANEL_CTRL_WORDS * 4, 256);
   l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
   l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)

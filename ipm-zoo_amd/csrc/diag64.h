@@ -2,6 +2,7 @@
 // diag kernel (ldlt.hip) and the fused panel-step kernel (panel.hip).
 #pragma once
 #include "common.h"
+#include "sync.h"
 
 namespace ipmz {
 
@@ -17,9 +18,9 @@ namespace ipmz {
 // k l>>4; C/D: col l&15, row (l>>4) + 4 reg), with one workgroup barrier per
 // stage (8 in all):
 //   leaf  p : L_pp, D_p, X_pp = L_pp^{-1}                       (wave 0)
-//   panel p : T = A_ip X_pp^T, W_ip = T, L_ip = T / D_p    (i > p)
+//   panel p : T = A_ip X_pp^T, L_ip = T / D_p              (i > p)
 //             X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj       (j < p)
-//   update p: A_ij -= L_ip W_jp^T (p < j <= i); wave 0 takes (p+1, p+1) first
+//   update p: A_ij -= L_ip (L_jp D_p)^T (p < j <= i); wave 0 takes (p+1, p+1) first
 //             and goes straight on to leaf p+1
 // X = L^{-1} (the block inverse the panel TRSM and the solve use) falls out of
 // the same tiles.  Leaf arithmetic is the reference's order
@@ -83,6 +84,17 @@ __device__ __forceinline__ double4_t tile_nt(const double* P, const double* Q, d
   }
   return acc;
 }
+// acc -= P (Q diag(dq))^T over 16: the W = L D operand formed on the fly
+// from the L tile and the pivots (no separate W tile in LDS)
+__device__ __forceinline__ double4_t tile_nt_lds(const double* P, const double* Q, const double* dq, double4_t acc,
+                                                 int lane) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int k = 4 * q + (lane >> 4);
+    acc = mfma_f64_16x16x4(-P[(lane & 15) * DS + k], Q[(lane & 15) * DS + k] * dq[k], acc);
+  }
+  return acc;
+}
 // acc += P Q over 16 (NN)
 __device__ __forceinline__ double4_t tile_nn(const double* P, const double* Q, double4_t acc, int lane) {
 #pragma unroll
@@ -106,17 +118,20 @@ __device__ __forceinline__ void tile_store(double* C, double4_t v, int lane) {
 using namespace diag64;
 
 // The whole diagonal-block factorization for one 256-thread workgroup.
-// LDS: M, X, Wt (64 x DS each) and dsh (64).  COH: Linv and D are stored
+// LDS: M, X (64 x DS each) and dsh (64) -- 66.5 KB, so a workgroup running
+// this fits the LDS slot one trailing-GEMM tile frees (73.7 KB) and a
+// high-priority panel launch is not starved behind a whole GEMM launch.
+// LSC: read the block with agent-scope loads (it was written earlier in the
+// same launch, possibly through another CU's L1).  COH: Linv and D are stored
 // write-through (agent-scope relaxed atomics) for consumers in other
 // workgroups of the same launch.  clk != nullptr records stage clocks.
-template <bool COH>
+template <bool COH, bool LSC = false>
 __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, int k0, int b, double* __restrict__ D,
                                             double* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
-                                            double* Wt, double* dsh, unsigned long long* clkbuf) {
+                                            double* dsh, unsigned long long* clkbuf) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
-  auto Wp = [&](int i, int p) { return &Wt[(16 * i) * DS + 16 * p]; };
   int nclk = 0;
   auto clk = [&]() {
     if (clkbuf && tid == 0) clkbuf[nclk] = __builtin_amdgcn_s_memtime();
@@ -130,7 +145,8 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
     for (int q = 0; q < 16; ++q) {
       const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
       const int r2 = rr < b ? rr : 0, c2 = cc <= r2 ? cc : 0;
-      t[q] = K[(int64_t)(k0 + r2) * ld + k0 + c2];
+      const double* src = &K[(int64_t)(k0 + r2) * ld + k0 + c2];
+      t[q] = LSC ? ld_sc1(src) : *src;
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -151,7 +167,6 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
         if (t < 3 - p) {
           const int i = p + 1 + t;
           double4_t acc = tile_nt(Mt(i, p), Xt(p, p), (double4_t){0.0, 0.0, 0.0, 0.0}, lane, false);
-          tile_store(Wp(i, p), acc, lane);
           const double rc = 1.0 / dsh[16 * p + (lane & 15)];
 #pragma unroll
           for (int g = 0; g < 4; ++g) acc[g] = acc[g] * rc;
@@ -176,7 +191,7 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
     if (wave == 0) {
       const int d = p + 1;
       double4_t acc = tile_load(Mt(d, d), lane);
-      acc = tile_nt(Mt(d, p), Wp(d, p), acc, lane, true);
+      acc = tile_nt_lds(Mt(d, p), Mt(d, p), &dsh[16 * p], acc, lane);
       tile_store(Mt(d, d), acc, lane);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -189,7 +204,7 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
           if (i == p + 1 && j == p + 1) continue;
           if (t++ % 3 != wave - 1) continue;
           double4_t acc = tile_load(Mt(i, j), lane);
-          acc = tile_nt(Mt(i, p), Wp(j, p), acc, lane, true);
+          acc = tile_nt_lds(Mt(i, p), Mt(j, p), &dsh[16 * p], acc, lane);
           tile_store(Mt(i, j), acc, lane);
         }
     }

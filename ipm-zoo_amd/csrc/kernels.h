@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 #define IPMZ_NBO_MAX 512
-#define IPMZ_PANEL_CTRL_WORDS 16
+#define IPMZ_PANEL_CTRL_WORDS 128
 
 namespace ipmz {
 
@@ -38,6 +38,11 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
 // outer panel ending at column c1 (panel.hip); Wc = W + (j0 - k0), row-indexed
 hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
                       int ldw, int* info, unsigned* ctrl, hipStream_t st);
+// the whole outer panel [k0, k0 + bo) in ONE launch (panel.hip): the nbo/64
+// inner blocks pipelined by flags instead of launch boundaries.  Lb0: L^{-1}
+// block of the panel's first inner block; Wp: the panel's W buffer (N x ldw)
+hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                       int* info, unsigned* ctrl, hipStream_t st);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
 hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,

@@ -270,8 +270,8 @@ __global__ __launch_bounds__(256) void ldlt_diag64_blk_kernel(double* __restrict
                                                               double* __restrict__ D, double* __restrict__ Linv,
                                                               int* __restrict__ info, int64_t sK, int64_t sD,
                                                               int64_t sL) {
-  __shared__ double M[64 * DS], X[64 * DS], Wt[64 * DS], dsh[64];
-  diag64_body<false>(K + blockIdx.x * sK, ld, k0, b, D + blockIdx.x * sD, Linv + blockIdx.x * sL, info, M, X, Wt, dsh,
+  __shared__ double M[64 * DS], X[64 * DS], dsh[64];
+  diag64_body<false>(K + blockIdx.x * sK, ld, k0, b, D + blockIdx.x * sD, Linv + blockIdx.x * sL, info, M, X, dsh,
                      PROF ? g_diag_clk : nullptr);
 }
 
@@ -680,12 +680,17 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 // Factor the outer panel [k0, k0 + bo): inner diag / TRSM / strip steps, all
 // on stream st.  Writes L (in K), D, the L11^{-1} blocks and W = L D for
 // the panel's rows below each inner block (W: N x nbo, this panel's buffer).
-static bool fused_panel_enabled() {
-  static const bool on = [] {
+// panel path: 2 = the whole outer panel in one launch (default), 1 = one
+// fused launch per inner block (IPMZ_PANEL=step), 0 = diag / TRSM / strip
+// kernel chain (IPMZ_PANEL=chain)
+static int panel_mode() {
+  static const int mode = [] {
     const char* e = std::getenv("IPMZ_PANEL");
-    return !(e && !std::strcmp(e, "chain"));
+    if (e && !std::strcmp(e, "chain")) return 0;
+    if (e && !std::strcmp(e, "step")) return 1;
+    return 2;
   }();
-  return on;
+  return mode;
 }
 
 static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo,
@@ -694,10 +699,12 @@ static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* 
   hipError_t e = hipSuccess;
   const int B = bs ? bs->B : 1;
   const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
+  if (pctrl && B == 1 && nbi == 64 && panel_mode() == 2)
+    return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
     double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
-    if (pctrl && B == 1 && nbi == 64 && fused_panel_enabled()) {
+    if (pctrl && B == 1 && nbi == 64 && panel_mode() == 1) {
       if ((e = panel_step(K, ld, N, j0, bi, k0 + bo, D, Lb, W + (j0 - k0), nbo, info, pctrl, st)) != hipSuccess)
         return e;
       continue;

@@ -22,6 +22,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
     tests) step tests 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
+    # HBM traffic: one counter group per pass (MI355X_MICROARCH.md, rocprofv3 PMC slots)
+    pmc_fetch) step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    pmc_write) step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     *) step "$s" 600 $s ;;
   esac
 done
