@@ -390,8 +390,48 @@ struct TileLoader {
   }
 };
 
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
-__global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g) {
+// OPT bits:
+//   OPT_NOR2  LDS offsets laundered per k-step so the compiler cannot fuse
+//             two reads into ds_read2_b64 (its 16-lane, mod-32 banking turns
+//             the PAD = 18 rows into 2-way conflicts; ds_read_b64 is
+//             conflict-free)
+//   OPT_GRP   grouped triangular enumeration: bands of GRP tile rows walked
+//             column by column, so an XCD's ~64 resident tiles share ~8 W and
+//             ~8 L row panels in its L2 instead of one W and ~64 L panels
+enum { OPT_NOR2 = 2, OPT_GRP = 4 };
+constexpr int GRP = 8;
+
+// grouped enumeration of the lower tiles (tm >= tn) of an ntm x ntm grid
+__device__ __forceinline__ void grouped_tile(int bid, int ntm, int& tm, int& tn) {
+  int r = (int)((sqrt(8.0 * (double)bid + 1.0) - 1.0) * 0.5);
+  while ((r + 1) * (r + 2) / 2 <= bid) ++r;
+  while (r * (r + 1) / 2 > bid) --r;
+  const int b0 = (r / GRP) * GRP;              // first row of the band
+  const int gb = ntm - b0 < GRP ? ntm - b0 : GRP;  // rows in the band
+  int li = bid - b0 * (b0 + 1) / 2;
+  if (li < b0 * gb) {  // rectangular part: columns < b0, gb rows each
+    tn = li / gb;
+    tm = b0 + li % gb;
+    return;
+  }
+  li -= b0 * gb;
+  for (int t = 0;; ++t) {  // triangular part: column b0 + t has rows b0 + t .. b0 + gb - 1
+    const int cnt = gb - t;
+    if (li < cnt) {
+      tn = b0 + t;
+      tm = b0 + t + li;
+      return;
+    }
+    li -= cnt;
+  }
+}
+
+// 8-wave tiles are sized for two workgroups per CU = 4 waves per SIMD, which
+// needs <= 128 VGPRs: pinned with amdgpu_waves_per_eu (the compiler otherwise
+// drifts to 129+ and silently halves the occupancy)
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
+__global__ __launch_bounds__(64 * WGM * WGN)
+__attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_kernel(GemmArgs g) {
   constexpr int BK = 16, PAD = 18, NTH = 64 * WGM * WGN;
   if (blockIdx.y) {
     const int64_t z = blockIdx.y;
@@ -417,12 +457,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g)
   }
   int tm, tn;
   if (g.lower == 2) {
-    // triangular enumeration of lower tiles: bid -> (tm >= tn)
-    int r = (int)((sqrt(8.0 * (double)bid + 1.0) - 1.0) * 0.5);
-    while ((r + 1) * (r + 2) / 2 <= bid) ++r;
-    while (r * (r + 1) / 2 > bid) --r;
-    tm = r;
-    tn = bid - r * (r + 1) / 2;
+    if constexpr ((OPT & OPT_GRP) != 0) {
+      grouped_tile(bid, g.ntm, tm, tn);
+    } else {
+      // triangular enumeration of lower tiles: bid -> (tm >= tn)
+      int r = (int)((sqrt(8.0 * (double)bid + 1.0) - 1.0) * 0.5);
+      while ((r + 1) * (r + 2) / 2 <= bid) ++r;
+      while (r * (r + 1) / 2 > bid) --r;
+      tm = r;
+      tn = bid - r * (r + 1) / 2;
+    }
   } else {
     tn = bid % g.ntn;
     tm = bid / g.ntn;
@@ -443,6 +487,8 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g)
   ld.load(g, i0, j0, 0);
   ld.store(As[0], Bs[0]);
   __syncthreads();
+  const int aoff = (wr * WM + (lane & 15)) * PAD + (lane >> 4);
+  const int boff = (wc * WN + (lane & 15)) * PAD + (lane >> 4);
   for (int t = 0; t < nch; ++t) {
     const int cur = t & 1;
     if (t + 1 < nch) ld.load(g, i0, j0, (t + 1) * BK);
@@ -450,12 +496,16 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g)
     const double* bs = Bs[cur];
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
-      const int k = 4 * s + (lane >> 4);
+      int ao = aoff + 4 * s, bo = boff + 4 * s;
+      if constexpr ((OPT & OPT_NOR2) != 0) {
+        asm volatile("" : "+v"(ao));
+        asm volatile("" : "+v"(bo));
+      }
       double af[TM], bf[TN];
 #pragma unroll
-      for (int a = 0; a < TM; ++a) af[a] = as[(wr * WM + a * 16 + (lane & 15)) * PAD + k];
+      for (int a = 0; a < TM; ++a) af[a] = as[ao + a * 16 * PAD];
 #pragma unroll
-      for (int b = 0; b < TN; ++b) bf[b] = bs[(wc * WN + b * 16 + (lane & 15)) * PAD + k];
+      for (int b = 0; b < TN; ++b) bf[b] = bs[bo + b * 16 * PAD];
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
@@ -490,7 +540,7 @@ __global__ __launch_bounds__(64 * WGM * WGN) void gemm_nt_f64_kernel(GemmArgs g)
     }
 }
 
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2>
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
 static hipError_t launch_gemm(GemmArgs g, hipStream_t st, int batch = 1) {
   g.ntm = (g.M + BM - 1) / BM;
   g.ntn = (g.N + BN - 1) / BN;
@@ -502,7 +552,7 @@ static hipError_t launch_gemm(GemmArgs g, hipStream_t st, int batch = 1) {
     if (BM == BN) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
     else g.lower = 1;
   }
-  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN>), dim3((unsigned)nblk, (unsigned)batch),
+  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN, OPT>), dim3((unsigned)nblk, (unsigned)batch),
                      dim3(64 * WGM * WGN), 0, st, g);
   return hipGetLastError();
 }
@@ -524,12 +574,14 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
   switch (variant) {
     case 0: return launch_gemm<128, 128, EPI_SUB>(g, st);
     case 1: return launch_gemm<256, 128, EPI_SUB, 4, 2>(g, st);
-    case 2: return launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st);
+    case 2: return launch_gemm<128, 128, EPI_SUB, 2, 4, 0>(g, st);
     case 3: return launch_gemm<128, 64, EPI_SUB, 2, 1>(g, st);
     case 4: return launch_gemm<256, 128, EPI_SUB, 4, 4>(g, st);
     case 5: return launch_gemm<128, 128, EPI_SUB, 4, 4>(g, st);
     case 6: return launch_gemm<128, 256, EPI_SUB, 2, 8>(g, st);
-    case 7: return launch_gemm<256, 256, EPI_SUB, 4, 4>(g, st);
+    case 9: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2>(g, st);
+    case 10: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_GRP>(g, st);  // (these two spill one VGPR)
+    case 14: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -656,8 +708,10 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   // 128x128 tile, 8 waves as 2 x 4 (64 x 32 per wave, 128 VGPRs), 72 KB LDS:
   // two workgroups per CU = 4 waves per SIMD (kbench: 47 TFLOP/s = 60 % of
   // the fp64 MFMA peak at R = 11008, vs 25 with 4 waves of 64 x 64)
-  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4>(g, st, batch)
-                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st, batch);
+  // ds_read_b64 without read2 fusion + grouped tile order: 53 vs 48 TFLOP/s
+  // (kbench, R = 11008, rank 256)
+  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch)
+                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
 }
 
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,

@@ -70,6 +70,27 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&pctrl, IPMZ_PANEL_CTRL_WORDS * 4));
   CK(hipMemset(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * 4));
   Timer t;
+  if (argc > 2 && std::string(argv[2]) == "gemm") {  // trailing GEMM alone (PMC passes)
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+    const int R = N - 256;
+    for (int r = 0; r < 3; ++r) {
+      t.start(st);
+      CK(ipmz::gemm_nt_sub(R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, 0, 0, true, st));
+      const float ms = t.stop(st);
+      std::printf("trailing R=%d nbo=256: %.3f ms %.2f TFLOP/s\n", R, ms, (double)R * (R + 1) * 256 / ms / 1e9);
+    }
+    for (int var : {2, 9, 10, 14}) {
+      for (int R : {5632, 11008}) {
+        hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+        CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        t.start(st);
+        for (int r = 0; r < 5; ++r) CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        const float ms = t.stop(st) / 5;
+        std::printf("gemm variant %d R=%d K=256: %.3f ms %.2f TFLOP/s\n", var, R, ms, (double)R * (R + 1) * 256 / ms / 1e9);
+      }
+    }
+    return 0;
+  }
   {  // panel-path pieces
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     for (int nbi : {64, -65, -69, 128}) {
