@@ -35,10 +35,16 @@ WORKLOADS = {
                                           "(Regularization), augmented LDL^T, KKT N=11264"),
     "c2size": dict(n=2048, m=512, p=0, desc="dense QP n=2048, m=512 ineq, augmented LDL^T, KKT N=2560"),
     "small": dict(n=1024, m=256, p=128, desc="dense QP n=1024, m=256, p=128 (smoke size)"),
+    "c5": dict(n=16384, m=0, p=0, mixed=True, sample_scale=8,
+               desc="dense QP n=16384 box-only (SlackedSlacks), fp32 LDL^T of the scaled KKT + fp64 iterative "
+                    "refinement to 1e-12"),
+    "c5_f64": dict(n=16384, m=0, p=0, sample_scale=8,
+                   desc="C5's QP (n=16384 box-only) with the plain fp64 factor, for comparison"),
 }
+FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X f32-input MFMA peak (MI355X_MICROARCH.md, Matrix cores)
 
 
-def cpu_baseline(wl, sample_scale=4):
+def cpu_baseline(wl):
     """Time the CPU oracle (a bit-faithful restatement of the reference path,
     oracle/ipmz_oracle.cpp, single thread) on a bounded sample: one Newton
     step of the same workload with every dimension divided by sample_scale,
@@ -48,6 +54,7 @@ def cpu_baseline(wl, sample_scale=4):
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import oracle  # test/baseline infrastructure only
 
+    sample_scale = wl.get("sample_scale", 4)
     n, m, p = (wl[k] // sample_scale for k in ("n", "m", "p"))
     qp = oracle.gen_qp(n, m, p, 1234)
     o = oracle.OracleQP(qp)
@@ -79,6 +86,7 @@ def main():
     ap.add_argument("--nbo", type=int, default=int(os.environ.get("IPMZ_NBO", 256)))
     ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 64)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ir-tol", type=float, default=1e-12, help="c5: refinement tolerance")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (allows graph replay)")
     args = ap.parse_args()
 
@@ -103,6 +111,9 @@ def main():
     ctx = I.Context(local_rank, stream=stream.cuda_stream, nbo=args.nbo, nbi=args.nbi)
     qp = I.Optimizer(n, m, p, ctx)
     qp.generate(1234 + rank)
+    mixed = wl.get("mixed", False)
+    if mixed:
+        qp.set_mixed_precision(True, args.ir_tol, 20)
     timing = not args.no_timing
     flags = I.STEP_RESTART_IF_CONVERGED | (0 if timing else I.STEP_GRAPH)
     from ipmz_amd.dist import pack_summary, reduce_summary
@@ -154,16 +165,24 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "f64",
+            "dtype": "f32 factor + f64 refinement" if mixed else "f64",
             "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; seed 1234+rank)",
             "config": {"workload": args.workload, "n": n, "m": m, "p": p, "kkt_N": Nk,
-                       "formulation": "SlackedSlacks ineq + Regularization eq (delta=1e-4), augmented LDL^T",
+                       "formulation": ("SlackedSlacks box-only, fp32 LDL^T of S K S + fp64 iterative refinement "
+                                       f"(tol {args.ir_tol:g})") if mixed else
+                                      "SlackedSlacks ineq + Regularization eq (delta=1e-4), augmented LDL^T",
                        "parallelism": f"replicas x{world} (independent QPs, RCCL all-reduce of convergence "
                                       f"scalars only)",
                        "blocking": {"nbo": args.nbo, "nbi": args.nbi},
                        "description": wl["desc"]},
             "restarts": s["restarts"],
         }
+        traffic = None
+        tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
+        if os.path.exists(tpath):  # HBM bytes per trailing launch from the committed PMC passes
+            with open(tpath) as f:
+                traffic = json.load(f)
+            traffic["source"] = os.path.relpath(tpath, REPO) + " (" + traffic.get("profile", "") + ")"
         if ph:
             k = args.steps
             factor_ms = ph["factor"] / k
@@ -172,14 +191,19 @@ def main():
             tr_s = ph["trailing"] * 1e-3
             launches = ph["trailing_launches"]
             achieved = ph["trailing_flops"] / tr_s / 1e12 if tr_s > 0 else 0.0
+            peak = FP32_MFMA_PEAK_TFLOPS if mixed else FP64_MFMA_PEAK_TFLOPS
             out["roofline"] = {
                 "bound": "mfma",
-                "kernel": "gemm_nt_f64_kernel<128,128,EPI_SUB> (trailing update A22 -= W21 L21^T, fp64 MFMA)",
+                "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB> (trailing update "
+                           f"A22 -= W21 L21^T, {'fp32' if mixed else 'fp64'} MFMA)"),
                 "achieved": achieved,
-                "peak": FP64_MFMA_PEAK_TFLOPS,
+                "peak": peak,
                 "unit": "TFLOP/s",
-                "frac": achieved / FP64_MFMA_PEAK_TFLOPS,
-                "traffic": None,
+                "frac": achieved / peak,
+                "traffic": traffic.get("traffic_bytes_per_launch") if traffic else None,
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)",
+                "traffic_source": traffic.get("source") if traffic else None,
+                "algorithmic_bytes_per_launch": traffic.get("algorithmic_bytes_per_launch") if traffic else None,
                 "launches": launches,
                 "avg_launch_ms": ph["trailing"] / max(1, launches),
                 "flops_per_launch": ph["trailing_flops"] / max(1, launches),

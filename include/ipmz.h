@@ -78,6 +78,10 @@ enum ipmz_scalar {
   IPMZ_SC_CONVERGED,    /* 1.0 when res < 1e-8 and mu < 1e-8                  */
   IPMZ_SC_MU_NEW,       /* last step: sigma * mu                              */
   IPMZ_SC_RESTARTS,     /* benchmark restarts taken                           */
+  IPMZ_SC_IR_RATIO_AFF, /* mixed precision: ||r||/||b|| reached, affine solve */
+  IPMZ_SC_IR_ITERS_AFF, /*   refinement corrections, affine solve             */
+  IPMZ_SC_IR_RATIO,     /*   the same for the corrector solve                 */
+  IPMZ_SC_IR_ITERS,
   IPMZ_SC_COUNT = 16
 };
 
@@ -110,6 +114,20 @@ int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, voi
 int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b);
 /* Rebuild the solve workspace from an explicit unit-lower L (device). */
 int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, void* ws, int64_t ws_bytes);
+
+/* ---- mixed precision (config C5): fp32 factor + fp64 refinement -----------
+ * No reference counterpart (the reference is fp64 throughout,
+ * LinearSolvers.cpp:14-74); the result is the fp64 solution of the same
+ * system to the requested tolerance.  K: device, lower triangle, row-major,
+ * fp64 (left intact: the refinement residual r = b - K x uses it).  The
+ * factor is of S K S, S = diag(|K_ii|^-1/2), stored in fp32 in ws. */
+int64_t ipmz_mixed_workspace_bytes(ipmz_ctx* ctx, int N);
+int ipmz_mixed_factor(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, int64_t ws_bytes);
+/* b (device) <- K^{-1} b, refined until ||b - K x||_inf <= tol ||b||_inf or
+ * max_refine corrections; stat (host, may be NULL): {ratio reached,
+ * corrections applied}. */
+int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, double* b, double tol,
+                     int max_refine, double* stat);
 
 /* ---- LinearSolvers with the reference's host signatures ------------------ */
 /* A: host N x N row-major (lower triangle read).  L: host N x N, written
@@ -164,6 +182,11 @@ int ipmz_qp_set_state(ipmz_qp* qp, const double* host_vars);
  * (lower triangle written, upper zero).  For parity tests. */
 int ipmz_qp_get_kkt(ipmz_qp* qp, double* host_K);
 int ipmz_qp_kkt_dim(ipmz_qp* qp);
+/* Newton directions through the mixed-precision solve (fp32 factor of the
+ * scaled KKT matrix + fp64 refinement to tol, at most max_refine corrections
+ * per solve); enable = 0 returns to the fp64 factor.  Single QPs only.  The
+ * scalar block then reports IPMZ_SC_IR_*. */
+int ipmz_qp_set_mixed_precision(ipmz_qp* qp, int enable, double tol, int max_refine);
 
 /* ---- batches of independent QPs (config C4) ------------------------------
  * A batch is an ipmz_qp holding `batch` QPs of identical (n, m, p); every

@@ -252,6 +252,67 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
   return IPMZ_OK;
 }
 
+// Mixed precision (config C5) -------------------------------------------------
+}  // extern "C"
+
+// factor of S K S in fp32, with the same two-stream look-ahead as the fp64 factor
+static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs& w, TrailTimer* timer) {
+  const int npan = (w.N + w.nbo - 1) / w.nbo;
+  if (!ctx->lookahead || npan < 3) {
+    HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, 0, timer));
+    return IPMZ_OK;
+  }
+  const int nev = 2 * npan + 4;
+  int rc = ensure_events(ctx, (size_t)nev);
+  if (rc) return rc;
+  hipEvent_t* ev = ctx->evpool.data();
+  HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
+  HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
+  HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
+  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ev, nev - 2, timer));
+  HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
+  HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  return IPMZ_OK;
+}
+
+extern "C" {
+
+int64_t ipmz_mixed_workspace_bytes(ipmz_ctx* ctx, int N) {
+  if (!ctx || N < 0) return 0;
+  return mixed_ws_bytes(N, ctx->nbo);
+}
+
+int ipmz_mixed_factor(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, int64_t ws_bytes) {
+  if (!ctx || N < 0 || (N > 0 && (!K || !ws)) || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_mixed_factor: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  if (ws_bytes < mixed_ws_bytes(N, ctx->nbo)) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  HIP_OK(hipSetDevice(ctx->device));
+  MixedWs w;
+  mixed_ws_carve(static_cast<char*>(ws), N, ctx->nbo, w);
+  int rc = mixed_factor_impl(ctx, K, ld, w, nullptr);
+  if (rc) return rc;
+  int info = 0;
+  HIP_OK(hipMemcpyAsync(&info, w.info, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  return info == 0x7f7f7f7f ? IPMZ_OK : info;
+}
+
+int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, double* b, double tol,
+                     int max_refine, double* stat) {
+  if (!ctx || N < 0 || ld < N || max_refine < 0) return fail(IPMZ_ERR_INVALID, "ipmz_mixed_solve: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  if (!K || !ws || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
+  HIP_OK(hipSetDevice(ctx->device));
+  MixedWs w;
+  mixed_ws_carve(static_cast<char*>(ws), N, ctx->nbo, w);
+  HIP_OK(mixed_solve(K, ld, w, b, tol, max_refine, ctx->stream));
+  if (stat) {
+    HIP_OK(hipMemcpyAsync(stat, w.stat, 2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
+    HIP_OK(hipStreamSynchronize(ctx->stream));
+  }
+  return IPMZ_OK;
+}
+
 // Host adapters with the reference's signatures ------------------------------
 int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, double* D) {
   if (!ctx || N < 0 || (N > 0 && (!A || !L || !D))) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_decomposition: bad arguments");
@@ -348,6 +409,12 @@ struct ipmz_qp {
   int* binfo = nullptr;
   int64_t sL = 0, sW = 0;
   bool loaded = false;
+  // mixed precision (C5): fp32 factor of S K S + fp64 refinement
+  bool mixed = false;
+  double ir_tol = 1e-12;
+  int ir_max = 10;
+  MixedWs mw;
+  char* mws = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
   int graph_flags = -1;
@@ -391,8 +458,12 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
 
 QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
 
-int solve_batch(ipmz_qp* s, hipStream_t st) {
-  if (s->B == 1) {
+int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
+  if (s->mixed) {
+    HIP_OK(mixed_solve(s->K, s->ldk, s->mw, q0(s).b, s->ir_tol, s->ir_max, st));
+    HIP_OK(hipMemcpyAsync(q0(s).scal + IPMZ_SC_IR_RATIO_AFF + 2 * which, s->mw.stat, 2 * sizeof(double),
+                          hipMemcpyDeviceToDevice, st));
+  } else if (s->B == 1) {
     HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, s->ctx->nbo, s->ctx->nbi, q0(s).b, st));
   } else {
     HIP_OK(ldlt_solve_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->ctx->nbi, q0(s).b, s->B, s->sK, s->sD, s->sL,
@@ -402,6 +473,7 @@ int solve_batch(ipmz_qp* s, hipStream_t st) {
 }
 
 int factor_batch(ipmz_qp* s, TrailTimer* tt) {
+  if (s->mixed) return mixed_factor_impl(s->ctx, s->K, s->ldk, s->mw, tt);
   if (s->B == 1) return factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, tt);
   BatchStrides bs;
   bs.B = s->B;
@@ -435,7 +507,7 @@ int run_step(ipmz_qp* s, int flags) {
   mark(2);
   // predictor (affine scaling) direction
   HIP_OK(qp_rhs(qb, st));
-  if ((rc = solve_batch(s, st))) return rc;
+  if ((rc = solve_batch(s, st, 0))) return rc;
   mark(3);
   HIP_OK(qp_backsub(qb, 0, st));
   HIP_OK(qp_ratio(qb, 0, SC_ALPHA_AFF, st));
@@ -444,7 +516,7 @@ int run_step(ipmz_qp* s, int flags) {
   HIP_OK(qp_corrector_residuals(qb, st));
   HIP_OK(qp_rhs(qb, st));
   mark(4);
-  if ((rc = solve_batch(s, st))) return rc;
+  if ((rc = solve_batch(s, st, 1))) return rc;
   mark(5);
   HIP_OK(qp_backsub(qb, 1, st));
   HIP_OK(qp_ratio(qb, 1, SC_ALPHA, st));
@@ -815,6 +887,31 @@ int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
   HIP_OK(hipStreamSynchronize(st));
   for (int i = 0; i < s->N; ++i)
     for (int j = i + 1; j < s->N; ++j) out[(int64_t)i * s->N + j] = 0.0;
+  return IPMZ_OK;
+}
+
+int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refine) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0))
+    return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  if (enable && !s->mws) {
+    const int64_t bytes = mixed_ws_bytes(s->N, s->ctx->nbo);
+    void* w = nullptr;
+    if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+    s->allocs.push_back(w);
+    s->mws = static_cast<char*>(w);
+    mixed_ws_carve(s->mws, s->N, s->ctx->nbo, s->mw);
+  }
+  s->mixed = enable != 0;
+  s->ir_tol = tol;
+  s->ir_max = max_refine;
+  if (s->gexec) {  // the captured step has the other solver baked in
+    hipGraphExecDestroy(s->gexec);
+    hipGraphDestroy(s->graph);
+    s->gexec = nullptr;
+    s->graph = nullptr;
+  }
   return IPMZ_OK;
 }
 

@@ -44,6 +44,31 @@ __device__ __forceinline__ double4_t mfma_f64_16x16x4(double a, double b, double
   return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
 }
 
+// One MFMA shape for both precisions of the factorization: 16 x 16 x 4 with
+// A/B fragments (row l & 15, k l >> 4) -- identical for f64 and f32 -- and
+// the accumulator map that differs: f64 rows (l >> 4) + 4 r, f32 rows
+// 4 (l >> 4) + r (cdna_hip_programming.md §3; the f32 form is an exact f32
+// fma chain at 2x the f64 rate, 32 vs 64 cycles per instruction).
+typedef float float4_t __attribute__((ext_vector_type(4)));
+template <typename T>
+struct Mfma;
+template <>
+struct Mfma<double> {
+  typedef double4_t acc_t;
+  typedef double2 vec2_t;
+  static __device__ __forceinline__ acc_t mma(double a, double b, acc_t c) { return mfma_f64_16x16x4(a, b, c); }
+  static __device__ __forceinline__ int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+template <>
+struct Mfma<float> {
+  typedef float4_t acc_t;
+  typedef float2 vec2_t;
+  static __device__ __forceinline__ acc_t mma(float a, float b, acc_t c) {
+    return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ int row(int lane, int r) { return 4 * (lane >> 4) + r; }
+};
+
 // Wave-level all-reductions (wave64) on the VALU: DPP inside 16-lane rows
 // (xor 1, xor 2, rotate 4, rotate 8), then v_permlane16_swap / 32_swap across
 // rows (gfx950).  No LDS round trips (ds_bpermute-based __shfl_xor costs ~6
@@ -71,6 +96,21 @@ __device__ __forceinline__ double fast_rcp(double d) {
   e = fma(-d, r, 1.0);
   return fma(r, e, r);
 }
+template <int CTRL>
+__device__ __forceinline__ float dpp_float(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_t(double v) { return dpp_double<CTRL>(v); }
+template <int CTRL>
+__device__ __forceinline__ float dpp_t(float v) { return dpp_float<CTRL>(v); }
+__device__ __forceinline__ double readlane_t(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l),
+                          __builtin_amdgcn_readlane(__double2loint(v), l));
+}
+__device__ __forceinline__ float readlane_t(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
 __device__ __forceinline__ void swap16(double v, double& a, double& b) {
   const auto lo = __builtin_amdgcn_permlane16_swap(__double2loint(v), __double2loint(v), false, false);
   const auto hi = __builtin_amdgcn_permlane16_swap(__double2hiint(v), __double2hiint(v), false, false);
@@ -93,6 +133,17 @@ __device__ __forceinline__ double wave_sum(double v) {
   v = a + b;
   swap32(v, a, b);
   return a + b;
+}
+__device__ __forceinline__ double wave_max(double v) {
+  v = fmax(v, dpp_double<0xb1>(v));
+  v = fmax(v, dpp_double<0x4e>(v));
+  v = fmax(v, dpp_double<0x124>(v));
+  v = fmax(v, dpp_double<0x128>(v));
+  double a, b;
+  swap16(v, a, b);
+  v = fmax(a, b);
+  swap32(v, a, b);
+  return fmax(a, b);
 }
 __device__ __forceinline__ double wave_min(double v) {
   v = fmin(v, dpp_double<0xb1>(v));

@@ -125,9 +125,11 @@ using namespace diag64;
 // same launch, possibly through another CU's L1).  COH: Linv and D are stored
 // write-through (agent-scope relaxed atomics) for consumers in other
 // workgroups of the same launch.  clk != nullptr records stage clocks.
-template <bool COH, bool LSC = false>
-__device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, int k0, int b, double* __restrict__ D,
-                                            double* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
+// TS: storage type of K, D and L^{-1} (float for the fp32 factor of the
+// mixed-precision path: the 64 x 64 block itself is factored in fp64).
+template <bool COH, bool LSC = false, typename TS = double>
+__device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
+                                            TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
@@ -145,8 +147,8 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
     for (int q = 0; q < 16; ++q) {
       const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
       const int r2 = rr < b ? rr : 0, c2 = cc <= r2 ? cc : 0;
-      const double* src = &K[(int64_t)(k0 + r2) * ld + k0 + c2];
-      t[q] = LSC ? ld_sc1(src) : *src;
+      const TS* src = &K[(int64_t)(k0 + r2) * ld + k0 + c2];
+      t[q] = (double)(LSC ? ld_sc1(src) : *src);
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -215,15 +217,15 @@ __device__ __forceinline__ void diag64_body(double* __restrict__ K, int64_t ld, 
 #pragma unroll 4
   for (int idx = tid; idx < 64 * 64; idx += 256) {
     const int rr = idx >> 6, cc = idx & 63;
-    if (rr < b && cc < rr) K[(int64_t)(k0 + rr) * ld + k0 + cc] = M[rr * DS + cc];
-    const double x = cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc]);
+    if (rr < b && cc < rr) K[(int64_t)(k0 + rr) * ld + k0 + cc] = (TS)M[rr * DS + cc];
+    const TS x = (TS)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc]));
     if constexpr (COH) __hip_atomic_store(&Linv[idx], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else Linv[idx] = x;
   }
   if (tid < b) {
     const double dk = dsh[tid];
-    if constexpr (COH) __hip_atomic_store(&D[k0 + tid], dk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else D[k0 + tid] = dk;
+    if constexpr (COH) __hip_atomic_store(&D[k0 + tid], (TS)dk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else D[k0 + tid] = (TS)dk;
     if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(info, k0 + tid + 1);  // first non-finite pivot
   }
   if (clkbuf) {

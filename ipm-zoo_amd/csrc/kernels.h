@@ -34,6 +34,10 @@ struct TrailTimer {  // HIP-event pairs around every trailing-update launch
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                        int* info, hipStream_t st, TrailTimer* timer = nullptr, hipStream_t st2 = nullptr,
                        hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr);
+// the same blocked LDL^T in fp32 (fp32 MFMA trailing update, kernel-chain
+// panel path): the factor of the mixed-precision solve (C5)
+hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev);
 // one fused diag + TRSM + strip launch for the inner block [j0, j0 + bi) of an
 // outer panel ending at column c1 (panel.hip); Wc = W + (j0 - k0), row-indexed
 hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
@@ -71,6 +75,30 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
 // ybuf, zbuf: N doubles; ctrl: 2 + 2*ceil(N/64) unsigned (zeroed inside).
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
                                  double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st);
+// fp32 variant; skip (device flag, may be null): return at once when set
+hipError_t ldlt_solve_persistent(const float* K, int64_t ld, int N, const float* D, const float* Linv, int nbi,
+                                 float* b, float* ybuf, float* zbuf, unsigned* ctrl, hipStream_t st,
+                                 const unsigned* skip = nullptr);
+
+// mixed.hip: fp32 factor of S K S + fp64 iterative refinement (config C5) ----
+struct MixedWs {
+  int N = 0, nbo = 256;
+  int64_t ld32 = 0;
+  float *K32 = nullptr, *D32 = nullptr, *Linv32 = nullptr, *W32 = nullptr;
+  float *y32 = nullptr, *z32 = nullptr, *r32 = nullptr;
+  unsigned *ctrl = nullptr, *state = nullptr;
+  int* info = nullptr;
+  double *s = nullptr, *x = nullptr, *colp = nullptr, *rowp = nullptr, *part = nullptr;
+  double* stat = nullptr;  // {||r||_inf / ||b||_inf, corrections} of the last solve
+};
+int64_t mixed_ws_bytes(int N, int nbo);
+int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w);  // base == nullptr: size only
+// scale + convert + fp32 factor of the lower triangle of K (fp64, row-major)
+hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipEvent_t* ev,
+                        int nev, TrailTimer* timer = nullptr);
+// b <- K^{-1} b by iterative refinement (device-side stop test)
+hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,
+                       hipStream_t st);
 
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };

@@ -45,81 +45,79 @@ namespace ipmz {
 //   everyone: A[r][c] -= l_r w_c (k < c <= r),  X^T[r][c] -= l_c x_r (r <= k < c)
 // The update is the reference's  sum -= L[r][k] * L[c][k] * D[k]
 // (LinearSolvers.cpp:33) with L[c][k] * D[k] = w_c formed exactly once.
-template <int NB>
-__global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restrict__ K, int64_t ld, int k0, int b,
-                                                                double* __restrict__ D, double* __restrict__ Linv,
+template <typename T, int NB>
+__global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(T* __restrict__ K, int64_t ld, int k0, int b,
+                                                                T* __restrict__ D, T* __restrict__ Linv,
                                                                 int* __restrict__ info, int64_t sK, int64_t sD,
                                                                 int64_t sL) {
-  constexpr int T = NB / 4, NT = T * T;
+  constexpr int TG = NB / 4, NT = TG * TG;
   K += blockIdx.x * sK;  // batch: one workgroup per QP
   D += blockIdx.x * sD;
   Linv += blockIdx.x * sL;
-  __shared__ double M[NB][NB + 1];  // coalesced staging in/out
-  __shared__ double wsh[2][NB], lsh[2][NB], xsh[2][NB];
-  __shared__ double dsh[NB];
+  __shared__ T M[NB][NB + 1];  // coalesced staging in/out
+  __shared__ T wsh[2][NB], lsh[2][NB], xsh[2][NB];
+  __shared__ T dsh[NB];
   const int tid = threadIdx.x;
-  const int tr = tid % T, tc = tid / T;
+  const int tr = tid % TG, tc = tid / TG;
   const int lane = tid & 63, wave = tid >> 6;
   for (int idx = tid; idx < NB * NB; idx += NT) {
     const int r = idx / NB, c = idx % NB;
-    M[r][c] = (r < b && c <= r) ? K[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? 1.0 : 0.0);
+    M[r][c] = (r < b && c <= r) ? K[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? T(1) : T(0));
   }
   __syncthreads();
-  double v[4][4];
+  T v[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) v[a][c4] = M[tr + T * a][tc + T * c4];
+    for (int c4 = 0; c4 < 4; ++c4) v[a][c4] = M[tr + TG * a][tc + TG * c4];
 
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb) {
-    for (int kk = 0; kk < T; ++kk) {
-      const int k = kb * T + kk;
+    for (int kk = 0; kk < TG; ++kk) {
+      const int k = kb * TG + kk;
       if (k >= b) break;
       const int buf = k & 1;
-      const int owner_wave = (kk * T) >> 6;
+      const int owner_wave = (kk * TG) >> 6;
       if (wave == owner_wave) {
-        const int diag_lane = (kk * T + kk) & 63;
-        const double draw =
-            __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v[kb][kb]), diag_lane),
-                             __builtin_amdgcn_readlane(__double2loint(v[kb][kb]), diag_lane));
-        const double dk = draw == 0.0 ? 1e-8 : draw;
-        const double rdk = 1.0 / dk;
+        const int diag_lane = (kk * TG + kk) & 63;
+        const T draw = readlane_t(v[kb][kb], diag_lane);
+        const T dk = draw == T(0) ? T(1e-8) : draw;
+        const T rdk = T(1) / dk;
         if (tc == kk) {
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
-            const int r = tr + T * a;
-            const double w = v[a][kb];
+            const int r = tr + TG * a;
+            const T w = v[a][kb];
             if (r > k) {
-              const double l = w * rdk;
+              const T l = w * rdk;
               v[a][kb] = l;
               wsh[buf][r] = w;
               lsh[buf][r] = l;
             } else if (r < k) {
               xsh[buf][r] = w;
             } else {
-              xsh[buf][r] = 1.0;
+              xsh[buf][r] = T(1);
               dsh[k] = dk;
             }
           }
         }
       }
       __syncthreads();
-      double lr[4], xr[4];
+      T lr[4], xr[4];
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
-        const int r = tr + T * a;
-        lr[a] = r > k ? lsh[buf][r] : 0.0;
-        xr[a] = r <= k ? xsh[buf][r] : 0.0;
+        const int r = tr + TG * a;
+        lr[a] = r > k ? lsh[buf][r] : T(0);
+        xr[a] = r <= k ? xsh[buf][r] : T(0);
       }
 #pragma unroll
       for (int c4 = kb; c4 < 4; ++c4) {  // columns of blocks < kb are finished
-        const int c = tc + T * c4;
+        const int c = tc + TG * c4;
         if (c > k) {
-          const double wc = wsh[buf][c], lc = lsh[buf][c];
+          const T wc = wsh[buf][c], lc = lsh[buf][c];
 #pragma unroll
           for (int a = 0; a < 4; ++a) {
-            const int r = tr + T * a;
+            const int r = tr + TG * a;
             if (r >= c) v[a][c4] = fma(-lr[a], wc, v[a][c4]);
             else if (r <= k) v[a][c4] = fma(-lc, xr[a], v[a][c4]);
           }
@@ -131,22 +129,22 @@ __global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(double* __restri
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int c4 = 0; c4 < 4; ++c4) M[tr + T * a][tc + T * c4] = v[a][c4];
+    for (int c4 = 0; c4 < 4; ++c4) M[tr + TG * a][tc + TG * c4] = v[a][c4];
   __syncthreads();
   // write back L (strict lower), D, and L^{-1} (NB x NB row-major, identity-padded)
   for (int idx = tid; idx < NB * NB; idx += NT) {
     const int r = idx / NB, c = idx % NB;
     if (r < b && c < r) K[(int64_t)(k0 + r) * ld + k0 + c] = M[r][c];
-    double x;
-    if (r == c) x = 1.0;
+    T x;
+    if (r == c) x = T(1);
     else if (c < r && r < b) x = M[c][r];
-    else x = 0.0;
+    else x = T(0);
     Linv[idx] = x;
   }
   for (int k = tid; k < b; k += NT) {
-    const double dk = dsh[k];
+    const T dk = dsh[k];
     D[k0 + k] = dk;
-    if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(info, k0 + k + 1);  // first non-finite pivot
+    if (!(fabs((double)dk) <= 1.7976931348623157e308)) atomicMin(info, k0 + k + 1);  // first non-finite pivot
   }
 }
 
@@ -325,18 +323,19 @@ hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv
 // row = (l >> 4) + 4 * reg (cdna_hip_programming.md §3, f64 form).
 enum { EPI_SUB = 0, EPI_PANEL = 1, EPI_STORE = 2, EPI_SUB_STRIP = 3 };
 
-struct GemmArgs {
+template <typename T>
+struct GemmArgsT {
   int M, N, Kd;
-  const double* A;
+  const T* A;
   int64_t lda;
-  const double* B;
+  const T* B;
   int64_t ldb;
-  double* C;
+  T* C;
   int64_t ldc;
   // EPI_PANEL: W[i][j] = acc, C[i][j] = acc / dvec[j]
-  double* W;
+  T* W;
   int64_t ldw;
-  const double* dvec;
+  const T* dvec;
   // lower-triangle restriction: tile skipped when row0+gi_end <= col0+gj_start
   int64_t row0, col0;
   int lower;  // 0: full rectangle, 1: skip strictly-upper tiles, 2: triangular grid (row0==col0, BM==BN)
@@ -344,16 +343,18 @@ struct GemmArgs {
   // batch (blockIdx.y = QP): element strides between the QPs' operands
   int64_t sA, sB, sC, sW, sD;
 };
+using GemmArgs = GemmArgsT<double>;
 
 // Tile pipeline: one LDS buffer is computed while the next k-chunk sits in
 // registers (loads issued before the MFMAs, written to the other buffer
 // after them): one barrier per 16-deep k-chunk.
-template <int BM, int BN, int NTH>
+template <typename T, int BM, int BN, int NTH>
 struct TileLoader {
+  typedef typename Mfma<T>::vec2_t V2;
   static constexpr int BK = 16, PAD = 18;
   static constexpr int QA = BM * BK / 2 / NTH, QB = BN * BK / 2 / NTH;  // double2 per thread
-  double2 ra[QA], rb[QB];
-  __device__ __forceinline__ void load(const GemmArgs& g, int i0, int j0, int kk) {
+  V2 ra[QA], rb[QB];
+  __device__ __forceinline__ void load(const GemmArgsT<T>& g, int i0, int j0, int kk) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
@@ -366,24 +367,26 @@ struct TileLoader {
       rb[q] = fetch(g.B, g.ldb, j0 + r, g.N, kk + c, g.Kd);
     }
   }
-  __device__ __forceinline__ void store(double* As, double* Bs) const {
+  __device__ __forceinline__ void store(T* As, T* Bs) const {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
       const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
-      *reinterpret_cast<double2*>(&As[r * PAD + c]) = ra[q];
+      *reinterpret_cast<V2*>(&As[r * PAD + c]) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
       const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
-      *reinterpret_cast<double2*>(&Bs[r * PAD + c]) = rb[q];
+      *reinterpret_cast<V2*>(&Bs[r * PAD + c]) = rb[q];
     }
   }
-  static __device__ __forceinline__ double2 fetch(const double* P, int64_t ld, int row, int rows, int k, int Kd) {
-    double2 t = make_double2(0.0, 0.0);
+  static __device__ __forceinline__ V2 fetch(const T* P, int64_t ld, int row, int rows, int k, int Kd) {
+    V2 t;
+    t.x = T(0);
+    t.y = T(0);
     if (row < rows) {
-      const double* p = P + (int64_t)row * ld + k;
-      if (k + 1 < Kd) t = *reinterpret_cast<const double2*>(p);
+      const T* p = P + (int64_t)row * ld + k;
+      if (k + 1 < Kd) t = *reinterpret_cast<const V2*>(p);
       else if (k < Kd) t.x = p[0];
     }
     return t;
@@ -429,9 +432,10 @@ __device__ __forceinline__ void grouped_tile(int bid, int ntm, int& tm, int& tn)
 // 8-wave tiles are sized for two workgroups per CU = 4 waves per SIMD, which
 // needs <= 128 VGPRs: pinned with amdgpu_waves_per_eu (the compiler otherwise
 // drifts to 129+ and silently halves the occupancy)
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
+template <typename T, int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
 __global__ __launch_bounds__(64 * WGM * WGN)
-__attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_kernel(GemmArgs g) {
+__attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_kernel(GemmArgsT<T> g) {
+  typedef Mfma<T> MF;
   constexpr int BK = 16, PAD = 18, NTH = 64 * WGM * WGN;
   if (blockIdx.y) {
     const int64_t z = blockIdx.y;
@@ -444,8 +448,8 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
     }
   }
   constexpr int WM = BM / WGM, WN = BN / WGN, TM = WM / 16, TN = WN / 16;
-  __shared__ __attribute__((aligned(16))) double As[2][BM * PAD];
-  __shared__ __attribute__((aligned(16))) double Bs[2][BN * PAD];
+  __shared__ __attribute__((aligned(16))) T As[2][BM * PAD];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BN * PAD];
 
   // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks
   // b and b+8 share an XCD, so consecutive logical tiles -- which share W
@@ -476,13 +480,13 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WGN, wc = wave % WGN;
-  double4_t acc[TM][TN];
+  typename MF::acc_t acc[TM][TN];
 #pragma unroll
   for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int b = 0; b < TN; ++b) acc[a][b] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    for (int b = 0; b < TN; ++b) acc[a][b] = (typename MF::acc_t){T(0), T(0), T(0), T(0)};
 
-  TileLoader<BM, BN, NTH> ld;
+  TileLoader<T, BM, BN, NTH> ld;
   const int nch = (g.Kd + BK - 1) / BK;
   ld.load(g, i0, j0, 0);
   ld.store(As[0], Bs[0]);
@@ -492,8 +496,8 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
   for (int t = 0; t < nch; ++t) {
     const int cur = t & 1;
     if (t + 1 < nch) ld.load(g, i0, j0, (t + 1) * BK);
-    const double* as = As[cur];
-    const double* bs = Bs[cur];
+    const T* as = As[cur];
+    const T* bs = Bs[cur];
 #pragma unroll
     for (int s = 0; s < BK / 4; ++s) {
       int ao = aoff + 4 * s, bo = boff + 4 * s;
@@ -501,7 +505,7 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
         asm volatile("" : "+v"(ao));
         asm volatile("" : "+v"(bo));
       }
-      double af[TM], bf[TN];
+      T af[TM], bf[TN];
 #pragma unroll
       for (int a = 0; a < TM; ++a) af[a] = as[ao + a * 16 * PAD];
 #pragma unroll
@@ -509,7 +513,7 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
 #pragma unroll
       for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int b = 0; b < TN; ++b) acc[a][b] = mfma_f64_16x16x4(af[a], bf[b], acc[a][b]);
+        for (int b = 0; b < TN; ++b) acc[a][b] = MF::mma(af[a], bf[b], acc[a][b]);
     }
     if (t + 1 < nch) ld.store(As[cur ^ 1], Bs[cur ^ 1]);
     __syncthreads();
@@ -523,10 +527,10 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
       const int j = j0 + wc * WN + b * 16 + (lane & 15);
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int i = i0 + wr * WM + a * 16 + (lane >> 4) + 4 * r;
+        const int i = i0 + wr * WM + a * 16 + MF::row(lane, r);
         if (i < g.M && j < g.N) {
-          const double v = acc[a][b][r];
-          double* cp = g.C + (int64_t)i * g.ldc + j;
+          const T v = acc[a][b][r];
+          T* cp = g.C + (int64_t)i * g.ldc + j;
           if (EPI == EPI_SUB || EPI == EPI_SUB_STRIP) {
             *cp = *cp - v;
           } else if (EPI == EPI_PANEL) {
@@ -540,8 +544,8 @@ __attribute__((amdgpu_waves_per_eu(WGM * WGN == 8 ? 4 : 1))) void gemm_nt_f64_ke
     }
 }
 
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
-static hipError_t launch_gemm(GemmArgs g, hipStream_t st, int batch = 1) {
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2, typename T = double>
+static hipError_t launch_gemm(GemmArgsT<T> g, hipStream_t st, int batch = 1) {
   g.ntm = (g.M + BM - 1) / BM;
   g.ntn = (g.N + BN - 1) / BN;
   if (g.ntm == 0 || g.ntn == 0 || g.Kd == 0) return hipSuccess;
@@ -552,7 +556,7 @@ static hipError_t launch_gemm(GemmArgs g, hipStream_t st, int batch = 1) {
     if (BM == BN) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
     else g.lower = 1;
   }
-  hipLaunchKernelGGL((gemm_nt_f64_kernel<BM, BN, EPI, WGM, WGN, OPT>), dim3((unsigned)nblk, (unsigned)batch),
+  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, EPI, WGM, WGN, OPT>), dim3((unsigned)nblk, (unsigned)batch),
                      dim3(64 * WGM * WGN), 0, st, g);
   return hipGetLastError();
 }
@@ -615,7 +619,13 @@ static void launch_diag64(int variant, int B, hipStream_t st, double* K, int64_t
     hipLaunchKernelGGL((ldlt_diag64_wave_kernel<true, false>), dim3(B), dim3(64), 0, st, K, ld, j0, bi, D, Lb, info, sK,
                        sD, sL);
   else
-    hipLaunchKernelGGL((ldlt_diag_kernel<64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+    hipLaunchKernelGGL((ldlt_diag_kernel<double, 64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+}
+
+// fp32 factor (mixed-precision path): the register-resident 4-wave kernel
+static void launch_diag64(int, int B, hipStream_t st, float* K, int64_t ld, int j0, int bi, float* D, float* Lb,
+                          int* info, int64_t sK, int64_t sD, int64_t sL) {
+  hipLaunchKernelGGL((ldlt_diag_kernel<float, 64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
 }
 
 // stage clock (s_memtime) of one ldlt_diag64_blk_kernel run, for kbench
@@ -630,7 +640,7 @@ hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int*
 
 hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st) {
   if (nbi == 128)
-    hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(1), dim3(1024), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
+    hipLaunchKernelGGL((ldlt_diag_kernel<double, 128>), dim3(1), dim3(1024), 0, st, K, ld, k0, nbi, D, Linv, info, 0, 0, 0);
   else  // nbi = -variant - 64 .. : kernel variants at 64
     launch_diag64(nbi <= -64 ? -nbi - 64 : 0, 1, st, K, ld, k0, 64, D, Linv, info, 0, 0, 0);
   return hipGetLastError();
@@ -680,10 +690,11 @@ hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc,
 }
 
 // C[i][j] -= sum_k A[i][k] B[j][k] over the lower part of a trailing region.
-hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
-                       const BatchStrides* bs) {
-  GemmArgs g{};
+template <typename T>
+static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, const T* B, int64_t ldb, T* C,
+                                int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
+                                const BatchStrides* bs) {
+  GemmArgsT<T> g{};
   int batch = 1;
   if (bs && bs->B > 1) {
     batch = bs->B;
@@ -712,6 +723,11 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   // (kbench, R = 11008, rank 256)
   return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch)
                       : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
+}
+hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
+                       double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
+                       const BatchStrides* bs) {
+  return gemm_nt_sub_t<double>(M, N, Kd, A, lda, B, ldb, C, ldc, row0, col0, square_lower, st, bs);
 }
 
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
@@ -747,31 +763,44 @@ static int panel_mode() {
   return mode;
 }
 
-static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo,
-                               int nbo, int nbi, int* info, hipStream_t st, const BatchStrides* bs = nullptr,
-                               unsigned* pctrl = nullptr) {
+// fused panel kernels (fp64): one launch per outer panel / per inner block
+static hipError_t fused_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo, int nbo,
+                              int nbi, int* info, unsigned* pctrl, hipStream_t st) {
+  if (panel_mode() == 2)
+    return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
+  hipError_t e = hipSuccess;
+  for (int j0 = k0; j0 < k0 + bo && e == hipSuccess; j0 += nbi) {
+    const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
+    e = panel_step(K, ld, N, j0, bi, k0 + bo, D, Linv + (int64_t)(j0 / nbi) * nbi * nbi, W + (j0 - k0), nbo, info,
+                   pctrl, st);
+  }
+  return e;
+}
+static hipError_t fused_panel(float*, int64_t, int, float*, float*, float*, int, int, int, int, int*, unsigned*,
+                              hipStream_t) {
+  return hipErrorInvalidValue;  // fp32 factors use the kernel chain
+}
+
+template <typename T>
+static hipError_t factor_panel(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int k0, int bo, int nbo, int nbi,
+                               int* info, hipStream_t st, const BatchStrides* bs = nullptr, unsigned* pctrl = nullptr) {
   hipError_t e = hipSuccess;
   const int B = bs ? bs->B : 1;
   const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
-  if (pctrl && B == 1 && nbi == 64 && panel_mode() == 2)
-    return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
+  if (std::is_same<T, double>::value && pctrl && B == 1 && nbi == 64 && panel_mode() >= 1)
+    return fused_panel(K, ld, N, D, Linv, W, k0, bo, nbo, nbi, info, pctrl, st);
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
-    double* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
-    if (pctrl && B == 1 && nbi == 64 && panel_mode() == 1) {
-      if ((e = panel_step(K, ld, N, j0, bi, k0 + bo, D, Lb, W + (j0 - k0), nbo, info, pctrl, st)) != hipSuccess)
-        return e;
-      continue;
-    }
+    T* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
     if (nbi == 128)
-      hipLaunchKernelGGL((ldlt_diag_kernel<128>), dim3(B), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
+      hipLaunchKernelGGL((ldlt_diag_kernel<T, 128>), dim3(B), dim3(1024), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     else
       launch_diag64(diag64_variant(), B, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
     if ((e = hipGetLastError()) != hipSuccess) return e;
     const int r1 = j0 + bi;
     if (r1 >= N) continue;
     // panel TRSM: rows [r1, N): T = A21 L11^{-T}, W21 = T, L21 = T / D1
-    GemmArgs g{};
+    GemmArgsT<T> g{};
     g.M = N - r1;
     g.N = bi;
     g.Kd = bi;
@@ -795,8 +824,8 @@ static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* 
     // strip update of the remaining columns of this outer panel
     const int c1 = k0 + bo;
     if (r1 < c1) {
-      e = gemm_nt_sub(N - r1, c1 - r1, bi, W + (int64_t)r1 * nbo + (j0 - k0), nbo, K + (int64_t)r1 * ld + j0, ld,
-                      K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st, bs);
+      e = gemm_nt_sub_t<T>(N - r1, c1 - r1, bi, W + (int64_t)r1 * nbo + (j0 - k0), nbo, K + (int64_t)r1 * ld + j0, ld,
+                           K + (int64_t)r1 * ld + r1, ld, r1, r1, false, st, bs);
       if (e != hipSuccess) return e;
     }
   }
@@ -805,10 +834,11 @@ static hipError_t factor_panel(double* K, int64_t ld, int N, double* D, double* 
 
 // Rank-bo update of the column block [c0, c1) (rows >= c0) with outer panel
 // k (W_k rows, L_k = K[:, k0:k0+bo)); square = the whole trailing triangle.
-static hipError_t panel_update(double* K, int64_t ld, int N, const double* Wk, int nbo, int k0, int bo, int c0,
-                               int c1, bool square, hipStream_t st, const BatchStrides* bs = nullptr) {
+template <typename T>
+static hipError_t panel_update(T* K, int64_t ld, int N, const T* Wk, int nbo, int k0, int bo, int c0, int c1,
+                               bool square, hipStream_t st, const BatchStrides* bs = nullptr) {
   if (c0 >= c1 || c0 >= N) return hipSuccess;
-  return gemm_nt_sub(N - c0, c1 - c0, bo, Wk + (int64_t)c0 * nbo, nbo, K + (int64_t)c0 * ld + k0, ld,
+  return gemm_nt_sub_t<T>(N - c0, c1 - c0, bo, Wk + (int64_t)c0 * nbo, nbo, K + (int64_t)c0 * ld + k0, ld,
                      K + (int64_t)c0 * ld + c0, ld, c0, c0, square, st, bs);
 }
 
@@ -839,16 +869,17 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 // columns A is factoring; W is triple-buffered so A's P_{k+1} never
 // overwrites the W_{k-2} a late B_{k-2} could still read (B_{k-2} precedes
 // N_{k-1} on B).  A waits for B's tail at the end.
-hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
-                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
-                       unsigned* pctrl) {
+template <typename T>
+static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int nbo, int nbi, int* info,
+                                hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
+                                unsigned* pctrl) {
   if (N <= 0) return hipSuccess;
   if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
   const int npan = (N + nbo - 1) / nbo;
   const bool two = st2 != nullptr && ev != nullptr && nev >= 2 * npan + 2;
   const int64_t wsz = (int64_t)N * nbo;
-  auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };
+  auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };  // T*
   auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
   hipError_t e = factor_panel(K, ld, N, D, Linv, Wb(0), 0, pw(0), nbo, nbi, info, st, nullptr, pctrl);
   if (e != hipSuccess) return e;
@@ -902,6 +933,16 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
   }
   if ((e = hipEventRecord(evJoin, st2)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, evJoin, 0);
+}
+
+hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
+                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
+                       unsigned* pctrl) {
+  return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, pctrl);
+}
+hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev) {
+  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, nullptr);
 }
 
 }  // namespace ipmz

@@ -15,10 +15,12 @@ namespace ipmz {
 // error word instead of a hung queue
 constexpr unsigned long long SPIN_TICKS = 50000000ull;  // 0.5 s
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ void st_sc1(double* p, double v) {
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* p, T v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 

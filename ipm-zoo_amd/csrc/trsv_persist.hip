@@ -32,9 +32,10 @@ namespace {
 constexpr int PNT = 256;                 // threads per workgroup
 
 // quad (4-lane) all-reduce on the VALU
-__device__ __forceinline__ double quad_sum(double v) {
-  v += dpp_double<0xb1>(v);
-  v += dpp_double<0x4e>(v);
+template <typename T>
+__device__ __forceinline__ T quad_sum(T v) {
+  v += dpp_t<0xb1>(v);
+  v += dpp_t<0x4e>(v);
   return v;
 }
 }  // namespace
@@ -42,14 +43,16 @@ __device__ __forceinline__ double quad_sum(double v) {
 // NB = 64: forward tiles are read row-wise (thread t: row t>>2, 16 columns
 // (t&3)*16..+16 -> 8 x 16-byte loads), backward tiles column-wise (thread t:
 // column t&63, rows (t>>6)*16..+16).
-template <int NB>
-__global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __restrict__ K, int64_t ld, int N,
-                                                              const double* __restrict__ D,
-                                                              const double* __restrict__ Linv, double* b,
-                                                              double* ybuf, double* zbuf, unsigned* ctrl, int nblk) {
+template <typename T, int NB>
+__global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const T* __restrict__ K, int64_t ld, int N,
+                                                              const T* __restrict__ D, const T* __restrict__ Linv,
+                                                              T* b, T* ybuf, T* zbuf, unsigned* ctrl, int nblk,
+                                                              const unsigned* __restrict__ skip) {
+  typedef typename Mfma<T>::vec2_t V2;
+  if (skip && *skip) return;  // mixed-precision refinement already converged
   static_assert(NB == 64, "persistent solve is written for 64-row blocks");
-  __shared__ double vec[NB];      // y_K / x_K of the tile being applied, then v / u
-  __shared__ double red[4][NB];   // cross-wave reduction (backward)
+  __shared__ T vec[NB];      // y_K / x_K of the tile being applied, then v / u
+  __shared__ T red[4][NB];   // cross-wave reduction (backward)
   __shared__ unsigned sh_ticket, sh_ok;
   unsigned* counter = ctrl;
   unsigned* err = ctrl + 1;
@@ -71,19 +74,19 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
       const int rows = N - J0 < NB ? N - J0 : NB;
       const int r = tid >> 2, c0 = (tid & 3) * 16;
       // diagonal-block inverse row r (Linv_J, NB x NB) and b_J[r]
-      double li[16];
+      T li[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) li[q] = Linv[(int64_t)J * NB * NB + r * NB + c0 + q];
-      double acc = 0.0;
-      double tile[16];
+      T acc = T(0);
+      T tile[16];
       auto load_tile = [&](int Kb) {
         const bool in = r < rows;
-        const double* p = K + (int64_t)(J0 + (in ? r : 0)) * ld + Kb * NB + c0;
+        const T* p = K + (int64_t)(J0 + (in ? r : 0)) * ld + Kb * NB + c0;
 #pragma unroll
         for (int q = 0; q < 16; q += 2) {
-          const double2 v2 = *reinterpret_cast<const double2*>(p + q);
-          tile[q] = in ? v2.x : 0.0;
-          tile[q + 1] = in ? v2.y : 0.0;
+          const V2 v2 = *reinterpret_cast<const V2*>(p + q);
+          tile[q] = in ? v2.x : T(0);
+          tile[q + 1] = in ? v2.y : T(0);
         }
       };
       if (J > 0) load_tile(0);
@@ -91,7 +94,7 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
         if (!wait_flag(&fflag[Kb], err, &sh_ok)) return;
         if (tid < NB) vec[tid] = ld_sc1(&ybuf[Kb * NB + tid]);
         __syncthreads();
-        double cur[16];
+        T cur[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) cur[q] = tile[q];
         if (Kb + 1 < J) load_tile(Kb + 1);  // next tile in flight during this product
@@ -100,10 +103,10 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
         __syncthreads();
       }
       acc = quad_sum(acc);
-      const double bv = r < rows ? b[J0 + r] : 0.0;
+      const T bv = r < rows ? b[J0 + r] : T(0);
       if ((tid & 3) == 0) vec[r] = bv - acc;  // v = b_J - L_J,<J y
       __syncthreads();
-      double y = 0.0;
+      T y = T(0);
 #pragma unroll
       for (int q = 0; q < 16; ++q) y = fma(li[q], vec[c0 + q], y);
       y = quad_sum(y);
@@ -118,26 +121,26 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
       const int rows = N - J0 < NB ? N - J0 : NB;
       const int c = lane, rq = wave * 16;
       // Linv_J^T column c: Linv_J[rq + q][c]
-      double li[16];
+      T li[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) li[q] = Linv[(int64_t)J * NB * NB + (rq + q) * NB + c];
-      double acc = 0.0;
-      double tile[16];
+      T acc = T(0);
+      T tile[16];
       auto load_tile = [&](int Kb) {  // L_KJ rows Kb*NB + rq.., column J0 + c
         const int R0 = Kb * NB + rq;
 #pragma unroll
         for (int q = 0; q < 16; ++q) {
           const int row = R0 + q;
-          tile[q] = (row < N && c < rows) ? K[(int64_t)row * ld + J0 + c] : 0.0;
+          tile[q] = (row < N && c < rows) ? K[(int64_t)row * ld + J0 + c] : T(0);
         }
       };
       if (J + 1 < nblk) load_tile(nblk - 1);
       if (!wait_flag(&fflag[J], err, &sh_ok)) return;  // z_J ready
       for (int Kb = nblk - 1; Kb > J; --Kb) {
         if (!wait_flag(&bflag[Kb], err, &sh_ok)) return;
-        if (tid < NB) vec[tid] = (Kb * NB + tid < N) ? ld_sc1(&b[Kb * NB + tid]) : 0.0;
+        if (tid < NB) vec[tid] = (Kb * NB + tid < N) ? ld_sc1(&b[Kb * NB + tid]) : T(0);
         __syncthreads();
-        double cur[16];
+        T cur[16];
 #pragma unroll
         for (int q = 0; q < 16; ++q) cur[q] = tile[q];
         if (Kb - 1 > J) load_tile(Kb - 1);
@@ -148,11 +151,11 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
       red[wave][c] = acc;
       __syncthreads();
       if (tid < NB) {
-        const double t = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
-        vec[tid] = tid < rows ? ld_sc1(&zbuf[J0 + tid]) - t : 0.0;  // u = z_J - sum L_KJ^T x_K
+        const T t = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+        vec[tid] = tid < rows ? ld_sc1(&zbuf[J0 + tid]) - t : T(0);  // u = z_J - sum L_KJ^T x_K
       }
       __syncthreads();
-      double x = 0.0;
+      T x = T(0);
 #pragma unroll
       for (int q = 0; q < 16; ++q) x = fma(li[q], vec[rq + q], x);
       red[wave][c] = x;
@@ -163,8 +166,9 @@ __global__ __launch_bounds__(PNT) void trsv_persistent_kernel(const double* __re
   }
 }
 
-hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
-                                 double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st) {
+template <typename T>
+static hipError_t solve_persistent_t(const T* K, int64_t ld, int N, const T* D, const T* Linv, int nbi, T* b, T* ybuf,
+                                     T* zbuf, unsigned* ctrl, hipStream_t st, const unsigned* skip = nullptr) {
   if (N <= 0) return hipSuccess;
   if (nbi != 64) return hipErrorInvalidValue;
   const int nblk = (N + 63) / 64;
@@ -173,9 +177,19 @@ hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const doubl
   // resident grid: 3 workgroups per CU fit (LDS ~2.6 KB, < 128 VGPRs); the
   // dequeue makes residency a performance matter only
   int grid = 2 * nblk < 512 ? 2 * nblk : 512;
-  hipLaunchKernelGGL((trsv_persistent_kernel<64>), dim3(grid), dim3(PNT), 0, st, K, ld, N, D, Linv, b, ybuf, zbuf,
-                     ctrl, nblk);
+  hipLaunchKernelGGL((trsv_persistent_kernel<T, 64>), dim3(grid), dim3(PNT), 0, st, K, ld, N, D, Linv, b, ybuf, zbuf,
+                     ctrl, nblk, skip);
   return hipGetLastError();
+}
+
+hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
+                                 double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st) {
+  return solve_persistent_t<double>(K, ld, N, D, Linv, nbi, b, ybuf, zbuf, ctrl, st);
+}
+hipError_t ldlt_solve_persistent(const float* K, int64_t ld, int N, const float* D, const float* Linv, int nbi,
+                                 float* b, float* ybuf, float* zbuf, unsigned* ctrl, hipStream_t st,
+                                 const unsigned* skip) {
+  return solve_persistent_t<float>(K, ld, N, D, Linv, nbi, b, ybuf, zbuf, ctrl, st, skip);
 }
 
 }  // namespace ipmz

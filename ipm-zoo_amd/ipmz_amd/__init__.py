@@ -25,7 +25,8 @@ LIB_PATH = os.path.join(os.path.dirname(HERE), "lib", "libipmz.so")
 IPMZ_OK = 0
 ERR = {-1: "invalid argument", -2: "HIP error", -3: "out of device memory", -4: "no gfx950 device",
        -5: "bad state"}
-SC = dict(f=0, res=1, mu=2, alpha_aff=3, mu_aff=4, sigma=5, alpha=6, converged=7, mu_new=8, restarts=9)
+SC = dict(f=0, res=1, mu=2, alpha_aff=3, mu_aff=4, sigma=5, alpha=6, converged=7, mu_new=8, restarts=9,
+          ir_ratio_aff=10, ir_iters_aff=11, ir_ratio=12, ir_iters=13)
 SC_COUNT = 16
 PH = dict(step=0, assemble=1, factor=2, solve=3, trailing=4, eval=5)
 STEP_RESTART_IF_CONVERGED = 1
@@ -41,6 +42,7 @@ EXPORTS = [
     "ipmz_qp_get_kkt", "ipmz_qp_kkt_dim", "ipmz_qp_set_timing", "ipmz_qp_phase_times",
     "ipmz_batch_create", "ipmz_batch_size", "ipmz_batch_load_host", "ipmz_batch_initialize", "ipmz_batch_scalars",
     "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
+    "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
 ]
 
 _P = ctypes.POINTER(ctypes.c_double)
@@ -108,6 +110,10 @@ def _load():
         "ipmz_batch_get_state": ([_VP, _I, _I, _P], _I),
         "ipmz_batch_set_state": ([_VP, _I, _P], _I),
         "ipmz_batch_solve": ([_VP, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)], _I),
+        "ipmz_mixed_workspace_bytes": ([_VP, _I], _I64),
+        "ipmz_mixed_factor": ([_VP, _I, _VP, _I64, _VP, _I64], _I),
+        "ipmz_mixed_solve": ([_VP, _I, _VP, _I64, _VP, _VP, ctypes.c_double, _I, _P], _I),
+        "ipmz_qp_set_mixed_precision": ([_VP, _I, ctypes.c_double, _I], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -179,6 +185,20 @@ class Context:
     def ldlt_solve(self, N, K_ptr, ld, D_ptr, ws_ptr, b_ptr):
         return _check(lib.ipmz_ldlt_solve(self.h, N, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), _VP(b_ptr)),
                       "ipmz_ldlt_solve")
+
+    # -- mixed precision (C5): fp32 factor of S K S + fp64 refinement --
+    def mixed_workspace_bytes(self, N):
+        return lib.ipmz_mixed_workspace_bytes(self.h, N)
+
+    def mixed_factor(self, N, K_ptr, ld, ws_ptr, ws_bytes):
+        return _check(lib.ipmz_mixed_factor(self.h, N, _VP(K_ptr), ld, _VP(ws_ptr), ws_bytes), "ipmz_mixed_factor")
+
+    def mixed_solve(self, N, K_ptr, ld, ws_ptr, b_ptr, tol=1e-12, max_refine=10):
+        """b <- K^{-1} b (device pointers); returns (ratio reached, corrections)."""
+        stat = np.zeros(2)
+        _check(lib.ipmz_mixed_solve(self.h, N, _VP(K_ptr), ld, _VP(ws_ptr), _VP(b_ptr), tol, max_refine, _dp(stat)),
+               "ipmz_mixed_solve")
+        return float(stat[0]), int(stat[1])
 
 
 _default_ctx = None
@@ -271,6 +291,10 @@ class Optimizer:
 
     def step(self, flags=0):
         _check(lib.ipmz_qp_step(self.h, flags), "ipmz_qp_step")
+
+    def set_mixed_precision(self, enable=True, tol=1e-12, max_refine=10):
+        """Newton directions via the fp32 factor + fp64 refinement (config C5)."""
+        _check(lib.ipmz_qp_set_mixed_precision(self.h, int(enable), tol, max_refine), "ipmz_qp_set_mixed_precision")
 
     def scalars(self):
         out = np.zeros(SC_COUNT)
