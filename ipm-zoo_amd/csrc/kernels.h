@@ -37,7 +37,8 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
 // the same blocked LDL^T in fp32 (fp32 MFMA trailing update, kernel-chain
 // panel path): the factor of the mixed-precision solve (C5)
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
-                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev);
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
+                       unsigned* pctrl = nullptr);
 // one fused diag + TRSM + strip launch for the inner block [j0, j0 + bi) of an
 // outer panel ending at column c1 (panel.hip); Wc = W + (j0 - k0), row-indexed
 hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
@@ -46,6 +47,8 @@ hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, doub
 // inner blocks pipelined by flags instead of launch boundaries.  Lb0: L^{-1}
 // block of the panel's first inner block; Wp: the panel's W buffer (N x ldw)
 hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                       int* info, unsigned* ctrl, hipStream_t st);
+hipError_t outer_panel(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                        int* info, unsigned* ctrl, hipStream_t st);
 hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
                                int64_t ldb, double* C, int64_t ldc, hipStream_t st);
@@ -86,7 +89,7 @@ struct MixedWs {
   int64_t ld32 = 0;
   float *K32 = nullptr, *D32 = nullptr, *Linv32 = nullptr, *W32 = nullptr;
   float *y32 = nullptr, *z32 = nullptr, *r32 = nullptr;
-  unsigned *ctrl = nullptr, *state = nullptr;
+  unsigned *ctrl = nullptr, *state = nullptr, *pctrl = nullptr;
   int* info = nullptr;
   double *s = nullptr, *x = nullptr, *colp = nullptr, *rowp = nullptr, *part = nullptr;
   double* stat = nullptr;  // {||r||_inf / ||b||_inf, corrections} of the last solve

@@ -776,9 +776,10 @@ static hipError_t fused_panel(double* K, int64_t ld, int N, double* D, double* L
   }
   return e;
 }
-static hipError_t fused_panel(float*, int64_t, int, float*, float*, float*, int, int, int, int, int*, unsigned*,
-                              hipStream_t) {
-  return hipErrorInvalidValue;  // fp32 factors use the kernel chain
+static hipError_t fused_panel(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int k0, int bo, int nbo,
+                              int nbi, int* info, unsigned* pctrl, hipStream_t st) {
+  if (panel_mode() != 2) return hipErrorInvalidValue;  // fp32: outer-panel kernel only
+  return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
 }
 
 template <typename T>
@@ -787,7 +788,7 @@ static hipError_t factor_panel(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int
   hipError_t e = hipSuccess;
   const int B = bs ? bs->B : 1;
   const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
-  if (std::is_same<T, double>::value && pctrl && B == 1 && nbi == 64 && panel_mode() >= 1)
+  if (pctrl && B == 1 && nbi == 64 && (panel_mode() == 2 || (std::is_same<T, double>::value && panel_mode() == 1)))
     return fused_panel(K, ld, N, D, Linv, W, k0, bo, nbo, nbi, info, pctrl, st);
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
@@ -941,8 +942,8 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
   return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, pctrl);
 }
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
-                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev) {
-  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, nullptr);
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev, unsigned* pctrl) {
+  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, pctrl);
 }
 
 }  // namespace ipmz

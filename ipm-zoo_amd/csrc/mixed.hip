@@ -214,6 +214,7 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   w.ctrl = reinterpret_cast<unsigned*>(take((2 + 2 * nblk) * 4));
   w.state = reinterpret_cast<unsigned*>(take(64));
   w.info = reinterpret_cast<int*>(take(64));
+  w.pctrl = reinterpret_cast<unsigned*>(take(IPMZ_PANEL_CTRL_WORDS * 4));
   w.s = reinterpret_cast<double*>(take((int64_t)N * 8));
   w.x = reinterpret_cast<double*>(take((int64_t)N * 8));
   w.colp = reinterpret_cast<double*>(take(nblk * N * 8));
@@ -231,7 +232,8 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   hipLaunchKernelGGL(k_mx_to_f32, dim3(N), dim3(MNT), 0, st, K, ld, N, w.s, w.K32, w.ld32);
   hipError_t e = hipMemsetAsync(w.info, 0x7f, sizeof(int), st);
   if (e != hipSuccess) return e;
-  return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, ev, nev);
+  if ((e = hipMemsetAsync(w.pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), st)) != hipSuccess) return e;
+  return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, ev, nev, w.pctrl);
 }
 
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,

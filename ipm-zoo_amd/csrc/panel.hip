@@ -186,10 +186,15 @@ static_assert(OP_DIAG + OP_NBMAX <= OP_REG, "ctrl layout");
 static_assert(OP_WORDS <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
 }  // namespace
 
-__global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K, int64_t ld, int N, int k0, int c1,
-                                                          double* __restrict__ D, double* __restrict__ Lb0,
-                                                          double* __restrict__ Wp, int ldw, int* __restrict__ info,
+// T = float: the fp32 factor of the mixed-precision path (f32 MFMA TRSM and
+// strip pieces; the diagonal block is factored in fp64 and stored in fp32).
+template <typename T>
+__global__ __launch_bounds__(256) void outer_panel_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
+                                                          T* __restrict__ D, T* __restrict__ Lb0, T* __restrict__ Wp,
+                                                          int ldw, int* __restrict__ info,
                                                           unsigned* __restrict__ ctrl) {
+  typedef Mfma<T> MF;
+  typedef typename MF::acc_t acc_t;
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   __shared__ unsigned sh_ticket, sh_ok;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -203,28 +208,28 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
   const int rows = N - row0 < 64 ? N - row0 : 64;
   const bool region = c < nb;
   const int jend = region ? c : nb;  // blocks this chunk TRSMs: j < jend
-  double* As = smem;            // A rows, then L rows (64 x DS)
-  double* Bs = smem + 64 * DS;  // L_jj^{-1}, then W pieces (64 x DS)
+  T* As = reinterpret_cast<T*>(smem);              // A rows, then L rows (64 x DS)
+  T* Bs = reinterpret_cast<T*>(smem + 64 * DS);  // L_jj^{-1}, then W pieces (64 x DS)
   const int arow = 16 * wave + (lane & 15);
   bool ok = true;
   for (int j = 0; j < jend && ok; ++j) {
     const int j0 = k0 + 64 * j;
     const int bj = ce - j0 < 64 ? ce - j0 : 64;
-    double* Lb = Lb0 + (int64_t)j * 64 * 64;
+    T* Lb = Lb0 + (int64_t)j * 64 * 64;
     {  // this chunk's A rows of block j: loads in flight before the wait
-      double v[16];
+      T v[16];
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
         const int r2 = rr < rows ? rr : 0, c2 = cc < bj ? cc : 0;
-        const double* src = &K[(int64_t)(row0 + r2) * ld + j0 + c2];
+        const T* src = &K[(int64_t)(row0 + r2) * ld + j0 + c2];
         v[q] = j ? ld_sc1(src) : *src;
       }
       __syncthreads();  // previous block's strip finished reading As / Bs
 #pragma unroll
       for (int q = 0; q < 16; ++q) {
         const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
-        As[rr * DS + cc] = (rr < rows && cc < bj) ? v[q] : 0.0;
+        As[rr * DS + cc] = (rr < rows && cc < bj) ? v[q] : T(0);
       }
     }
     if (!(ok = wait_flag(&ctrl[OP_DIAG + j], err, &sh_ok))) break;
@@ -233,34 +238,34 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
       const int idx = tid + 256 * q;
       Bs[(idx >> 6) * DS + (idx & 63)] = ld_sc1(&Lb[idx]);
     }
-    double rd[4];
+    T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int col = 16 * n + (lane & 15);
-      rd[n] = col < bj ? 1.0 / ld_sc1(&D[j0 + col]) : 0.0;
+      rd[n] = col < bj ? T(1) / ld_sc1(&D[j0 + col]) : T(0);
     }
     __syncthreads();
     // ---- TRSM: wave w owns rows 16w..16w+15, all 64 columns
-    double4_t acc[4];
+    acc_t acc[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = (double4_t){0.0, 0.0, 0.0, 0.0};
+    for (int n = 0; n < 4; ++n) acc[n] = (acc_t){T(0), T(0), T(0), T(0)};
 #pragma unroll 4
     for (int s = 0; s < 16; ++s) {
       const int k = 4 * s + (lane >> 4);
-      const double a = As[arow * DS + k];
+      const T a = As[arow * DS + k];
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = mfma_f64_16x16x4(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
+      for (int n = 0; n < 4; ++n) acc[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
     }
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int col = 16 * n + (lane & 15);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int row = 16 * wave + (lane >> 4) + 4 * g;
-        const double w = acc[n][g], l = w * rd[n];
+        const int row = 16 * wave + MF::row(lane, g);
+        const T w = acc[n][g], l = w * rd[n];
         As[row * DS + col] = l;  // this wave's rows only
         if (row < rows && col < bj) {
-          double* wp = &Wp[(int64_t)(row0 + row) * ldw + 64 * j + col];
+          T* wp = &Wp[(int64_t)(row0 + row) * ldw + 64 * j + col];
           if (region) st_sc1(wp, w);
           else *wp = w;
           K[(int64_t)(row0 + row) * ld + j0 + col] = l;
@@ -277,7 +282,7 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
       for (int u = 0; u < 16; ++u) {
         const int kk = (tid >> 6) + 4 * u, cc = tid & 63;
         const int wr = cbase + kk;
-        Bs[kk * DS + cc] = (wr < ce && cc < bj) ? ld_sc1(&Wp[(int64_t)wr * ldw + 64 * j + cc]) : 0.0;
+        Bs[kk * DS + cc] = (wr < ce && cc < bj) ? ld_sc1(&Wp[(int64_t)wr * ldw + 64 * j + cc]) : T(0);
       }
       __syncthreads();
 #pragma unroll
@@ -285,25 +290,25 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
         const int cabs = cbase + 16 * n + (lane & 15);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int row = 16 * wave + (lane >> 4) + 4 * g;
+          const int row = 16 * wave + MF::row(lane, g);
           const bool in = row < rows && cabs < ce && cabs <= row0 + row;
-          const double* src = &K[(int64_t)(row0 + (in ? row : 0)) * ld + (in ? cabs : k0)];
-          acc[n][g] = in ? (j ? ld_sc1(src) : *src) : 0.0;
+          const T* src = &K[(int64_t)(row0 + (in ? row : 0)) * ld + (in ? cabs : k0)];
+          acc[n][g] = in ? (j ? ld_sc1(src) : *src) : T(0);
         }
       }
 #pragma unroll 4
       for (int s = 0; s < 16; ++s) {
         const int k = 4 * s + (lane >> 4);
-        const double a = -As[arow * DS + k];
+        const T a = -As[arow * DS + k];
 #pragma unroll
-        for (int n = 0; n < 4; ++n) acc[n] = mfma_f64_16x16x4(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
+        for (int n = 0; n < 4; ++n) acc[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
       }
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
         const int cabs = cbase + 16 * n + (lane & 15);
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
-          const int row = 16 * wave + (lane >> 4) + 4 * g;
+          const int row = 16 * wave + MF::row(lane, g);
           if (row < rows && cabs < ce && cabs <= row0 + row) K[(int64_t)(row0 + row) * ld + cabs] = acc[n][g];
         }
       }
@@ -316,8 +321,8 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
     __syncthreads();
     const int j0 = k0 + 64 * c;
     const int bj = ce - j0 < 64 ? ce - j0 : 64;
-    diag64_body<true, true>(K, ld, j0, bj, D, Lb0 + (int64_t)c * 64 * 64, info, smem, smem + 64 * DS,
-                            smem + 2 * 64 * DS, nullptr);
+    diag64_body<true, true, T>(K, ld, j0, bj, D, Lb0 + (int64_t)c * 64 * 64, info, smem, smem + 64 * DS,
+                               smem + 2 * 64 * DS, nullptr);
     publish(&ctrl[OP_DIAG + c]);
   }
   // ---- completion: the last workgroup out zeroes the ctrl words
@@ -331,13 +336,22 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(double* __restrict__ K
   }
 }
 
-hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
-                       int* info, unsigned* ctrl, hipStream_t st) {
+template <typename T>
+static hipError_t outer_panel_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw, int* info,
+                                unsigned* ctrl, hipStream_t st) {
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
   const int nch = (N - k0 + 63) / 64;
-  hipLaunchKernelGGL(outer_panel_kernel, dim3(nch), dim3(256), 0, st, K, ld, N, k0, k0 + bo, D, Lb0, Wp, ldw, info,
+  hipLaunchKernelGGL(outer_panel_kernel<T>, dim3(nch), dim3(256), 0, st, K, ld, N, k0, k0 + bo, D, Lb0, Wp, ldw, info,
                      ctrl);
   return hipGetLastError();
+}
+hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                       int* info, unsigned* ctrl, hipStream_t st) {
+  return outer_panel_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, ctrl, st);
+}
+hipError_t outer_panel(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
+                       int* info, unsigned* ctrl, hipStream_t st) {
+  return outer_panel_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, ctrl, st);
 }
 
 hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
