@@ -38,6 +38,9 @@ WORKLOADS = {
     "c5": dict(n=16384, m=0, p=0, mixed=True, sample_scale=8,
                desc="dense QP n=16384 box-only (SlackedSlacks), fp32 LDL^T of the scaled KKT + fp64 iterative "
                     "refinement to 1e-12"),
+    "c4": dict(n=256, m=64, p=0, batch=1024, sample_scale=1,
+               desc="batch of 1024 independent dense QPs n=256, m=64 ineq (KKT N=320), sharded across ranks; "
+                    "one launch per phase for a rank's whole shard"),
     "c5_f64": dict(n=16384, m=0, p=0, sample_scale=8,
                    desc="C5's QP (n=16384 box-only) with the plain fp64 factor, for comparison"),
 }
@@ -56,6 +59,21 @@ def cpu_baseline(wl):
 
     sample_scale = wl.get("sample_scale", 4)
     n, m, p = (wl[k] // sample_scale for k in ("n", "m", "p"))
+    if wl.get("batch"):  # C4: QP-steps/s of one core, from a bounded run of whole QPs
+        steps = 0
+        seed = 0
+        wall = 0.0
+        while wall < 10.0:
+            o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed))  # generation is not timed
+            t1 = time.perf_counter()
+            for _ in range(3):
+                o.iterate()
+                steps += 1
+            wall += time.perf_counter() - t1
+            seed += 1
+        return {"value": steps / wall, "unit": "QP-steps/s", "cores": 1, "kind": "port",
+                "sample": f"{steps} Newton steps of the oracle on {seed} QPs n={n}, m={m} (3 steps each) in "
+                          f"{wall:.1f} s, single thread; cpu={platform.processor() or platform.machine()}"}
     qp = oracle.gen_qp(n, m, p, 1234)
     o = oracle.OracleQP(qp)
     t0 = time.perf_counter()
@@ -109,8 +127,17 @@ def main():
     Nk = n + m + p
     stream = torch.cuda.current_stream()
     ctx = I.Context(local_rank, stream=stream.cuda_stream, nbo=args.nbo, nbi=args.nbi)
-    qp = I.Optimizer(n, m, p, ctx)
-    qp.generate(1234 + rank)
+    nbatch = wl.get("batch", 0)
+    if nbatch:  # C4: this rank's contiguous shard of the batch, one Batch object
+        from ipmz_amd.dist import shard
+        mine = shard(nbatch, world, rank)
+        B = len(mine)
+        qp = I.Batch(n, m, p, B, ctx)
+        qp.generate(mine.start)  # QP i has seed i, as in the single-GPU batch
+    else:
+        B = 1
+        qp = I.Optimizer(n, m, p, ctx)
+        qp.generate(1234 + rank)
     mixed = wl.get("mixed", False)
     if mixed:
         qp.set_mixed_precision(True, args.ir_tol, 20)
@@ -118,15 +145,19 @@ def main():
     flags = I.STEP_RESTART_IF_CONVERGED | (0 if timing else I.STEP_GRAPH)
     from ipmz_amd.dist import pack_summary, reduce_summary
 
-    sc = torch.zeros(I.SC_COUNT, dtype=torch.float64, device="cuda")
+    sc = torch.zeros(B, I.SC_COUNT, dtype=torch.float64, device="cuda")
 
     def one_step():
         qp.step(flags)
         if world > 1:
-            # RCCL all-reduce of the convergence scalars only,
+            # RCCL all-reduce of the convergence summary only,
             # enqueued on the solver's stream: no host round trip
-            qp.copy_scalars(sc.data_ptr())
-            reduce_summary(pack_summary(sc[I.SC["res"]], sc[I.SC["mu"]], sc[I.SC["converged"]], "cuda"))
+            if nbatch:
+                qp.copy_batch_scalars(sc.data_ptr())
+            else:
+                qp.copy_scalars(sc.data_ptr())
+            reduce_summary(pack_summary(sc[:, I.SC["res"]].max(), sc[:, I.SC["mu"]].max(),
+                                        sc[:, I.SC["converged"]].sum(), "cuda"))
 
     for _ in range(args.warmup):
         one_step()
@@ -152,27 +183,30 @@ def main():
     ph = qp.phase_times() if timing else None
 
     if rank == 0:
-        steps_total = args.steps * world
+        steps_total = args.steps * (nbatch if nbatch else world)
         value = steps_total / elapsed
         out = {
-            "metric": "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X",
+            "metric": ("QP Newton steps/sec, batch of 1024 dense QPs n=256, 1/2/4/8 MI355X" if nbatch else
+                       "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X"),
             "value": value,
-            "unit": "steps/s",
+            "unit": "QP-steps/s" if nbatch else "steps/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": 1e3 * elapsed / args.steps,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if nbatch else "weak",
             "vs_baseline": None,
             "dtype": "f32 factor + f64 refinement" if mixed else "f64",
             "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; seed 1234+rank)",
             "config": {"workload": args.workload, "n": n, "m": m, "p": p, "kkt_N": Nk,
                        "formulation": ("SlackedSlacks box-only, fp32 LDL^T of S K S + fp64 iterative refinement "
                                        f"(tol {args.ir_tol:g})") if mixed else
-                                      "SlackedSlacks ineq + Regularization eq (delta=1e-4), augmented LDL^T",
-                       "parallelism": f"replicas x{world} (independent QPs, RCCL all-reduce of convergence "
-                                      f"scalars only)",
+                                      ("SlackedSlacks" + (" ineq" if m else " box-only") +
+                                       (" + Regularization eq (delta=1e-4)" if p else "") + ", augmented LDL^T"),
+                       "parallelism": (f"batch sharded over {world} rank(s), {B} QPs on rank 0" if nbatch else
+                                       f"replicas x{world} (independent QPs)") +
+                                      ", RCCL all-reduce of the convergence summary only",
                        "blocking": {"nbo": args.nbo, "nbi": args.nbi},
                        "description": wl["desc"]},
             "restarts": s["restarts"],
@@ -186,12 +220,20 @@ def main():
         if ph:
             k = args.steps
             factor_ms = ph["factor"] / k
-            out["factor_tflops"] = (Nk ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
+            out["factor_tflops"] = B * (Nk ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
             out["phase_ms_per_step"] = {kk: ph[kk] / k for kk in ("step", "assemble", "factor", "solve", "eval")}
             tr_s = ph["trailing"] * 1e-3
             launches = ph["trailing_launches"]
             achieved = ph["trailing_flops"] / tr_s / 1e12 if tr_s > 0 else 0.0
             peak = FP32_MFMA_PEAK_TFLOPS if mixed else FP64_MFMA_PEAK_TFLOPS
+        if ph and nbatch:
+            # batched factor: every launch serves the whole shard; the bound at
+            # N = 320 is latency, priced here against the fp64 MFMA peak
+            out["roofline"] = {"bound": "mfma", "kernel": "batched blocked LDL^T (whole factor phase)",
+                               "achieved": out["factor_tflops"], "peak": peak, "unit": "TFLOP/s",
+                               "frac": out["factor_tflops"] / peak, "traffic": None,
+                               "note": "factor flops B*N^3/3 over the factor phase time (HIP events)"}
+        elif ph:
             out["roofline"] = {
                 "bound": "mfma",
                 "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB> (trailing update "

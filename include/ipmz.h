@@ -205,6 +205,9 @@ int ipmz_batch_initialize(ipmz_qp* qp);
 int ipmz_batch_scalars(ipmz_qp* qp, double* out);
 int ipmz_batch_get_state(ipmz_qp* qp, int index, int which, double* host_out);
 int ipmz_batch_set_state(ipmz_qp* qp, int index, const double* host_vars);
+/* Enqueue a device-to-device copy of all batch * IPMZ_SC_COUNT scalars
+ * (QP-major) to dst (device): the input of the cross-GPU convergence summary. */
+int ipmz_batch_copy_scalars(ipmz_qp* qp, double* dst_device);
 /* Step until every QP converged (converged QPs keep their iterate). */
 int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
 

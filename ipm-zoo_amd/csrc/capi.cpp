@@ -737,9 +737,9 @@ int step_impl(ipmz_qp* s, int flags) {
   return IPMZ_OK;
 }
 
-int scalars_impl(ipmz_qp* s, double* out) {
+int scalars_impl(ipmz_qp* s, double* out, int count) {
   HIP_OK(hipSetDevice(s->ctx->device));
-  for (int i = 0; i < s->B; ++i)
+  for (int i = 0; i < count; ++i)
     HIP_OK(hipMemcpyAsync(out + (int64_t)i * SC_COUNT, s->hq[i].scal, SC_COUNT * 8, hipMemcpyDeviceToHost,
                           s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
@@ -810,7 +810,7 @@ int ipmz_qp_step(ipmz_qp* s, int flags) { return step_impl(s, flags); }
 
 int ipmz_qp_scalars(ipmz_qp* s, double* out) {
   if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
-  return scalars_impl(s, out);
+  return scalars_impl(s, out, 1);  // QP 0 (the ipmz_qp_* accessors address QP 0)
 }
 
 int ipmz_qp_device_scalars(ipmz_qp* s, double** out) {
@@ -829,7 +829,7 @@ int ipmz_qp_copy_scalars(ipmz_qp* s, double* dst) {
 int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   double sc[SC_COUNT];
-  int rc = scalars_impl(s, sc);
+  int rc = scalars_impl(s, sc, 1);
   if (rc) return rc;
   int it = 0;
   for (; it < max_iter; ++it) {  // Optimizer.cpp:127-135
@@ -844,7 +844,7 @@ int ipmz_qp_solve(ipmz_qp* s, int max_iter, double* trace, int* iterations) {
     if (sc[SC_CONVERGED] != 0.0) break;
     rc = step_impl(s, 0);
     if (rc) return rc;
-    rc = scalars_impl(s, sc);
+    rc = scalars_impl(s, sc, 1);
     if (rc) return rc;
     if (row) {
       row[3] = sc[SC_ALPHA_AFF];
@@ -967,7 +967,7 @@ int ipmz_batch_initialize(ipmz_qp* s) {
 }
 int ipmz_batch_scalars(ipmz_qp* s, double* out) {
   if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");
-  return scalars_impl(s, out);
+  return scalars_impl(s, out, s->B);
 }
 int ipmz_batch_get_state(ipmz_qp* s, int index, int which, double* out) {
   int rc = check_index(s, index);
@@ -984,6 +984,14 @@ int ipmz_batch_set_state(ipmz_qp* s, int index, const double* in) {
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   return IPMZ_OK;
 }
+int ipmz_batch_copy_scalars(ipmz_qp* s, double* dst) {
+  if (!s || !dst) return fail(IPMZ_ERR_INVALID, "null argument");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  // the B scalar blocks are one allocation with a stride of SC_COUNT doubles
+  HIP_OK(hipMemcpy2DAsync(dst, SC_COUNT * 8, s->hq[0].scal, (s->B > 1 ? (s->hq[1].scal - s->hq[0].scal) : SC_COUNT) * 8,
+                          SC_COUNT * 8, s->B, hipMemcpyDeviceToDevice, s->ctx->stream));
+  return IPMZ_OK;
+}
 // Steps until every QP converged or max_iter; a converged QP keeps its
 // iterate.  converged_count: host, may be NULL.
 int ipmz_batch_solve(ipmz_qp* s, int max_iter, int* iterations, int* converged_count) {
@@ -991,7 +999,7 @@ int ipmz_batch_solve(ipmz_qp* s, int max_iter, int* iterations, int* converged_c
   std::vector<double> sc((size_t)s->B * SC_COUNT);
   int it = 0, nconv = 0;
   for (;; ++it) {
-    int rc = scalars_impl(s, sc.data());
+    int rc = scalars_impl(s, sc.data(), s->B);
     if (rc) return rc;
     nconv = 0;
     for (int i = 0; i < s->B; ++i) nconv += sc[(size_t)i * SC_COUNT + SC_CONVERGED] != 0.0;

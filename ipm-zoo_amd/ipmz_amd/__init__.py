@@ -43,6 +43,7 @@ EXPORTS = [
     "ipmz_batch_create", "ipmz_batch_size", "ipmz_batch_load_host", "ipmz_batch_initialize", "ipmz_batch_scalars",
     "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
+    "ipmz_batch_copy_scalars",
 ]
 
 _P = ctypes.POINTER(ctypes.c_double)
@@ -114,6 +115,7 @@ def _load():
         "ipmz_mixed_factor": ([_VP, _I, _VP, _I64, _VP, _I64], _I),
         "ipmz_mixed_solve": ([_VP, _I, _VP, _I64, _VP, _VP, ctypes.c_double, _I, _P], _I),
         "ipmz_qp_set_mixed_precision": ([_VP, _I, ctypes.c_double, _I], _I),
+        "ipmz_batch_copy_scalars": ([_VP, _VP], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -392,6 +394,10 @@ class Batch(Optimizer):
 
     def initialize(self):
         _check(lib.ipmz_batch_initialize(self.h), "ipmz_batch_initialize")
+
+    def copy_batch_scalars(self, dst_ptr):
+        """Async device copy of all batch x SC_COUNT scalars (ctx stream)."""
+        _check(lib.ipmz_batch_copy_scalars(self.h, _VP(dst_ptr)), "ipmz_batch_copy_scalars")
 
     def batch_scalars(self):
         out = np.zeros(self.batch * SC_COUNT)
