@@ -31,9 +31,11 @@ sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
 FP64_MFMA_PEAK_TFLOPS = 78.6  # MI355X dense fp64 matrix peak (BASELINE.md "Peaks")
 
 WORKLOADS = {
-    "c3": dict(n=8192, m=2048, p=1024, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
+    "c3": dict(n=8192, m=2048, p=1024, sample_scale=2, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
                                           "(Regularization), augmented LDL^T, KKT N=11264"),
-    "c2size": dict(n=2048, m=512, p=0, desc="dense QP n=2048, m=512 ineq, augmented LDL^T, KKT N=2560"),
+    "c2": dict(n=2048, m=512, p=0, normal=True, sample_scale=1,
+               desc="dense QP n=2048, m=512 ineq, normal equations: Cholesky(H) + TRSM + SYRK + Cholesky(S)"),
+    "c2_aug": dict(n=2048, m=512, p=0, sample_scale=1, desc="C2's QP (n=2048, m=512) with the augmented LDL^T, for comparison"),
     "small": dict(n=1024, m=256, p=128, desc="dense QP n=1024, m=256, p=128 (smoke size)"),
     "c5": dict(n=16384, m=0, p=0, mixed=True, sample_scale=8,
                desc="dense QP n=16384 box-only (SlackedSlacks), fp32 LDL^T of the scaled KKT + fp64 iterative "
@@ -141,6 +143,8 @@ def main():
     mixed = wl.get("mixed", False)
     if mixed:
         qp.set_mixed_precision(True, args.ir_tol, 20)
+    if wl.get("normal"):
+        qp.set_reduction(I.REDUCTION_NORMAL)
     timing = not args.no_timing
     flags = I.STEP_RESTART_IF_CONVERGED | (0 if timing else I.STEP_GRAPH)
     from ipmz_amd.dist import pack_summary, reduce_summary
@@ -203,7 +207,9 @@ def main():
                        "formulation": ("SlackedSlacks box-only, fp32 LDL^T of S K S + fp64 iterative refinement "
                                        f"(tol {args.ir_tol:g})") if mixed else
                                       ("SlackedSlacks" + (" ineq" if m else " box-only") +
-                                       (" + Regularization eq (delta=1e-4)" if p else "") + ", augmented LDL^T"),
+                                       (" + Regularization eq (delta=1e-4)" if p else "") +
+                                       (", normal equations (Cholesky H, S)" if wl.get("normal") else
+                                        ", augmented LDL^T")),
                        "parallelism": (f"batch sharded over {world} rank(s), {B} QPs on rank 0" if nbatch else
                                        f"replicas x{world} (independent QPs)") +
                                       ", RCCL all-reduce of the convergence summary only",

@@ -129,6 +129,21 @@ int ipmz_mixed_factor(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* w
 int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, double* b, double tol,
                      int max_refine, double* stat);
 
+/* ---- normal-equations reduction (config C2) ------------------------------
+ * The reference derives it symbolically (get_normal_equations,
+ * SymbolicOptimization.cpp:465-478; built at Optimizer.cpp:39-40) but never
+ * evaluates it.  For the augmented K = [[H, B^T], [B, -E]] (device, lower
+ * triangle, order n + mp, H SPD, E > 0 diagonal): Cholesky of H (as L D L^T,
+ * D > 0), Vt = B L^{-T}, S = E + B H^{-1} B^T, Cholesky of S.  The H block is
+ * overwritten by its factor, the (2,2) block by S's, B is left intact.  D:
+ * device, n + mp doubles (pivots of H, then of S).  Returns > 0 (1-based
+ * augmented index) when H or S has a non-positive pivot. */
+int64_t ipmz_normal_workspace_bytes(ipmz_ctx* ctx, int n, int mp);
+int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes);
+/* b = [r0; r1] (device) <- [x; l]:  l = S^{-1} (B H^{-1} r0 - r1),
+ * x = H^{-1} (r0 - B^T l). */
+int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D, void* ws, double* b);
+
 /* ---- LinearSolvers with the reference's host signatures ------------------ */
 /* A: host N x N row-major (lower triangle read).  L: host N x N, written
  * full (zeros above, ones on the diagonal); D: host N. */
@@ -187,6 +202,13 @@ int ipmz_qp_kkt_dim(ipmz_qp* qp);
  * per solve); enable = 0 returns to the fp64 factor.  Single QPs only.  The
  * scalar block then reports IPMZ_SC_IR_*. */
 int ipmz_qp_set_mixed_precision(ipmz_qp* qp, int enable, double tol, int max_refine);
+/* KKT reduction of the Newton step: augmented LDL^T (default, what the
+ * reference solves, Optimizer.cpp:137-138) or the normal equations (the
+ * reference's normal_equations_ reduction, Optimizer.cpp:39-40).  Single
+ * QPs; not combined with mixed precision. */
+#define IPMZ_REDUCTION_AUGMENTED 0
+#define IPMZ_REDUCTION_NORMAL 1
+int ipmz_qp_set_reduction(ipmz_qp* qp, int reduction);
 
 /* ---- batches of independent QPs (config C4) ------------------------------
  * A batch is an ipmz_qp holding `batch` QPs of identical (n, m, p); every

@@ -313,6 +313,112 @@ int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws
   return IPMZ_OK;
 }
 
+// Normal equations (config C2) ---------------------------------------------
+}  // extern "C"
+
+namespace {
+// [spd info (256 B)] [ws of the H factor] [ws of the S factor] [Vt mp x ldv]
+// [W mp x ldv] [u n] [part ceil(mp/64) x n]
+struct NormalWs {
+  int* info = nullptr;
+  char *wsH = nullptr, *wsS = nullptr;
+  double *Vt = nullptr, *W = nullptr, *u = nullptr, *part = nullptr;
+  int64_t ldv = 0, total = 0;
+};
+NormalWs normal_ws(char* base, int n, int mp, int nbo, int nbi) {
+  NormalWs w;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += round_up(bytes, 256);
+    return p;
+  };
+  w.ldv = round_up(n, 8);
+  w.info = reinterpret_cast<int*>(take(256));
+  w.wsH = take(ws_layout(n, nbo, nbi).total);
+  w.wsS = take(ws_layout(mp > 0 ? mp : 1, nbo, nbi).total);
+  w.Vt = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
+  w.W = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
+  w.u = reinterpret_cast<double*>(take((int64_t)n * 8));
+  w.part = reinterpret_cast<double*>(take((int64_t)((mp + 63) / 64) * n * 8));
+  w.total = off;
+  return w;
+}
+}  // namespace
+
+static int normal_factor_impl(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, const NormalWs& w,
+                              TrailTimer* timer) {
+  hipStream_t st = ctx->stream;
+  HIP_OK(hipMemsetAsync(w.info, 0x7f, sizeof(int), st));
+  // Cholesky of H as L D L^T (the blocked factor on the leading n x n block)
+  int rc = factor_impl(ctx, n, K, ld, D, w.wsH, timer);
+  if (rc) return rc;
+  HIP_OK(ne_check_pos(D, n, 0, w.info, st));
+  if (mp == 0) return IPMZ_OK;
+  // Vt = B L^{-T}, S = E + Vt D^{-1} Vt^T (into the (2,2) block), Cholesky of S
+  const WsLayout lh = ws_layout(n, ctx->nbo, ctx->nbi);
+  const double* LinvH = reinterpret_cast<const double*>(w.wsH + lh.linv_off);
+  HIP_OK(hipMemcpy2DAsync(w.Vt, w.ldv * 8, K + (int64_t)n * ld, ld * 8, (size_t)n * 8, mp, hipMemcpyDeviceToDevice,
+                          st));
+  HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, LinvH, ctx->nbi, st));
+  double* K22 = K + (int64_t)n * ld + n;
+  HIP_OK(ne_schur(K22, ld, mp, w.Vt, w.W, w.ldv, n, D, st));
+  if ((rc = factor_impl(ctx, mp, K22, ld, D + n, w.wsS, nullptr))) return rc;
+  HIP_OK(ne_check_pos(D + n, mp, n, w.info, st));
+  return IPMZ_OK;
+}
+
+static int normal_solve_impl(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D,
+                             const NormalWs& w, double* b) {
+  hipStream_t st = ctx->stream;
+  HIP_OK(hipMemcpyAsync(w.u, b, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+  HIP_OK(solve_ws(K, ld, n, D, w.wsH, ctx->nbo, ctx->nbi, w.u, st));  // u = H^{-1} r0
+  if (mp == 0) {
+    HIP_OK(hipMemcpyAsync(b, w.u, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
+    return IPMZ_OK;
+  }
+  const double* Bm = K + (int64_t)n * ld;
+  HIP_OK(ne_gemv(Bm, ld, mp, n, w.u, b + n, b + n, st));                                     // B u - r1
+  HIP_OK(solve_ws(K + (int64_t)n * ld + n, ld, mp, D + n, w.wsS, ctx->nbo, ctx->nbi, b + n, st));  // l
+  HIP_OK(ne_gemvt(Bm, ld, mp, n, b + n, w.part, b, st));                                    // r0 - B^T l
+  HIP_OK(solve_ws(K, ld, n, D, w.wsH, ctx->nbo, ctx->nbi, b, st));                           // x
+  return IPMZ_OK;
+}
+
+extern "C" {
+
+int64_t ipmz_normal_workspace_bytes(ipmz_ctx* ctx, int n, int mp) {
+  if (!ctx || n <= 0 || mp < 0) return 0;
+  return normal_ws(nullptr, n, mp, ctx->nbo, ctx->nbi).total;
+}
+
+int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes) {
+  if (!ctx || n <= 0 || mp < 0 || !K || !D || !ws || ld < n + mp || (ld & 1))
+    return fail(IPMZ_ERR_INVALID, "ipmz_normal_factor: bad arguments (n > 0, ld >= n + mp, ld even)");
+  const NormalWs w = normal_ws(static_cast<char*>(ws), n, mp, ctx->nbo, ctx->nbi);
+  if (ws_bytes < w.total) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  HIP_OK(hipSetDevice(ctx->device));
+  int rc = normal_factor_impl(ctx, n, mp, K, ld, D, w, nullptr);
+  if (rc) return rc;
+  int info = 0;
+  HIP_OK(hipMemcpyAsync(&info, w.info, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (info != 0x7f7f7f7f) return info;
+  // non-finite pivots of the two LDL^T factors (their own info words)
+  const int ih = read_info(ctx, w.wsH);
+  if (ih) return ih;
+  const int is = mp ? read_info(ctx, w.wsS) : 0;
+  return is > 0 ? n + is : is;
+}
+
+int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D, void* ws,
+                      double* b) {
+  if (!ctx || n <= 0 || mp < 0 || !K || !D || !ws || !b || ld < n + mp)
+    return fail(IPMZ_ERR_INVALID, "ipmz_normal_solve: bad arguments");
+  HIP_OK(hipSetDevice(ctx->device));
+  return normal_solve_impl(ctx, n, mp, K, ld, D, normal_ws(static_cast<char*>(ws), n, mp, ctx->nbo, ctx->nbi), b);
+}
+
 // Host adapters with the reference's signatures ------------------------------
 int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, double* D) {
   if (!ctx || N < 0 || (N > 0 && (!A || !L || !D))) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_decomposition: bad arguments");
@@ -415,6 +521,9 @@ struct ipmz_qp {
   int ir_max = 10;
   MixedWs mw;
   char* mws = nullptr;
+  // normal-equations reduction (C2)
+  bool normal = false;
+  char* nws = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
   int graph_flags = -1;
@@ -459,7 +568,10 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
 QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
 
 int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
-  if (s->mixed) {
+  if (s->normal) {
+    return normal_solve_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
+                             normal_ws(s->nws, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi), q0(s).b);
+  } else if (s->mixed) {
     HIP_OK(mixed_solve(s->K, s->ldk, s->mw, q0(s).b, s->ir_tol, s->ir_max, st));
     HIP_OK(hipMemcpyAsync(q0(s).scal + IPMZ_SC_IR_RATIO_AFF + 2 * which, s->mw.stat, 2 * sizeof(double),
                           hipMemcpyDeviceToDevice, st));
@@ -474,6 +586,9 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
 
 int factor_batch(ipmz_qp* s, TrailTimer* tt) {
   if (s->mixed) return mixed_factor_impl(s->ctx, s->K, s->ldk, s->mw, tt);
+  if (s->normal)
+    return normal_factor_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
+                              normal_ws(s->nws, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi), tt);
   if (s->B == 1) return factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, tt);
   BatchStrides bs;
   bs.B = s->B;
@@ -892,8 +1007,8 @@ int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
 
 int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refine) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
-  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0))
-    return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0");
+  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0 || s->normal))
+    return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0, augmented reduction");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (enable && !s->mws) {
     const int64_t bytes = mixed_ws_bytes(s->N, s->ctx->nbo);
@@ -907,6 +1022,30 @@ int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refi
   s->ir_tol = tol;
   s->ir_max = max_refine;
   if (s->gexec) {  // the captured step has the other solver baked in
+    hipGraphExecDestroy(s->gexec);
+    hipGraphDestroy(s->graph);
+    s->gexec = nullptr;
+    s->graph = nullptr;
+  }
+  return IPMZ_OK;
+}
+
+int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
+  if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
+  if (reduction != IPMZ_REDUCTION_AUGMENTED && reduction != IPMZ_REDUCTION_NORMAL)
+    return fail(IPMZ_ERR_INVALID, "unknown reduction");
+  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed))
+    return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  if (reduction == IPMZ_REDUCTION_NORMAL && !s->nws) {
+    const int64_t bytes = normal_ws(nullptr, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi).total;
+    void* w = nullptr;
+    if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+    s->allocs.push_back(w);
+    s->nws = static_cast<char*>(w);
+  }
+  s->normal = reduction == IPMZ_REDUCTION_NORMAL;
+  if (s->gexec) {
     hipGraphExecDestroy(s->gexec);
     hipGraphDestroy(s->graph);
     s->gexec = nullptr;

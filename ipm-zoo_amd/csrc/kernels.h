@@ -103,6 +103,20 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,
                        hipStream_t st);
 
+// normal.hip: normal-equations reduction (config C2) -------------------------
+hipError_t ne_check_pos(const double* D, int N, int offset, int* info, hipStream_t st);
+hipError_t ne_trsm_right(double* Vt, int64_t ldv, int rows, int n, const double* K, int64_t ld, const double* LinvH,
+                         int nb, hipStream_t st);
+hipError_t ne_schur(double* K22, int64_t ld, int mp, const double* Vt, double* W, int64_t ldv, int n,
+                    const double* DH, hipStream_t st);
+hipError_t ne_gemv(const double* Bm, int64_t ld, int rows, int cols, const double* u, const double* r1, double* t,
+                   hipStream_t st);
+hipError_t ne_gemvt(const double* Bm, int64_t ld, int rows, int cols, const double* l, double* part, double* r0,
+                    hipStream_t st);
+// C -= A B^T over the full rectangle (no triangle restriction)
+hipError_t gemm_nt_sub_rect(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
+                            double* C, int64_t ldc, hipStream_t st);
+
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
 

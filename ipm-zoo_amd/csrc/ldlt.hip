@@ -730,6 +730,22 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   return gemm_nt_sub_t<double>(M, N, Kd, A, lda, B, ldb, C, ldc, row0, col0, square_lower, st, bs);
 }
 
+hipError_t gemm_nt_sub_rect(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
+                            double* C, int64_t ldc, hipStream_t st) {
+  GemmArgs g{};
+  g.M = M;
+  g.N = N;
+  g.Kd = Kd;
+  g.A = A;
+  g.lda = lda;
+  g.B = B;
+  g.ldb = ldb;
+  g.C = C;
+  g.ldc = ldc;
+  g.lower = 0;
+  return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st);
+}
+
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                          double* C, int64_t ldc, hipStream_t st) {
   GemmArgs g{};

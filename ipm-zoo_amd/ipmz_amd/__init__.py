@@ -43,8 +43,10 @@ EXPORTS = [
     "ipmz_batch_create", "ipmz_batch_size", "ipmz_batch_load_host", "ipmz_batch_initialize", "ipmz_batch_scalars",
     "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
-    "ipmz_batch_copy_scalars",
+    "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
+    "ipmz_qp_set_reduction",
 ]
+REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
 _P = ctypes.POINTER(ctypes.c_double)
 _VP = ctypes.c_void_p
@@ -116,6 +118,10 @@ def _load():
         "ipmz_mixed_solve": ([_VP, _I, _VP, _I64, _VP, _VP, ctypes.c_double, _I, _P], _I),
         "ipmz_qp_set_mixed_precision": ([_VP, _I, ctypes.c_double, _I], _I),
         "ipmz_batch_copy_scalars": ([_VP, _VP], _I),
+        "ipmz_normal_workspace_bytes": ([_VP, _I, _I], _I64),
+        "ipmz_normal_factor": ([_VP, _I, _I, _VP, _I64, _VP, _VP, _I64], _I),
+        "ipmz_normal_solve": ([_VP, _I, _I, _VP, _I64, _VP, _VP, _VP], _I),
+        "ipmz_qp_set_reduction": ([_VP, _I], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -201,6 +207,18 @@ class Context:
         _check(lib.ipmz_mixed_solve(self.h, N, _VP(K_ptr), ld, _VP(ws_ptr), _VP(b_ptr), tol, max_refine, _dp(stat)),
                "ipmz_mixed_solve")
         return float(stat[0]), int(stat[1])
+
+    # -- normal equations (C2) --
+    def normal_workspace_bytes(self, n, mp):
+        return lib.ipmz_normal_workspace_bytes(self.h, n, mp)
+
+    def normal_factor(self, n, mp, K_ptr, ld, D_ptr, ws_ptr, ws_bytes):
+        return _check(lib.ipmz_normal_factor(self.h, n, mp, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), ws_bytes),
+                      "ipmz_normal_factor")
+
+    def normal_solve(self, n, mp, K_ptr, ld, D_ptr, ws_ptr, b_ptr):
+        return _check(lib.ipmz_normal_solve(self.h, n, mp, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), _VP(b_ptr)),
+                      "ipmz_normal_solve")
 
 
 _default_ctx = None
@@ -293,6 +311,10 @@ class Optimizer:
 
     def step(self, flags=0):
         _check(lib.ipmz_qp_step(self.h, flags), "ipmz_qp_step")
+
+    def set_reduction(self, reduction):
+        """REDUCTION_AUGMENTED (default) or REDUCTION_NORMAL (config C2)."""
+        _check(lib.ipmz_qp_set_reduction(self.h, reduction), "ipmz_qp_set_reduction")
 
     def set_mixed_precision(self, enable=True, tol=1e-12, max_refine=10):
         """Newton directions via the fp32 factor + fp64 refinement (config C5)."""
