@@ -19,8 +19,11 @@ step() {  # name timeout cmd...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -q --timeout=300 -p no:cacheprovider ;;
+    tests) step tests 900 python -m pytest tests -m gpu -v --timeout=300 --timeout-method thread -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    bench_c2) step bench_c2 300 python bench.py --workload c2 ;;
+    bench_c4) step bench_c4 300 python bench.py --workload c4 ;;
+    bench_c5) step bench_c5 300 python bench.py --workload c5 ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 5 --warmup 1 --no-cpu-baseline ;;
     # HBM traffic: one counter group per pass (MI355X_MICROARCH.md, rocprofv3 PMC slots)
     pmc_fetch) step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;

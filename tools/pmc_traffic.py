@@ -13,14 +13,14 @@ triangle): C read + written once, W and L panels read once:
 R per launch is recovered from the grid size (triangular grid of 128 x 128
 tiles, 512 threads per workgroup).
 
-    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write > profiles/<round>/pmc_traffic.json
+    python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write <profile label> > profiles/pmc_traffic.json
 """
 import csv
 import json
 import math
 import sys
 
-KERNEL = "gemm_nt_f64_kernel<128, 128, 0, 2, 4>"
+KERNEL = "gemm_nt_kernel<double, 128, 128, 0, 2, 4, 6>"
 NBO = 256
 
 
@@ -54,6 +54,7 @@ def main():
         "traffic_bytes_per_launch": per,
         "algorithmic_bytes_per_launch": tot_alg / n,
         "traffic_over_algorithmic": per / (tot_alg / n),
+        "profile": sys.argv[3] if len(sys.argv) > 3 else "",
         "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->B; one bench.py step, "
                 "separate --pmc passes; algorithmic = C lower triangle read+write + W, L panels",
     }
