@@ -22,6 +22,7 @@
 // Product terms are multiplied left to right, X^{-1} is an element-wise
 // reciprocal with 0 -> sqrt(DBL_MAX) (Evaluation.cpp:267-271).
 #include <chrono>
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -395,8 +396,159 @@ int iterate(QP& q, double* rec, double* phase_s) {
 }  // namespace
 
 // ===========================================================================
+// Bunch-Kaufman (LinearSolvers.cpp:76-207 factor, :209-318 solve), restated:
+// LAPACK dsytf2-'L' style diagonal pivoting with alpha = (1 + sqrt 17) / 8,
+// in place on a full row-major matrix (only the lower triangle is touched).
+// ipiv: >= 0 a 1x1 pivot with that interchange, < 0 (-kp, twice) a 2x2.
+// fix_kp = false reproduces the reference exactly, including its defect of
+// leaving kp = 0 for a second all-zero column (LinearSolvers.cpp:111-116);
+// fix_kp = true records kp = k there (what LAPACK does).
+namespace {
+struct ArgMax {
+  int64_t idx;
+  double val;
+};
+// largest |.| over i in [b, e) of column c (col) or row r (!col); ties keep
+// the first index (strictly-greater scan from b)
+ArgMax absmax(const double* A, int64_t ld, int64_t b, int64_t e, int64_t fixed, bool col) {
+  ArgMax m{0, 0.0};
+  for (int64_t i = b; i < e; ++i) {
+    const double v = std::fabs(col ? A[i * ld + fixed] : A[fixed * ld + i]);
+    if (v > m.val) m = {i, v};
+  }
+  return m;
+}
+}  // namespace
+
+static int bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, bool fix_kp) {
+  const double alpha = (1.0 + std::sqrt(17.0)) / 8.0;
+  auto a = [&](int64_t i, int64_t j) -> double& { return A[i * ld + j]; };
+  int info = 0;
+  for (int64_t k = 0; k < n;) {
+    int step = 1;
+    int64_t kp = 0;
+    const double akk = std::fabs(a(k, k));
+    const ArgMax cm = absmax(A, ld, k + 1, n, k, true);
+    if (akk == 0.0 && cm.val == 0.0) {
+      if (info == 0) {
+        info = (int)k;
+        kp = k;
+      } else if (fix_kp) {
+        kp = k;
+      }
+    } else {
+      if (akk >= alpha * cm.val) {
+        kp = k;
+      } else {
+        const double rmax = std::max(absmax(A, ld, k, cm.idx, cm.idx, false).val,
+                                     absmax(A, ld, cm.idx + 1, n, cm.idx, true).val);
+        if (akk * rmax >= alpha * cm.val * cm.val) kp = k;
+        else if (std::fabs(a(cm.idx, cm.idx)) >= alpha * rmax) kp = cm.idx;
+        else {
+          kp = cm.idx;
+          step = 2;
+        }
+      }
+      const int64_t kk = k + step - 1;
+      if (kp != kk) {  // symmetric interchange of kk and kp in A(k:n, k:n), lower part
+        for (int64_t i = kp + 1; i < n; ++i) std::swap(a(i, kp), a(i, kk));
+        for (int64_t j = kk + 1; j < kp; ++j) std::swap(a(kp, j), a(j, kk));
+        std::swap(a(kp, kp), a(kk, kk));
+        if (step == 2) std::swap(a(kk, k), a(kp, k));
+      }
+      if (step == 1) {  // rank-1: A -= W (1/d) W^T, column k -> L(k)
+        const double r = 1.0 / a(k, k);
+        for (int64_t j = k + 1; j < n; ++j) {
+          const double f = r * a(j, k);
+          for (int64_t i = j; i < n; ++i) a(i, j) -= f * a(i, k);
+          a(j, k) *= r;
+        }
+      } else if (k < n - 1) {  // rank-2 with the inverse of the 2x2 block
+        double d21 = a(k + 1, k);
+        const double d11 = a(k + 1, k + 1) / d21;
+        const double d22 = a(k, k) / d21;
+        const double t = 1.0 / (d11 * d22 - 1.0);
+        d21 = t / d21;
+        for (int64_t j = k + 2; j < n; ++j) {
+          const double wk = d21 * (d11 * a(j, k) - a(j, k + 1));
+          const double wk1 = d21 * (d22 * a(j, k + 1) - a(j, k));
+          for (int64_t i = j; i < n; ++i) a(i, j) -= (a(i, k) * wk + a(i, k + 1) * wk1);
+          a(j, k) = wk;
+          a(j, k + 1) = wk1;
+        }
+      }
+    }
+    if (step == 1) ipiv[k] = kp;
+    else ipiv[k] = ipiv[k + 1] = -kp;
+    k += step;
+  }
+  return info;
+}
+
+static void bk_solve(int64_t n, const double* L, int64_t ld, const int64_t* ipiv, double* b) {
+  if (n == 0) return;
+  auto l = [&](int64_t i, int64_t j) { return L[i * ld + j]; };
+  auto axpy_col = [&](int64_t from, int64_t j) {  // b[from:] -= L[from:, j] b[j]
+    const double mlt = -b[j];
+    for (int64_t i = from; i < n; ++i) b[i] += l(i, j) * mlt;
+  };
+  for (int64_t k = 0; k < n;) {  // L D y = P b
+    if (ipiv[k] >= 0) {
+      const int64_t kp = ipiv[k];
+      if (kp != k) std::swap(b[k], b[kp]);
+      axpy_col(k + 1, k);
+      b[k] /= l(k, k);
+      k += 1;
+    } else {
+      const int64_t kp = -ipiv[k];
+      if (kp != k + 1) std::swap(b[k + 1], b[kp]);
+      if (k < n - 1) {
+        axpy_col(k + 2, k);
+        axpy_col(k + 2, k + 1);
+      }
+      const double d21 = l(k + 1, k);
+      const double d11 = l(k, k) / d21;
+      const double d22 = l(k + 1, k + 1) / d21;
+      const double den = d11 * d22 - 1.0;
+      const double b1 = b[k] / d21, b2 = b[k + 1] / d21;
+      b[k] = (d22 * b1 - b2) / den;
+      b[k + 1] = (d11 * b2 - b1) / den;
+      k += 2;
+    }
+  }
+  auto dot_col = [&](int64_t from, int64_t j) {  // b[j] -= L[from:, j] . b[from:]
+    double s = 0.0;
+    for (int64_t i = from; i < n; ++i) s += l(i, j) * b[i];
+    b[j] -= s;
+  };
+  for (int64_t k = n - 1; k >= 0;) {  // L^T x = y, then undo the interchanges
+    if (ipiv[k] >= 0) {
+      if (k < n - 1) dot_col(k + 1, k);
+      const int64_t kp = ipiv[k];
+      if (kp != k) std::swap(b[k], b[kp]);
+      k -= 1;
+    } else {
+      if (k < n - 1) {
+        dot_col(k + 1, k);
+        dot_col(k + 1, k - 1);
+      }
+      const int64_t kp = -ipiv[k];
+      if (kp != k) std::swap(b[k], b[kp]);
+      k -= 2;
+    }
+  }
+}
+
+// ===========================================================================
 // C ABI for ctypes (tests, smoke, bench cpu_baseline)
 extern "C" {
+
+int ipmzo_bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, int fix_kp) {
+  return bk_factor(n, A, ld, ipiv, fix_kp != 0);
+}
+void ipmzo_bk_solve(int64_t n, const double* F, int64_t ld, const int64_t* ipiv, double* b) {
+  bk_solve(n, F, ld, ipiv, b);
+}
 
 void ipmzo_gen_qp(int64_t n, int64_t m, int64_t p, uint64_t seed, double* Q, double* c, double* A, double* lA,
                   double* uA, double* C, double* d, double* lx, double* ux) {

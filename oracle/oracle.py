@@ -62,6 +62,9 @@ def _load():
     lib.ipmzo_gen_qp.argtypes = [_i64, _i64, _i64, _u64] + [_P] * 9
     lib.ipmzo_ldlt.argtypes = [_i64, _P, _i64, _P, _i64, _P]
     lib.ipmzo_solve_ldlt.argtypes = [_i64, _P, _i64, _P, _P]
+    lib.ipmzo_bk_factor.argtypes = [_i64, _P, _i64, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
+    lib.ipmzo_bk_factor.restype = ctypes.c_int
+    lib.ipmzo_bk_solve.argtypes = [_i64, _P, _i64, ctypes.POINTER(ctypes.c_int64), _P]
     lib.ipmzo_u01.restype = ctypes.c_double
     lib.ipmzo_u01.argtypes = [_u64, _u64, _u64, _u64]
     return lib
@@ -108,6 +111,27 @@ def solve_ldlt(L, D, b):
     L = np.ascontiguousarray(L, dtype=np.float64)
     x = np.array(b, dtype=np.float64, copy=True)
     lib().ipmzo_solve_ldlt(len(x), _dp(L), L.shape[1], _dp(np.ascontiguousarray(D, dtype=np.float64)), _dp(x))
+    return x
+
+
+def bk_factor(K, fix_kp=False):
+    """Restatement of LinearSolvers::symmetric_indefinite_factorization
+    (LinearSolvers.cpp:76-207): returns (F, ipiv, info); fix_kp=True records
+    kp = k for a second zero column instead of the reference's kp = 0."""
+    F = np.array(K, dtype=np.float64, copy=True, order="C")
+    N = F.shape[0]
+    ipiv = np.zeros(N, dtype=np.int64)
+    info = lib().ipmzo_bk_factor(N, _dp(F), N, ipiv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), int(fix_kp))
+    return F, ipiv, info
+
+
+def bk_solve(F, ipiv, b):
+    """Restatement of LinearSolvers::overwriting_solve_bunch_kaufman
+    (LinearSolvers.cpp:209-318): returns x."""
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    ipiv = np.ascontiguousarray(ipiv, dtype=np.int64)
+    x = np.array(b, dtype=np.float64, copy=True)
+    lib().ipmzo_bk_solve(len(x), _dp(F), F.shape[1], ipiv.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), _dp(x))
     return x
 
 

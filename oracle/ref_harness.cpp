@@ -14,6 +14,9 @@
 //   bk <dir> <N> <seed> <tag>       symmetric_indefinite_factorization +
 //                                   overwriting_solve_bunch_kaufman
 //                                   (LinearSolvers.cpp:76-318)
+//   bk_rand <dir> <N> <seed> <zeros> <tag>
+//                                   the same pair on a dense indefinite K that
+//                                   forces interchanges and 2 x 2 pivots
 //   newton <dir> <n> <m> <seed> <iters> <tag>
 //                                   SlackedSlacks (box [+ ineq]) Newton
 //                                   iterations through the reference's own
@@ -243,6 +246,39 @@ static int mode_bk(const std::string& dir, size_t N, uint64_t seed, const std::s
   return 0;
 }
 
+// Dense symmetric indefinite K with a small diagonal, so the reference's
+// Bunch-Kaufman takes row/column interchanges and 2 x 2 pivots; `zeros`
+// rows/columns (indices N/2, N/2 + 1, ...) are set to zero, which exercises
+// the zero-column branch (and, for a second zero column, the kp = 0 defect,
+// LinearSolvers.cpp:111-116).
+static int mode_bk_rand(const std::string& dir, size_t N, uint64_t seed, size_t zeros, const std::string& tag) {
+  Mat K(N, Vec(N, 0.0));
+  for (size_t i = 0; i < N; ++i) {
+    for (size_t j = 0; j < i; ++j) {
+      const double v = 2.0 * u01(seed, TAG_K, i, j) - 1.0;
+      K[i][j] = v;
+      K[j][i] = v;
+    }
+    K[i][i] = 0.05 * (2.0 * u01(seed, TAG_K, i, i) - 1.0);
+  }
+  for (size_t z = 0; z < zeros; ++z) {
+    const size_t r = N / 2 + z;
+    for (size_t j = 0; j < N; ++j) K[r][j] = K[j][r] = 0.0;
+  }
+  Vec b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = 2.0 * u01(seed, TAG_B, i, 0) - 1.0;
+  auto [F, ipiv] = NO::LinearSolvers::symmetric_indefinite_factorization(K);
+  Vec x = b;
+  NO::LinearSolvers::overwriting_solve_bunch_kaufman(F, ipiv, x);
+  Vec piv(ipiv.begin(), ipiv.end());
+  write_bin(dir + "/" + tag + "_K.bin", flatten(K));
+  write_bin(dir + "/" + tag + "_F.bin", flatten(F));
+  write_bin(dir + "/" + tag + "_ipiv.bin", piv);
+  write_bin(dir + "/" + tag + "_b.bin", b);
+  write_bin(dir + "/" + tag + "_x.bin", x);
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // One reference Newton iteration, restated around the reference's own private
 // methods (Optimizer.cpp:127-219), recording KKT, directions and scalars.
@@ -429,6 +465,8 @@ int main(int argc, char** argv) {
     if (mode == "formulation") return mode_formulation(dir);
     if (mode == "ldlt" && argc == 6) return mode_ldlt(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk" && argc == 6) return mode_bk(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
+    if (mode == "bk_rand" && argc == 7)
+      return mode_bk_rand(dir, std::stoul(argv[3]), std::stoull(argv[4]), std::stoul(argv[5]), argv[6]);
     if (mode == "newton" && argc == 8)
       return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
                          argv[7]);

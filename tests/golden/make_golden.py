@@ -31,6 +31,12 @@ CASES = [
     ("ldlt", 320, 13, "ldlt320"),
     ("bk", 8, 21, "bk8"),
     ("bk", 64, 22, "bk64"),
+    # dense indefinite, small diagonal: interchanges + 2x2 pivots; bkz16 has two
+    # zero columns (zero-column branch + the kp = 0 defect)
+    ("bk_rand", 8, 31, 0, "bkr8"),
+    ("bk_rand", 64, 32, 0, "bkr64"),
+    ("bk_rand", 200, 33, 0, "bkr200"),
+    ("bk_rand", 16, 34, 2, "bkz16"),
     # C1: box-only SlackedSlacks, n=64, seed 1234, full solve trace
     ("newton", 64, 0, 1234, 100, "c1"),
     # C4-size QP: n=256, m=64 (N=320), seed 0, iterates 0-3
