@@ -144,6 +144,23 @@ int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, doub
  * x = H^{-1} (r0 - B^T l). */
 int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D, void* ws, double* b);
 
+/* ---- Bunch-Kaufman (symmetric indefinite) ---------
+ * LinearSolvers::symmetric_indefinite_factorization (LinearSolvers.h:23-26,
+ * LinearSolvers.cpp:76-207) and overwriting_solve_bunch_kaufman
+ * (LinearSolvers.h:28-31, :209-318); never called by the reference's
+ * Optimizer (solve_indefinite_ is ASSERT(false), Optimizer.cpp:75).
+ * Device: A row-major (lower triangle factored in place), N <= 4096; ipiv:
+ * device int[N] in the reference's convention (>= 0: 1x1 pivot with that
+ * interchange; < 0: -kp on both rows of a 2x2 pivot).  fix_kp = 0 keeps the
+ * reference's kp = 0 for a second all-zero column (LinearSolvers.cpp:111-116),
+ * 1 records kp = k.  Returns 0, or 1 + the first all-zero column. */
+int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp);
+int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* ipiv, double* b);
+/* Host signatures of the reference (value semantics, reference pivoting
+ * including its kp = 0 defect): F = A with the lower triangle factored. */
+int ipmz_symmetric_indefinite_factorization(ipmz_ctx* ctx, int N, const double* A, double* F, int* ipiv);
+int ipmz_overwriting_solve_bunch_kaufman(ipmz_ctx* ctx, int N, const double* F, const int* ipiv, double* b);
+
 /* ---- LinearSolvers with the reference's host signatures ------------------ */
 /* A: host N x N row-major (lower triangle read).  L: host N x N, written
  * full (zeros above, ones on the diagonal); D: host N. */

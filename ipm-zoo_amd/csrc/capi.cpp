@@ -419,6 +419,79 @@ int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld,
   return normal_solve_impl(ctx, n, mp, K, ld, D, normal_ws(static_cast<char*>(ws), n, mp, ctx->nbo, ctx->nbi), b);
 }
 
+// Bunch-Kaufman (f3) ----------------------------------------------------------
+int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp) {
+  if (!ctx || N < 0 || ld < N || (N > 0 && (!A || !ipiv))) return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: bad arguments");
+  if (N > IPMZ_BK_NMAX) return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: N > 4096 (one-workgroup factor)");
+  if (N == 0) return IPMZ_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  int* dinfo = nullptr;
+  HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dinfo), sizeof(int), ctx->stream));
+  int rc = IPMZ_OK, info = 0;
+  if (bk_factor(A, ld, N, ipiv, dinfo, fix_kp, 1, 0, 0, ctx->stream) != hipSuccess ||
+      hipMemcpyAsync(&info, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      hipStreamSynchronize(ctx->stream) != hipSuccess)
+    rc = fail(IPMZ_ERR_HIP, "ipmz_bk_factor: launch failed");
+  hipFreeAsync(dinfo, ctx->stream);
+  return rc ? rc : info;
+}
+
+int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* ipiv, double* b) {
+  if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_bk_solve: bad arguments");
+  if (N == 0) return IPMZ_OK;  // LinearSolvers.cpp:212-214
+  if (!F || !ipiv || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
+  HIP_OK(hipSetDevice(ctx->device));
+  HIP_OK(bk_solve(F, ld, N, ipiv, b, 1, 0, 0, 0, ctx->stream));
+  return IPMZ_OK;
+}
+
+int ipmz_symmetric_indefinite_factorization(ipmz_ctx* ctx, int N, const double* A, double* F, int* ipiv) {
+  if (!ctx || N < 0 || (N > 0 && (!A || !F || !ipiv)))
+    return fail(IPMZ_ERR_INVALID, "ipmz_symmetric_indefinite_factorization: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  HIP_OK(hipSetDevice(ctx->device));
+  double* dA = nullptr;
+  int* dp = nullptr;
+  if (hipMalloc(&dA, (size_t)N * N * 8) != hipSuccess || hipMalloc(&dp, (size_t)N * 4) != hipSuccess) {
+    hipFree(dA);
+    return fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  }
+  int rc = IPMZ_OK;
+  if (hipMemcpyAsync(dA, A, (size_t)N * N * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    rc = fail(IPMZ_ERR_HIP, "copy-in failed");
+  if (!rc) rc = ipmz_bk_factor(ctx, N, dA, N, dp, 0);
+  if (rc >= 0 && (hipMemcpy(F, dA, (size_t)N * N * 8, hipMemcpyDeviceToHost) != hipSuccess ||
+                  hipMemcpy(ipiv, dp, (size_t)N * 4, hipMemcpyDeviceToHost) != hipSuccess))
+    rc = fail(IPMZ_ERR_HIP, "copy-out failed");
+  hipFree(dA);
+  hipFree(dp);
+  return rc < 0 ? rc : IPMZ_OK;  // the reference reports no info
+}
+
+int ipmz_overwriting_solve_bunch_kaufman(ipmz_ctx* ctx, int N, const double* F, const int* ipiv, double* b) {
+  if (!ctx || N < 0) return fail(IPMZ_ERR_INVALID, "ipmz_overwriting_solve_bunch_kaufman: bad arguments");
+  if (N == 0) return IPMZ_OK;
+  if (!F || !ipiv || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
+  HIP_OK(hipSetDevice(ctx->device));
+  double *dF = nullptr, *db = nullptr;
+  int* dp = nullptr;
+  bool ok = hipMalloc(&dF, (size_t)N * N * 8) == hipSuccess && hipMalloc(&db, (size_t)N * 8) == hipSuccess &&
+            hipMalloc(&dp, (size_t)N * 4) == hipSuccess;
+  int rc = ok ? IPMZ_OK : fail(IPMZ_ERR_NOMEM, "device allocation failed");
+  if (!rc && (hipMemcpyAsync(dF, F, (size_t)N * N * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+              hipMemcpyAsync(db, b, (size_t)N * 8, hipMemcpyHostToDevice, ctx->stream) != hipSuccess ||
+              hipMemcpyAsync(dp, ipiv, (size_t)N * 4, hipMemcpyHostToDevice, ctx->stream) != hipSuccess))
+    rc = fail(IPMZ_ERR_HIP, "copy-in failed");
+  if (!rc) rc = ipmz_bk_solve(ctx, N, dF, N, dp, db);
+  if (!rc && (hipMemcpyAsync(b, db, (size_t)N * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+              hipStreamSynchronize(ctx->stream) != hipSuccess))
+    rc = fail(IPMZ_ERR_HIP, "copy-out failed");
+  hipFree(dF);
+  hipFree(db);
+  hipFree(dp);
+  return rc;
+}
+
 // Host adapters with the reference's signatures ------------------------------
 int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, double* D) {
   if (!ctx || N < 0 || (N > 0 && (!A || !L || !D))) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_decomposition: bad arguments");

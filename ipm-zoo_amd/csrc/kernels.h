@@ -117,6 +117,13 @@ hipError_t ne_gemvt(const double* Bm, int64_t ld, int rows, int cols, const doub
 hipError_t gemm_nt_sub_rect(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                             double* C, int64_t ldc, hipStream_t st);
 
+// bk.hip: Bunch-Kaufman factor / solve (one workgroup per matrix) -----------
+#define IPMZ_BK_NMAX 4096
+hipError_t bk_factor(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, int batch, int64_t sA,
+                     int64_t sP, hipStream_t st);
+hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double* b, int batch, int64_t sA, int64_t sP,
+                    int64_t sb, hipStream_t st);
+
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
 

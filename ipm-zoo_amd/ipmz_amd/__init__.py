@@ -44,7 +44,8 @@ EXPORTS = [
     "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
-    "ipmz_qp_set_reduction",
+    "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
+    "ipmz_overwriting_solve_bunch_kaufman",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
@@ -122,6 +123,10 @@ def _load():
         "ipmz_normal_factor": ([_VP, _I, _I, _VP, _I64, _VP, _VP, _I64], _I),
         "ipmz_normal_solve": ([_VP, _I, _I, _VP, _I64, _VP, _VP, _VP], _I),
         "ipmz_qp_set_reduction": ([_VP, _I], _I),
+        "ipmz_bk_factor": ([_VP, _I, _VP, _I64, _VP, _I], _I),
+        "ipmz_bk_solve": ([_VP, _I, _VP, _I64, _VP, _VP], _I),
+        "ipmz_symmetric_indefinite_factorization": ([_VP, _I, _P, _P, ctypes.POINTER(ctypes.c_int)], _I),
+        "ipmz_overwriting_solve_bunch_kaufman": ([_VP, _I, _P, ctypes.POINTER(ctypes.c_int), _P], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -208,6 +213,13 @@ class Context:
                "ipmz_mixed_solve")
         return float(stat[0]), int(stat[1])
 
+    # -- Bunch-Kaufman on device memory (f3) --
+    def bk_factor(self, N, A_ptr, ld, ipiv_ptr, fix_kp=False):
+        return _check(lib.ipmz_bk_factor(self.h, N, _VP(A_ptr), ld, _VP(ipiv_ptr), int(fix_kp)), "ipmz_bk_factor")
+
+    def bk_solve(self, N, F_ptr, ld, ipiv_ptr, b_ptr):
+        return _check(lib.ipmz_bk_solve(self.h, N, _VP(F_ptr), ld, _VP(ipiv_ptr), _VP(b_ptr)), "ipmz_bk_solve")
+
     # -- normal equations (C2) --
     def normal_workspace_bytes(self, n, mp):
         return lib.ipmz_normal_workspace_bytes(self.h, n, mp)
@@ -259,6 +271,38 @@ class LinearSolvers:
         _check(lib.ipmz_overwriting_solve_ldlt((ctx or default_context()).h, N, _dp(L), _dp(D), _dp(b)),
                "ipmz_overwriting_solve_ldlt")
         return b
+
+
+def _ip(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def symmetric_indefinite_factorization(A, ctx=None):
+    """LinearSolvers::symmetric_indefinite_factorization (LinearSolvers.h:23-26):
+    returns (F, ipiv) -- F is A with its lower triangle factored."""
+    A = np.ascontiguousarray(A, dtype=np.float64)
+    if A.ndim != 2 or A.shape[0] != A.shape[1]:
+        raise IpmzError("symmetric_indefinite_factorization: matrix must be square")
+    N = A.shape[0]
+    F = np.zeros((N, N))
+    ipiv = np.zeros(N, dtype=np.int32)
+    _check(lib.ipmz_symmetric_indefinite_factorization((ctx or default_context()).h, N, _dp(A), _dp(F), _ip(ipiv)),
+           "ipmz_symmetric_indefinite_factorization")
+    return F, ipiv
+
+
+def overwriting_solve_bunch_kaufman(F, ipiv, b, ctx=None):
+    """LinearSolvers::overwriting_solve_bunch_kaufman (LinearSolvers.h:28-31): b overwritten."""
+    F = np.ascontiguousarray(F, dtype=np.float64)
+    ipiv = np.ascontiguousarray(ipiv, dtype=np.int32)
+    if b.dtype != np.float64 or not b.flags.c_contiguous:
+        raise IpmzError("overwriting_solve_bunch_kaufman: b must be a contiguous float64 array")
+    _check(lib.ipmz_overwriting_solve_bunch_kaufman((ctx or default_context()).h, len(b), _dp(F), _ip(ipiv), _dp(b)),
+           "ipmz_overwriting_solve_bunch_kaufman")
+
+
+LinearSolvers.symmetric_indefinite_factorization = staticmethod(symmetric_indefinite_factorization)
+LinearSolvers.overwriting_solve_bunch_kaufman = staticmethod(overwriting_solve_bunch_kaufman)
 
 
 class Data:

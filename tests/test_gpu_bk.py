@@ -1,0 +1,77 @@
+"""Bunch-Kaufman (LinearSolvers.cpp:76-318) on the GPU
+against the reference's golden vectors and the CPU oracle.
+
+The factor updates every element with the reference's own expression and
+operand order, so F and ipiv are compared BITWISE -- including the fixtures
+that force interchanges and 2x2 pivots (bkr*) and the one with two zero
+columns that trips the reference's kp = 0 defect (bkz16).  The solve's
+backward dot products are tree reductions: x within 1e-13 relative.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import load
+
+pytestmark = pytest.mark.gpu
+I = pytest.importorskip("ipmz_amd")
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return I.Context(0)
+
+
+@pytest.mark.parametrize("N,tag", [(8, "bk8"), (64, "bk64"), (8, "bkr8"), (64, "bkr64"), (200, "bkr200"),
+                                   (16, "bkz16")])
+def test_bk_golden(ctx, N, tag):
+    K = load(f"{tag}_K.bin").reshape(N, N)
+    F, ipiv = I.LinearSolvers.symmetric_indefinite_factorization(K, ctx)
+    assert np.array_equal(F, load(f"{tag}_F.bin").reshape(N, N))
+    assert np.array_equal(ipiv, load(f"{tag}_ipiv.bin").astype(np.int32))
+    x = load(f"{tag}_b.bin").copy()
+    I.LinearSolvers.overwriting_solve_bunch_kaufman(F, ipiv, x, ctx)
+    ref = load(f"{tag}_x.bin")
+    if np.isfinite(ref).all():
+        assert np.abs(x - ref).max() <= 1e-13 * max(1.0, np.abs(ref).max())
+    else:  # the reference's defect divides by zero: the same entries are non-finite
+        assert np.array_equal(np.isfinite(x), np.isfinite(ref))
+
+
+def _indef(N, seed, zeros=0):
+    rng = np.random.default_rng(seed)
+    K = rng.uniform(-1, 1, (N, N))
+    K = np.tril(K) + np.tril(K, -1).T
+    K[np.arange(N), np.arange(N)] *= 0.05
+    for z in range(zeros):
+        K[N // 2 + z, :] = 0
+        K[:, N // 2 + z] = 0
+    return K
+
+
+@pytest.mark.parametrize("N", [1, 2, 3, 100, 513, 1500])
+def test_bk_vs_oracle_bitwise(ctx, N):
+    K = _indef(N, N)
+    F, ipiv = I.LinearSolvers.symmetric_indefinite_factorization(K, ctx)
+    Fo, po, _ = oracle.bk_factor(K)
+    assert np.array_equal(ipiv, po.astype(np.int32))
+    assert np.array_equal(F, Fo)
+    b = np.random.default_rng(1).uniform(-1, 1, N)
+    x = b.copy()
+    I.LinearSolvers.overwriting_solve_bunch_kaufman(F, ipiv, x, ctx)
+    # an indefinite system solved: residual check in fp64
+    assert np.abs(K @ x - b).max() < 1e-10 * max(1.0, np.abs(K).max() * np.abs(x).max())
+
+
+def test_bk_device_fix_kp(ctx):
+    # device API: fix_kp=1 records kp = k for the second zero column (LAPACK),
+    # info = 1 + the first zero column
+    N = 16
+    K = load("bkz16_K.bin").reshape(N, N)
+    A = torch.from_numpy(K.copy()).cuda()
+    piv = torch.zeros(N, dtype=torch.int32, device="cuda")
+    info = ctx.bk_factor(N, A.data_ptr(), N, piv.data_ptr(), fix_kp=True)
+    _, po, info_o = oracle.bk_factor(K, fix_kp=True)
+    assert info == info_o + 1
+    assert np.array_equal(piv.cpu().numpy(), po.astype(np.int32))
