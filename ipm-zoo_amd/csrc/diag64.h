@@ -127,7 +127,9 @@ using namespace diag64;
 // workgroups of the same launch.  clk != nullptr records stage clocks.
 // TS: storage type of K, D and L^{-1} (float for the fp32 factor of the
 // mixed-precision path: the 64 x 64 block itself is factored in fp64).
-template <bool COH, bool LSC = false, typename TS = double>
+// PRE: the block is already in M (row stride DS, lower triangle, upper
+// zero, identity padding past b) -- handed over through LDS by its producer.
+template <bool COH, bool LSC = false, typename TS = double, bool PRE = false>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf) {
@@ -141,7 +143,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   };
   clk();
   // coalesced load, identity padding past b; X upper tiles are never read
-  {
+  if constexpr (!PRE) {
     double t[16];  // all 16 loads in flight: addresses clamped into the valid triangle
 #pragma unroll
     for (int q = 0; q < 16; ++q) {

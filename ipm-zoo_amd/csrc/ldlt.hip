@@ -586,6 +586,15 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 9: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2>(g, st);
     case 10: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_GRP>(g, st);  // (these two spill one VGPR)
     case 14: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st);
+    case 23: return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st);
+    default: break;
+  }
+  // strip (rectangle, upper tiles of the diagonal band skipped) variants
+  g.lower = 1;
+  switch (variant) {
+    case 20: return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st);
+    case 21: return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st);
+    case 22: return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -720,9 +729,16 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // two workgroups per CU = 4 waves per SIMD (kbench: 47 TFLOP/s = 60 % of
   // the fp64 MFMA peak at R = 11008, vs 25 with 4 waves of 64 x 64)
   // ds_read_b64 without read2 fusion + grouped tile order: 53 vs 48 TFLOP/s
-  // (kbench, R = 11008, rank 256)
-  return square_lower ? launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch)
-                      : launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
+  // (kbench, R = 11008, rank 256).  Small updates -- the look-ahead strip and
+  // the trailing updates of the last panels, all latency-bound -- take
+  // 64-wide tiles: 4x the workgroups, a quarter of the work per k-chunk
+  // (kbench rank 256: strip M = 4096 46 -> 24 us, trailing R = 1536 51 -> 34 us)
+  if (square_lower)
+    return M <= 3072 ? launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch)
+                     : launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
+  if (M <= 4096) return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st, batch);
+  if (M <= 8192) return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
+  return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
 }
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,

@@ -244,6 +244,22 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(T* __restrict__ K, int
       const int col = 16 * n + (lane & 15);
       rd[n] = col < bj ? T(1) / ld_sc1(&D[j0 + col]) : T(0);
     }
+    // region chunk: its own diagonal block (columns of block c), the target
+    // of this iteration's first strip piece -- loads in flight during the TRSM
+    acc_t own[4];
+    if (region) {
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int cabs = row0 + 16 * n + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = 16 * wave + MF::row(lane, g);
+          const bool in = row < rows && cabs < ce && cabs <= row0 + row;
+          const T* src = &K[(int64_t)(row0 + (in ? row : 0)) * ld + (in ? cabs : k0)];
+          own[n][g] = in ? (j ? ld_sc1(src) : *src) : T(0);
+        }
+      }
+    }
     __syncthreads();
     // ---- TRSM: wave w owns rows 16w..16w+15, all 64 columns
     acc_t acc[4];
@@ -272,9 +288,53 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(T* __restrict__ K, int
         }
       }
     }
-    if (region) publish(&ctrl[OP_REG + j * OP_NBMAX + c]);
-    // ---- strip: A[c, q] -= L[c, j] W[q, j]^T, q = j+1 .. (region: c; else nb-1)
-    const int qend = region ? c : nb - 1;
+    if (region) {
+      publish(&ctrl[OP_REG + j * OP_NBMAX + c]);  // (its barrier also frees Bs)
+      // ---- own piece first: A[c, c] -= L[c, j] W[c, j]^T with W from this
+      // workgroup's registers through LDS, no global round trip -- for
+      // j = c - 1 it is the last link of the chain to this chunk's diagonal
+      // factorization
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int col = 16 * n + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) Bs[(16 * wave + MF::row(lane, g)) * DS + col] = acc[n][g];
+      }
+      __syncthreads();
+#pragma unroll 4
+      for (int s = 0; s < 16; ++s) {
+        const int k = 4 * s + (lane >> 4);
+        const T a = -As[arow * DS + k];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) own[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], own[n]);
+      }
+      if (j + 1 < c) {  // more blocks to come: back to K (re-read with sc1)
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int cabs = row0 + 16 * n + (lane & 15);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int row = 16 * wave + MF::row(lane, g);
+            if (row < rows && cabs < ce && cabs <= row0 + row) K[(int64_t)(row0 + row) * ld + cabs] = own[n][g];
+          }
+        }
+      } else {  // final: straight into the diagonal factorization's LDS image
+        const int bc = ce - row0 < 64 ? ce - row0 : 64;
+        double* M = smem;
+        __syncthreads();  // every wave done reading As / Bs
+#pragma unroll
+        for (int n = 0; n < 4; ++n) {
+          const int col = 16 * n + (lane & 15);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int row = 16 * wave + MF::row(lane, g);
+            M[row * DS + col] = (row < bc && col <= row) ? (double)own[n][g] : (row == col ? 1.0 : 0.0);
+          }
+        }
+      }
+    }
+    // ---- strip: A[c, q] -= L[c, j] W[q, j]^T, q = j+1 .. (region: c - 1; else nb-1)
+    const int qend = region ? c - 1 : nb - 1;
     for (int q = j + 1; q <= qend; ++q) {
       if (!(ok = wait_flag(&ctrl[OP_REG + j * OP_NBMAX + q], err, &sh_ok))) break;  // also: Bs is free
       const int cbase = k0 + 64 * q;
@@ -317,12 +377,15 @@ __global__ __launch_bounds__(256) void outer_panel_kernel(T* __restrict__ K, int
   }
   if (ok && region) {
     // this chunk's diagonal block: every earlier block's strip is applied
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    // (chunk 0 reads it from K; the others left it in LDS, see above)
     const int j0 = k0 + 64 * c;
     const int bj = ce - j0 < 64 ? ce - j0 : 64;
-    diag64_body<true, true, T>(K, ld, j0, bj, D, Lb0 + (int64_t)c * 64 * 64, info, smem, smem + 64 * DS,
-                               smem + 2 * 64 * DS, nullptr);
+    if (c == 0)
+      diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb0, info, smem, smem + 64 * DS, smem + 2 * 64 * DS,
+                                         nullptr);
+    else
+      diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb0 + (int64_t)c * 64 * 64, info, smem, smem + 64 * DS,
+                                        smem + 2 * 64 * DS, nullptr);
     publish(&ctrl[OP_DIAG + c]);
   }
   // ---- completion: the last workgroup out zeroes the ctrl words

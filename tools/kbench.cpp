@@ -79,6 +79,23 @@ int main(int argc, char** argv) {
       const float ms = t.stop(st);
       std::printf("trailing R=%d nbo=256: %.3f ms %.2f TFLOP/s\n", R, ms, (double)R * (R + 1) * 256 / ms / 1e9);
     }
+    for (int M : {1024, 2048, 4096, 8192}) {  // look-ahead strip: M x 256, rank 256
+      for (int var : {20, 21, 22}) {
+        CK(ipmz::gemm_nt_sub_variant(var, M, 256, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        t.start(st);
+        for (int r = 0; r < 10; ++r) CK(ipmz::gemm_nt_sub_variant(var, M, 256, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        std::printf("strip variant %d M=%d: %.1f us\n", var, M, t.stop(st) / 10 * 1e3);
+      }
+    }
+    for (int R : {768, 1536, 3072, 4608}) {  // small trailing updates
+      for (int var : {14, 23}) {
+        CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        t.start(st);
+        for (int r = 0; r < 10; ++r) CK(ipmz::gemm_nt_sub_variant(var, R, R, 256, W, 256, K, ld, K + 256 * ld + 256, ld, st));
+        const float ms = t.stop(st) / 10;
+        std::printf("trailing variant %d R=%d: %.1f us %.2f TFLOP/s\n", var, R, ms * 1e3, (double)R * (R + 1) * 256 / ms / 1e9);
+      }
+    }
     for (int var : {2, 9, 10, 14}) {
       for (int R : {5632, 11008}) {
         hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
