@@ -108,6 +108,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ir-tol", type=float, default=1e-12, help="c5: refinement tolerance")
     ap.add_argument("--no-timing", action="store_true", help="no per-kernel HIP events (allows graph replay)")
+    ap.add_argument("--batch", type=int, default=0, help="c4: override the global batch (e.g. 128 = one rank's "
+                                                          "shard at 8 GPUs, measured on one GPU)")
     args = ap.parse_args()
 
     import torch
@@ -130,6 +132,8 @@ def main():
     stream = torch.cuda.current_stream()
     ctx = I.Context(local_rank, stream=stream.cuda_stream, nbo=args.nbo, nbi=args.nbi)
     nbatch = wl.get("batch", 0)
+    if nbatch and args.batch:
+        nbatch = args.batch
     if nbatch:  # C4: this rank's contiguous shard of the batch, one Batch object
         from ipmz_amd.dist import shard
         mine = shard(nbatch, world, rank)
@@ -190,7 +194,7 @@ def main():
         steps_total = args.steps * (nbatch if nbatch else world)
         value = steps_total / elapsed
         out = {
-            "metric": ("QP Newton steps/sec, batch of 1024 dense QPs n=256, 1/2/4/8 MI355X" if nbatch else
+            "metric": (f"QP Newton steps/sec, batch of {nbatch} dense QPs n=256, 1/2/4/8 MI355X" if nbatch else
                        "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X"),
             "value": value,
             "unit": "QP-steps/s" if nbatch else "steps/s",

@@ -908,10 +908,16 @@ int step_impl(ipmz_qp* s, int flags) {
     if (s->graph) hipGraphDestroy(s->graph);
     s->gexec = nullptr;
     s->graph = nullptr;
-    HIP_OK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    // capture on the context's own stream: the caller's stream may be the
+    // legacy default stream (torch's), which cannot be captured; the graph
+    // is then launched on the caller's stream
+    hipStream_t cap = s->ctx->own;
+    HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
+    s->ctx->stream = cap;
     int rc = run_step(s, flags);
+    s->ctx->stream = st;
     hipGraph_t g = nullptr;
-    hipError_t e = hipStreamEndCapture(st, &g);
+    hipError_t e = hipStreamEndCapture(cap, &g);
     if (rc) {
       if (g) hipGraphDestroy(g);
       return rc;

@@ -19,6 +19,7 @@
 namespace ipmz {
 
 constexpr int TRSV_NT = 256;
+constexpr int TRSV_SMALL_NMAX = 4096;  // trsv_small_kernel: 2 N doubles of LDS
 
 // Stage an NB x NB row-major block into LDS (padded rows) -- coalesced.
 template <int NB>
@@ -308,10 +309,128 @@ __global__ __launch_bounds__(TRSV_NT) void trsv_batched_kernel(const double* __r
   }
 }
 
+// Small-factor batched solve (config C4, N <= TRSV_SMALL_NMAX, NB = 64):
+// one workgroup of NW waves per QP, the whole vector in LDS and both sweeps
+// LEFT-looking, so every block step is ONE round of independent, coalesced
+// global loads (no read-modify-write of b in global memory, no serial
+// per-row chains):
+//   forward : u_J = b_J - L[J, 0:J0] y[0:J0]      (row segments, lanes over
+//             columns, waves over the block's rows, DPP row sums)
+//             y_J = Linv_J u_J
+//   scale   : z = y / D
+//   backward: u_J = z_J - L[J0+64:N, J]^T x[J0+64:N] (64-wide row segments,
+//             lane = column, waves over rows, LDS cross-wave sum)
+//             x_J = Linv_J^T u_J
+// Linv_J is read from global memory (row-major, identity-padded) with its
+// loads issued ahead of the step's dot products.
+template <int NW>
+__global__ __launch_bounds__(64 * NW) void trsv_small_kernel(const double* __restrict__ K, int64_t ld, int N,
+                                                             const double* __restrict__ D,
+                                                             const double* __restrict__ Linv,
+                                                             double* __restrict__ b, int64_t sK, int64_t sD,
+                                                             int64_t sL, int64_t sb) {
+  extern __shared__ double sm[];
+  constexpr int RW = 64 / NW;  // block rows per wave
+  const int Np = (N + 63) & ~63;
+  double* bv = sm;             // rhs, then x
+  double* yv = sm + Np;        // y, then z
+  double* part = yv + Np;      // NW x 64 partial sums
+  double* ub = part + NW * 64; // 64: the block's u
+  const int64_t q = blockIdx.x;
+  K += q * sK;
+  D += q * sD;
+  Linv += q * sL;
+  b += q * sb;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = tid; t < Np; t += 64 * NW) {
+    bv[t] = t < N ? b[t] : 0.0;
+    yv[t] = 0.0;
+  }
+  __syncthreads();
+  const int nblk = Np / 64;
+  // ---- forward
+  for (int J = 0; J < nblk; ++J) {
+    const int J0 = 64 * J, bj = N - J0 < 64 ? N - J0 : 64;
+    const double* Lb = Linv + (int64_t)J * 64 * 64;
+    double lv[RW], acc[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      lv[k] = Lb[(wave * RW + k) * 64 + lane];
+      acc[k] = 0.0;
+    }
+#pragma unroll 2
+    for (int c0 = 0; c0 < J0; c0 += 64) {
+      const double yc = yv[c0 + lane];
+#pragma unroll
+      for (int k = 0; k < RW; ++k) {
+        const int r = wave * RW + k;
+        const int rr = r < bj ? r : 0;  // clamp: rows past N read row J0 (discarded)
+        acc[k] = fma(K[(int64_t)(J0 + rr) * ld + c0 + lane], yc, acc[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const double s = wave_sum(acc[k]);
+      const int r = wave * RW + k;
+      if (lane == 0) ub[r] = r < bj ? bv[J0 + r] - s : 0.0;
+    }
+    __syncthreads();
+    const double uc = ub[lane];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) {
+      const double s = wave_sum(lv[k] * uc);
+      const int r = wave * RW + k;
+      if (lane == 0 && r < bj) yv[J0 + r] = s;
+    }
+    __syncthreads();
+  }
+  // ---- z = y / D
+  for (int t = tid; t < N; t += 64 * NW) yv[t] = yv[t] / D[t];
+  __syncthreads();
+  // ---- backward
+  for (int J = nblk - 1; J >= 0; --J) {
+    const int J0 = 64 * J, bj = N - J0 < 64 ? N - J0 : 64;
+    const double* Lb = Linv + (int64_t)J * 64 * 64;
+    double lv[RW];
+#pragma unroll
+    for (int k = 0; k < RW; ++k) lv[k] = Lb[(wave * RW + k) * 64 + lane];
+    double acc = 0.0;
+#pragma unroll 8
+    for (int i = J0 + 64 + wave; i < N; i += NW) acc = fma(K[(int64_t)i * ld + J0 + lane], bv[i], acc);
+    part[wave * 64 + lane] = acc;
+    __syncthreads();
+    if (wave == 0) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += part[w * 64 + lane];
+      ub[lane] = lane < bj ? yv[J0 + lane] - s : 0.0;
+    }
+    __syncthreads();
+    double t = 0.0;
+#pragma unroll
+    for (int k = 0; k < RW; ++k) t = fma(lv[k], ub[wave * RW + k], t);
+    part[wave * 64 + lane] = t;
+    __syncthreads();
+    if (wave == 0 && lane < bj) {
+      double s = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) s += part[w * 64 + lane];
+      bv[J0 + lane] = s;
+    }
+    __syncthreads();
+  }
+  for (int t = tid; t < N; t += 64 * NW) b[t] = bv[t];
+}
+
 hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
                               double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st) {
   if (N <= 0 || B <= 0) return hipSuccess;
-  if (nbi == 64)
+  if (nbi == 64 && N <= TRSV_SMALL_NMAX) {
+    constexpr int NW = 8;
+    const size_t lds = (2 * (size_t)((N + 63) & ~63) + NW * 64 + 64) * sizeof(double);
+    hipLaunchKernelGGL((trsv_small_kernel<NW>), dim3(B), dim3(64 * NW), lds, st, K, ld, N, D, Linv, b, sK, sD, sL,
+                       sb);
+  } else if (nbi == 64)
     hipLaunchKernelGGL((trsv_batched_kernel<64>), dim3(B), dim3(TRSV_NT), 0, st, K, ld, N, D, Linv, b, sK, sD, sL, sb);
   else if (nbi == 128)
     hipLaunchKernelGGL((trsv_batched_kernel<128>), dim3(B), dim3(TRSV_NT), 0, st, K, ld, N, D, Linv, b, sK, sD, sL,
