@@ -129,7 +129,9 @@ using namespace diag64;
 // mixed-precision path: the 64 x 64 block itself is factored in fp64).
 // PRE: the block is already in M (row stride DS, lower triangle, upper
 // zero, identity padding past b) -- handed over through LDS by its producer.
-template <bool COH, bool LSC = false, typename TS = double, bool PRE = false>
+// NW: waves in the workgroup (4 or 8); waves >= 4 only load/store and join
+// the barriers.
+template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf) {
@@ -144,17 +146,18 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   clk();
   // coalesced load, identity padding past b; X upper tiles are never read
   if constexpr (!PRE) {
-    double t[16];  // all 16 loads in flight: addresses clamped into the valid triangle
+    constexpr int NQ = 64 / NW;
+    double t[NQ];  // all loads in flight: addresses clamped into the valid triangle
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    for (int q = 0; q < NQ; ++q) {
+      const int rr = (tid >> 6) + NW * q, cc = tid & 63;
       const int r2 = rr < b ? rr : 0, c2 = cc <= r2 ? cc : 0;
       const TS* src = &K[(int64_t)(k0 + r2) * ld + k0 + c2];
       t[q] = (double)(LSC ? ld_sc1(src) : *src);
     }
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    for (int q = 0; q < NQ; ++q) {
+      const int rr = (tid >> 6) + NW * q, cc = tid & 63;
       M[rr * DS + cc] = (rr < b && cc <= rr) ? t[q] : (rr == cc ? 1.0 : 0.0);
     }
   }
@@ -217,7 +220,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   }
   // write back L (strict lower), D, and L^{-1} (64 x 64 row-major, identity-padded)
 #pragma unroll 4
-  for (int idx = tid; idx < 64 * 64; idx += 256) {
+  for (int idx = tid; idx < 64 * 64; idx += 64 * NW) {
     const int rr = idx >> 6, cc = idx & 63;
     if (rr < b && cc < rr) K[(int64_t)(k0 + rr) * ld + k0 + cc] = (TS)M[rr * DS + cc];
     const TS x = (TS)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc]));

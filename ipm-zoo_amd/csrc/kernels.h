@@ -15,6 +15,13 @@ struct BatchStrides {
   int B = 1;
   int64_t sK = 0, sD = 0, sL = 0, sW = 0;
 };
+// small.hip: whole factor per workgroup (N <= IPMZ_SMALL_NMAX, nbi = 64;
+// W: N x 64 per QP)
+#define IPMZ_SMALL_NMAX 1024
+hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
+                                     hipStream_t st, const BatchStrides& bs);
+hipError_t small_clock_probe(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
+                             hipStream_t st, const BatchStrides& bs, unsigned long long* out);
 hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                                int* info, hipStream_t st, const BatchStrides& bs);
 // In-place blocked LDL^T of the lower triangle of K (row-major, ld).

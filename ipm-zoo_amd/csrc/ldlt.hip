@@ -883,6 +883,12 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
   if (N <= 0 || bs.B <= 0) return hipSuccess;
   if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
+  // small systems (C4): the whole factor in one workgroup per QP (small.hip)
+  static const bool small_ok = [] {
+    const char* e = std::getenv("IPMZ_SMALL");
+    return !(e && !std::strcmp(e, "0"));
+  }();
+  if (small_ok && nbi == 64 && N <= IPMZ_SMALL_NMAX) return ldlt_factor_small_batched(K, ld, N, D, Linv, W, info, st, bs);
   hipError_t e = hipSuccess;
   for (int k0 = 0; k0 < N; k0 += nbo) {
     const int bo = N - k0 < nbo ? N - k0 : nbo, t0 = k0 + bo;

@@ -1,0 +1,216 @@
+// Whole LDL^T of one small KKT matrix per workgroup (config C4: batches of
+// N = 320 systems).  Replaces LinearSolvers::ldlt_decomposition
+// (LinearSolvers.cpp:14-42) for the batched path: same factor (unit-lower L
+// in the strict lower triangle of K, D, the 1e-8 zero-pivot rule inside
+// diag64_body), blocked by 64 columns, right-looking, every step inside ONE
+// workgroup -- no launch boundaries, no inter-workgroup hand-offs:
+//   for each 64-column block J:
+//     diag64_body: factor the diagonal block (L_JJ, D_J, L_JJ^{-1})
+//     TRSM  : for every 64-row chunk c below: W_c = A[c, J] L_JJ^{-T},
+//             L[c, J] = W_c / D_J                       (f64 MFMA 16x16x4)
+//     update: A[c, q] -= L[c, J] W_q^T, J < q <= c      (f64 MFMA 16x16x4)
+// The multi-launch batched factor paid a launch + a grid-wide drain per
+// inner block and per update (and left half the chip idle at 128 QPs per
+// GPU); here the only serialization is the algorithm's own.  LDS: the two
+// 64 x DS operand tiles double as diag64_body's M and X (66.5 KB).  Eight
+// waves (two per SIMD) split every 64 x 64 MFMA tile so one wave's LDS and
+// memory waits overlap the other's MFMAs; operand tiles for the next step
+// are loaded into registers while the current one computes.
+#include "common.h"
+#include "kernels.h"
+#include "diag64.h"
+
+namespace ipmz {
+
+namespace {
+typedef Mfma<double> MF;
+typedef MF::acc_t acc_t;
+
+constexpr int SNW = 8;          // waves per workgroup: two per SIMD
+constexpr int SNT = 64 * SNW;   // threads
+constexpr int SFR = 64 / SNW;   // tile rows fetched per thread
+constexpr int SNN = 4 * 4 / SNW;  // 16-column MFMA blocks per wave (rows: 16 (w & 3)..)
+
+// 64 x 64 tile rows [0, nrows) of a row-major source (row stride lds): wave w
+// loads rows w, w+SNW, ... (one 512-byte row per load instruction); rows
+// past nrows read row 0 and are zeroed on the LDS store.
+__device__ __forceinline__ void tile_fetch(const double* __restrict__ src, int64_t lds, int nrows, double (&v)[SFR]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < SFR; ++i) {
+    const int rr = wave + SNW * i;
+    v[i] = src[(int64_t)(rr < nrows ? rr : 0) * lds + lane];
+  }
+}
+__device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&v)[SFR]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < SFR; ++i) {
+    const int rr = wave + SNW * i;
+    dst[rr * DS + lane] = rr < nrows ? v[i] : 0.0;
+  }
+}
+// this wave's part of the 64 x 64 result: rows 16 (w & 3) .. +15, column
+// blocks n0 + (0 .. SNN-1), n0 = SNN (w >> 2)
+__device__ __forceinline__ int tile_r0() { return 16 * ((threadIdx.x >> 6) & 3); }
+__device__ __forceinline__ int tile_n0() { return SNN * (threadIdx.x >> 8); }
+// acc[n] (+)= sgn * As[rows, :] Bs[16 (n0 + n).., :]^T
+template <bool NEG>
+__device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[SNN]) {
+  const int lane = threadIdx.x & 63;
+  const int arow = tile_r0() + (lane & 15), n0 = tile_n0();
+#pragma unroll 4
+  for (int s = 0; s < 16; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    const double a = NEG ? -As[arow * DS + k] : As[arow * DS + k];
+#pragma unroll
+    for (int n = 0; n < SNN; ++n) acc[n] = MF::mma(a, Bs[(16 * (n0 + n) + (lane & 15)) * DS + k], acc[n]);
+  }
+}
+}  // namespace
+
+__device__ unsigned long long g_small_clk[64];  // PROF: stage clocks of workgroup 0 (kbench)
+template <bool PROF>
+__global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
+                                                         double* __restrict__ D, double* __restrict__ Linv,
+                                                         double* __restrict__ W, int* __restrict__ info, int64_t sK,
+                                                         int64_t sD, int64_t sL, int64_t sW) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
+  const int64_t qp = blockIdx.x;
+  K += qp * sK;
+  D += qp * sD;
+  Linv += qp * sL;
+  W += qp * sW;  // N x 64 row-major: the current block column's W = L D
+  const int lane = threadIdx.x & 63;
+  const int r0 = tile_r0(), n0 = tile_n0();
+  double* As = smem;
+  double* Bs = smem + 64 * DS;
+  const int nblk = (N + 63) / 64;
+  auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
+  int nclk = 0;
+  auto clk = [&]() {
+    if (PROF && blockIdx.x == 0 && threadIdx.x == 0 && nclk < 63) g_small_clk[nclk] = __builtin_amdgcn_s_memtime();
+    ++nclk;
+  };
+  clk();
+  for (int J = 0; J < nblk; ++J) {
+    const int J0 = 64 * J;
+    diag64_body<false, false, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
+                                                  smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
+    clk();
+    if (J == nblk - 1) break;
+    __syncthreads();  // diag64_body's LDS is free; its L, D, L^{-1} stores are visible to the workgroup
+    // ---- TRSM of the chunks below (block J is full: J0 + 64 < N)
+    double v[SFR], u[SFR];
+    tile_fetch(Linv + (int64_t)J * 64 * 64, 64, 64, u);
+    tile_fetch(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    double rd[SNN];
+#pragma unroll
+    for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / D[J0 + 16 * (n0 + n) + (lane & 15)];
+    tile_put(Bs, 64, u);
+    for (int c = J + 1; c < nblk; ++c) {
+      const int rows = nrows(c);
+      tile_put(As, rows, v);
+      __syncthreads();
+      if (c + 1 < nblk) tile_fetch(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
+      acc_t acc[SNN];
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
+      tile_mma<false>(As, Bs, acc);
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          if (row < rows) {
+            W[(int64_t)(64 * c + row) * 64 + col] = acc[n][g];
+            K[(int64_t)(64 * c + row) * ld + J0 + col] = acc[n][g] * rd[n];
+          }
+        }
+      }
+      __syncthreads();  // As / Bs reads done before the next tile is staged
+    }
+    clk();
+    // ---- trailing update of the lower triangle below block J, tile (c, q)
+    // in row order (the next diagonal block first); L[c, J] staged once per
+    // row of tiles
+    int c = J + 1, q = J + 1;
+    tile_fetch(K + (int64_t)(64 * c) * ld + J0, ld, nrows(c), v);  // L[c, J]
+    tile_fetch(W + (int64_t)(64 * q) * 64, 64, nrows(q), u);       // W_q
+    for (;;) {
+      const int rows = nrows(c);
+      if (q == J + 1) tile_put(As, rows, v);
+      tile_put(Bs, nrows(q), u);
+      // the target tile C: its loads stay in flight through the MFMA chain,
+      // which accumulates -L W^T from zero; C is added at the end
+      acc_t acc[SNN], cv[SNN];
+      const bool diag = q == c;
+      // this lane's elements: rows r0 + (lane >> 4) + 4g, columns 16 (n0 + n) + (lane & 15)
+      double* Ct = K + (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
+      const double* Ct0 = K + (int64_t)(64 * c) * ld + 64 * q;
+      const int64_t ld4 = 4 * ld;
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+        acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          const bool in = row < rows && (!diag || col <= row);
+          cv[n][g] = *(in ? Ct + g * ld4 + 16 * n : Ct0);  // (out-of-tile lanes: a valid dummy address)
+        }
+      }
+      __syncthreads();
+      // next tile's operands
+      int cn = c, qn = q + 1;
+      if (qn > cn) {
+        ++cn;
+        qn = J + 1;
+      }
+      const bool more = cn < nblk;
+      if (more) {
+        if (qn == J + 1) tile_fetch(K + (int64_t)(64 * cn) * ld + J0, ld, nrows(cn), v);
+        tile_fetch(W + (int64_t)(64 * qn) * 64, 64, nrows(qn), u);
+      }
+      tile_mma<true>(As, Bs, acc);
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          if (row < rows && (!diag || col <= row)) Ct[g * ld4 + 16 * n] = cv[n][g] + acc[n][g];
+        }
+      }
+      __syncthreads();  // As / Bs free; the tile's stores visible to the next diagonal factor
+      if (!more) break;
+      c = cn;
+      q = qn;
+    }
+    clk();
+  }
+  if (PROF && blockIdx.x == 0 && threadIdx.x == 0) g_small_clk[63] = nclk;
+}
+
+hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
+                                     hipStream_t st, const BatchStrides& bs) {
+  if (N <= 0 || bs.B <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ldlt_small_kernel<false>, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD, bs.sL,
+                     bs.sW);
+  return hipGetLastError();
+}
+
+// stage clocks of workgroup 0 (s_memtime): [0] start, then per block J:
+// after diag, after TRSM, after the trailing update; [63] = count
+hipError_t small_clock_probe(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
+                             hipStream_t st, const BatchStrides& bs, unsigned long long* out) {
+  hipLaunchKernelGGL(ldlt_small_kernel<true>, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
+                     bs.sL, bs.sW);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_small_clk), sizeof(unsigned long long) * 64, 0,
+                                  hipMemcpyDeviceToHost, st);
+}
+
+}  // namespace ipmz

@@ -70,6 +70,40 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&pctrl, IPMZ_PANEL_CTRL_WORDS * 4));
   CK(hipMemset(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * 4));
   Timer t;
+  if (argc > 2 && std::string(argv[2]) == "small") {  // batched one-workgroup factor (C4)
+    for (int B : {1, 128, 256, 1024}) {
+      double *Kb, *Db, *Lb, *Wb;
+      const int64_t sK = ld * N, sL = (int64_t)((N + 63) / 64) * 64 * 64;
+      CK(hipMalloc(&Kb, sK * B * 8));
+      CK(hipMalloc(&Db, (int64_t)N * B * 8));
+      CK(hipMalloc(&Lb, sL * B * 8));
+      CK(hipMalloc(&Wb, (int64_t)N * 64 * B * 8));
+      ipmz::BatchStrides bs;
+      bs.B = B;
+      bs.sK = sK;
+      bs.sD = N;
+      bs.sL = sL;
+      bs.sW = (int64_t)N * 64;
+      for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
+      unsigned long long clk[64];
+      CK(ipmz::small_clock_probe(Kb, ld, N, Db, Lb, Wb, info, st, bs, clk));
+      CK(hipStreamSynchronize(st));
+      if (B == 1) {
+        std::printf("small N=%d stage clocks (diag / trsm / update per block):", N);
+        for (unsigned i = 1; i < clk[63] && i < 63; ++i) std::printf(" %llu", clk[i] - clk[i - 1]);
+        std::printf("  total %llu\n", clk[clk[63] - 1] - clk[0]);
+      }
+      for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
+      t.start(st);
+      CK(ipmz::ldlt_factor_small_batched(Kb, ld, N, Db, Lb, Wb, info, st, bs));
+      std::printf("small factor N=%d B=%d: %.1f us\n", N, B, t.stop(st) * 1e3);
+      CK(hipFree(Kb));
+      CK(hipFree(Db));
+      CK(hipFree(Lb));
+      CK(hipFree(Wb));
+    }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "gemm") {  // trailing GEMM alone (PMC passes)
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     const int R = N - 256;
