@@ -170,11 +170,17 @@ int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, do
 int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const double* D, double* b);
 
 /* ---- the Newton-step solver --------------------------------------------- */
+/* Settings::EqualityHandling (SymbolicOptimization.h:28-64) */
+#define IPMZ_EQ_REGULARIZATION 0 /* (lambda_C, lambda_C) block -delta^2, slack p: LDL^T   */
+#define IPMZ_EQ_NONE 1           /* zero (lambda_C, lambda_C) block, no p: the reference's
+                                    "indefinite" case (Optimizer.cpp:63-75), factored with
+                                    Bunch-Kaufman (LinearSolvers.cpp:76-318); N <= 4096 */
 typedef struct ipmz_qp_config {
   int n;         /* primal dimension                                  */
   int m;         /* inequality rows  l_A <= A x <= u_A (SlackedSlacks) */
-  int p;         /* equality rows C x = d (Regularization)            */
+  int p;         /* equality rows C x = d                              */
   double delta;  /* regularization (EnvironmentBuilder.cpp:48: 1e-4)  */
+  int equality_handling; /* IPMZ_EQ_* (0 = Regularization)            */
 } ipmz_qp_config;
 
 int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out);

@@ -596,6 +596,10 @@ struct ipmz_qp {
   char* mws = nullptr;
   // normal-equations reduction (C2)
   bool normal = false;
+  // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
+  bool eqnone = false;
+  int* ipiv = nullptr;
+  int64_t sP = 0;
   char* nws = nullptr;
   hipGraph_t graph = nullptr;
   hipGraphExec_t gexec = nullptr;
@@ -615,6 +619,7 @@ int64_t slot_len(const ipmz_qp* s, int slot) {
   switch (slot) {
     case X: case LY: case LZ: case Y: case Z: return s->n;
     case LA: case S: case LG: case LH: case G: case H: return s->m;
+    case P: return s->eqnone ? 0 : s->p;
     default: return s->p;
   }
 }
@@ -641,7 +646,9 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
 QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
 
 int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
-  if (s->normal) {
+  if (s->eqnone) {  // overwriting_solve_bunch_kaufman
+    HIP_OK(bk_solve(s->K, s->ldk, s->N, s->ipiv, q0(s).b, s->B, s->sK, s->sP, s->sb, st));
+  } else if (s->normal) {
     return normal_solve_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
                              normal_ws(s->nws, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi), q0(s).b);
   } else if (s->mixed) {
@@ -658,6 +665,10 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
 }
 
 int factor_batch(ipmz_qp* s, TrailTimer* tt) {
+  if (s->eqnone) {  // zero diagonal block: symmetric_indefinite_factorization (reference kp behaviour)
+    HIP_OK(bk_factor(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->B, s->sK, s->sP, s->ctx->stream));
+    return IPMZ_OK;
+  }
   if (s->mixed) return mixed_factor_impl(s->ctx, s->K, s->ldk, s->mw, tt);
   if (s->normal)
     return normal_factor_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
@@ -747,6 +758,11 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   *out = nullptr;
   if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0 || B <= 0)
     return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
+  if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE)
+    return fail(IPMZ_ERR_INVALID, "unknown equality handling");
+  if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + cfg->m + cfg->p > IPMZ_BK_NMAX)
+    return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
+                                  "N <= " + std::to_string(IPMZ_BK_NMAX));
   HIP_OK(hipSetDevice(ctx->device));
   auto* s = new ipmz_qp();
   s->ctx = ctx;
@@ -756,9 +772,10 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->p = cfg->p;
   s->N = cfg->n + cfg->m + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
+  s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
   s->ldn = round_up(s->n, 8);
   s->ldk = round_up(s->N, 64);
-  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + 2 * (int64_t)s->p;
+  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + (s->eqnone ? 1 : 2) * (int64_t)s->p;
   const int n = s->n, m = s->m, p = s->p, N = s->N;
   int64_t sQ, sA, sC, sn, sm, sp, sS, sNb, sScal, sPart, sT;
   double* Q = dev_array(s, (int64_t)n * s->ldn, &sQ);
@@ -806,6 +823,18 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     if (ok) s->allocs.push_back(w);
     s->binfo = static_cast<int*>(w);
   }
+  if (ok && s->eqnone) {
+    s->sP = round_up(N, 16);
+    void* w = nullptr;
+    ok = hipMalloc(&w, (size_t)(s->sP * B) * sizeof(int)) == hipSuccess;
+    if (ok) s->allocs.push_back(w);
+    s->ipiv = static_cast<int*>(w);
+    if (ok && !s->binfo) {
+      ok = hipMalloc(&w, 256) == hipSuccess;
+      if (ok) s->allocs.push_back(w);
+      s->binfo = static_cast<int*>(w);
+    }
+  }
   if (!ok) {
     ipmz_qp_destroy(s);
     return fail(IPMZ_ERR_NOMEM, "device allocation failed");
@@ -822,6 +851,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.ldk = s->ldk;
     q.state_len = s->state_len;
     q.delta = s->delta;
+    q.eqnone = s->eqnone ? 1 : 0;
     q.Q = Q + i * sQ;
     q.A = A + i * sA;
     q.C = C + i * sC;
@@ -1086,8 +1116,9 @@ int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
 
 int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refine) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
-  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0 || s->normal))
-    return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0, augmented reduction");
+  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0 || s->normal || s->eqnone))
+    return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0, augmented reduction, "
+                                  "Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (enable && !s->mws) {
     const int64_t bytes = mixed_ws_bytes(s->N, s->ctx->nbo);
@@ -1113,8 +1144,8 @@ int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
   if (reduction != IPMZ_REDUCTION_AUGMENTED && reduction != IPMZ_REDUCTION_NORMAL)
     return fail(IPMZ_ERR_INVALID, "unknown reduction");
-  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed))
-    return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision");
+  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed || s->eqnone))
+    return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision, Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (reduction == IPMZ_REDUCTION_NORMAL && !s->nws) {
     const int64_t bytes = normal_ws(nullptr, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi).total;

@@ -141,7 +141,7 @@ __global__ void k_init_iterate(const QPDev* __restrict__ qs) {
   }
   if (t < q.p) {
     q.v[LC][t] = 1.0;
-    q.v[P][t] = 1.0;
+    if (!q.eqnone) q.v[P][t] = 1.0;
   }
 }
 
@@ -269,11 +269,17 @@ __global__ __launch_bounds__(NT) void k_residuals(const QPDev* __restrict__ qs, 
       comp += fabs(rg) + fabs(rh);
     } else {
       const int i = t - n - m;
-      const double rlc = (q.Cx[i] + q.delta * q.v[P][i]) + (-q.d[i]);
-      const double rp = q.v[P][i] + q.delta * q.v[LC][i];
-      q.r[LC][i] = rlc;
-      q.r[P][i] = rp;
-      res2 += rlc * rlc + rp * rp;
+      if (q.eqnone) {  // ((C*x) - d)
+        const double rlc = q.Cx[i] + (-q.d[i]);
+        q.r[LC][i] = rlc;
+        res2 += rlc * rlc;
+      } else {  // ((C*x) + (delta*p) - d), (p + (delta*lambda_C))
+        const double rlc = (q.Cx[i] + q.delta * q.v[P][i]) + (-q.d[i]);
+        const double rp = q.v[P][i] + q.delta * q.v[LC][i];
+        q.r[LC][i] = rlc;
+        q.r[P][i] = rp;
+        res2 += rlc * rlc + rp * rp;
+      }
     }
   }
   if (!with_stats) return;
@@ -363,7 +369,7 @@ __global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
     const double* Cr = q.C + (int64_t)r * q.ldn;
     for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Cr[j];
     for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
-    if (threadIdx.x == 0) Kr[i] = -(q.delta * q.delta);
+    if (threadIdx.x == 0) Kr[i] = q.eqnone ? 0.0 : -(q.delta * q.delta);
   }
 }
 
@@ -390,7 +396,7 @@ __global__ void k_rhs(const QPDev* __restrict__ qs) {
     q.b[t] = ds_inv(q, i) * ((th + (-q.r[S][i])) + (-tg)) + (-q.r[LA][i]);
   } else if (t < q.N) {
     const int i = t - n - m;
-    q.b[t] = q.delta * q.r[P][i] + (-q.r[LC][i]);
+    q.b[t] = q.eqnone ? -q.r[LC][i] : q.delta * q.r[P][i] + (-q.r[LC][i]);
   }
 }
 
@@ -441,7 +447,7 @@ __global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
     const int i = t - n - m;
     const double dlc = q.b[t];
     D.d[LC][i] = dlc;
-    D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
+    if (!q.eqnone) D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
   }
 }
 
@@ -597,7 +603,7 @@ __global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
   }
   if (t < p) {
     q.v[LC][t] = q.v[LC][t] + s * q.dir[LC][t];
-    q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
+    if (!q.eqnone) q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
   }
 }
 

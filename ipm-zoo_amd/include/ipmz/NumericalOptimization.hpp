@@ -104,14 +104,21 @@ struct IterationRecord {
   double f, res, mu, alpha_aff, mu_aff, sigma, alpha;
 };
 
+// Settings::EqualityHandling (SymbolicOptimization.h:28-64), the two the
+// numeric path supports: Regularization (quasi-definite, LDL^T) and None
+// (zero diagonal block: Optimizer::solve's indefinite branch,
+// Optimizer.cpp:63-75, on the Bunch-Kaufman factor)
+enum class EqualityHandling { Regularization = IPMZ_EQ_REGULARIZATION, None = IPMZ_EQ_NONE };
+
 // build_environment + Optimizer: the iterate lives in device memory; solve()
 // runs Optimizer.cpp:124-219 (tolerance 1e-8, at most 100 iterations).
 class Optimizer {
  public:
-  explicit Optimizer(const Data& d, Context& ctx = Context::instance()) {
+  explicit Optimizer(const Data& d, Context& ctx = Context::instance(),
+                     EqualityHandling eq = EqualityHandling::Regularization) {
     const int n = (int)d.Q.size(), m = (int)d.A_ineq.size(), p = (int)d.A_eq.size();
     n_ = n;
-    ipmz_qp_config cfg{n, m, p, 1e-4};
+    ipmz_qp_config cfg{n, m, p, 1e-4, static_cast<int>(eq)};
     check(ipmz_qp_create(ctx.get(), &cfg, &h_), "ipmz_qp_create");
     auto flat = [](const Matrix& M, size_t cols) {
       std::vector<double> f;

@@ -59,8 +59,13 @@ class IpmzError(AssertionError):
     """A failed libipmz call (the reference throws Utils::AssertionError)."""
 
 
+EQ_REGULARIZATION = 0  # Settings::EqualityHandling::Regularization (include/ipmz.h IPMZ_EQ_*)
+EQ_NONE = 1            # zero (lambda_C, lambda_C) block, Bunch-Kaufman factor
+
+
 class _QPConfig(ctypes.Structure):
-    _fields_ = [("n", ctypes.c_int), ("m", ctypes.c_int), ("p", ctypes.c_int), ("delta", ctypes.c_double)]
+    _fields_ = [("n", ctypes.c_int), ("m", ctypes.c_int), ("p", ctypes.c_int), ("delta", ctypes.c_double),
+                ("equality_handling", ctypes.c_int)]
 
 
 def _load():
@@ -325,12 +330,16 @@ class Optimizer:
     """The Newton-step solver: build_environment + Optimizer (Optimizer.h:15-20).
 
     Formulation: InequalityHandling::SlackedSlacks with Bounds::Both, and
-    EqualityHandling::Regularization (delta = 1e-4) when equalities exist.
+    EqualityHandling::Regularization (delta = 1e-4) when equalities exist --
+    or equality_handling=EQ_NONE: the zero (lambda_C, lambda_C) block the
+    reference routes to solve_indefinite_ (Optimizer.cpp:63-75), factored
+    with Bunch-Kaufman (N <= 4096).
     """
 
-    def __init__(self, n, m=0, p=0, ctx=None, delta=1e-4):
+    def __init__(self, n, m=0, p=0, ctx=None, delta=1e-4, equality_handling=0):
         self.ctx = ctx or default_context()
-        cfg = _QPConfig(n, m, p, delta)
+        cfg = _QPConfig(n, m, p, delta, equality_handling)
+        self.equality_handling = equality_handling
         h = _VP()
         _check(lib.ipmz_qp_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)), "ipmz_qp_create")
         self.h = h
@@ -442,9 +451,10 @@ class Batch(Optimizer):
     kernel launch serves the whole batch.  QP i of generate(seed) uses
     seed + i."""
 
-    def __init__(self, n, m=0, p=0, batch=1, ctx=None, delta=1e-4):
+    def __init__(self, n, m=0, p=0, batch=1, ctx=None, delta=1e-4, equality_handling=0):
         self.ctx = ctx or default_context()
-        cfg = _QPConfig(n, m, p, delta)
+        cfg = _QPConfig(n, m, p, delta, equality_handling)
+        self.equality_handling = equality_handling
         h = _VP()
         _check(lib.ipmz_batch_create(self.ctx.h, ctypes.byref(cfg), batch, ctypes.byref(h)), "ipmz_batch_create")
         self.h = h

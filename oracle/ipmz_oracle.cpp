@@ -59,6 +59,11 @@ enum Slot { X, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
 struct QP {
   int64_t n, m, p;
   double delta;  // EnvironmentBuilder.cpp:48
+  // EqualityHandling::None (tests/golden/formulations.txt): no p, a zero
+  // (lambda_C, lambda_C) block -- the reference's "indefinite" case, factored
+  // with Bunch-Kaufman (Optimizer.cpp:63-75; solve_indefinite_ is ASSERT(false)
+  // there, this is the completion §8f row f3 asks for)
+  bool eq_none = false;
   Vec Q, c, A, lA, uA, C, d, lx, ux;
   Vec v[NSLOT];       // iterate
   Vec daff[NSLOT], dir[NSLOT];
@@ -67,6 +72,7 @@ struct QP {
     switch (s) {
       case X: case LY: case LZ: case Y: case Z: return n;
       case LA: case S: case LG: case LH: case G: case H: return m;
+      case P: return eq_none ? 0 : p;
       default: return p;
     }
   }
@@ -128,7 +134,8 @@ void residuals(const QP& q, double mu, Residuals& R) {
     R.r[G][i] = v[G][i] * v[LG][i] + (-(mu * 1.0));
     R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
   }
-  for (int64_t i = 0; i < p; ++i) {
+  for (int64_t i = 0; i < p && q.eq_none; ++i) R.r[LC][i] = Cx[i] + (-q.d[i]);  // ((C*x) - d)
+  for (int64_t i = 0; i < p && !q.eq_none; ++i) {
     R.r[LC][i] = (Cx[i] + q.delta * v[P][i]) + (-q.d[i]);          // ((C*x) + (delta*p) - d)
     R.r[P][i] = v[P][i] + q.delta * v[LC][i];                      // (p + (delta*lambda_C))
   }
@@ -215,7 +222,7 @@ void assemble(const QP& q, double* K) {
       K[(n + m + r) * N + j] = q.C[r * n + j];
       K[j * N + n + m + r] = q.C[r * n + j];
     }
-    K[(n + m + r) * N + n + m + r] = -(q.delta * q.delta);
+    K[(n + m + r) * N + n + m + r] = q.eq_none ? 0.0 : -(q.delta * q.delta);
   }
 }
 
@@ -233,7 +240,8 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
     const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
     b[n + i] = ds_inv(q, i) * ((th + (-R.r[S][i])) + (-tg)) + (-R.r[LA][i]);
   }
-  for (int64_t i = 0; i < p; ++i) b[n + m + i] = q.delta * R.r[P][i] + (-R.r[LC][i]);
+  for (int64_t i = 0; i < p; ++i)  // None: -r_lambda_C ; Regularization: (delta*r_p) - r_lambda_C
+    b[n + m + i] = q.eq_none ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
 }
 
 // Eliminated-variable back-substitution (delta_definitions evaluated in
@@ -251,7 +259,7 @@ void back_substitute(const QP& q, const Residuals& R, Vec* D) {
     D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));
     D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
   }
-  for (int64_t i = 0; i < p; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
+  for (int64_t i = 0; i < p && !q.eq_none; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
   for (int64_t i = 0; i < n; ++i) {
     const double dx = D[X][i];
     D[LY][i] = -((inv(v[Y][i]) * v[LY][i]) * ((dx + inv(v[LY][i]) * R.r[Y][i]) + (-R.r[LY][i])));
@@ -325,17 +333,29 @@ void axpy_all(QP& q, double s, const Vec* D) {
     for (int64_t j = 0; j < q.size(slot); ++j) q.v[slot][j] = q.v[slot][j] + s * D[slot][j];
 }
 
+}  // namespace
+static int bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, bool fix_kp);
+static void bk_solve(int64_t n, const double* L, int64_t ld, const int64_t* ipiv, double* b);
+namespace {
+
 // One Newton iteration (Optimizer.cpp:127-219).  rec = {f, res, mu,
 // alpha_aff, mu_aff, sigma, alpha, converged}.
-struct Workspace {
-  Vec K, L, Dd, b;
+// The factor: ldlt_decomposition for the quasi-definite KKT matrix; for a
+// zero diagonal block (EqualityHandling::None, Optimizer.cpp:63-75)
+// symmetric_indefinite_factorization + overwriting_solve_bunch_kaufman, with
+// the reference's kp = 0 behaviour (fix_kp = false).  L holds F, ipiv the
+// pivots, in that case.
+struct Factor {
+  Vec L, Dd;
+  std::vector<int64_t> ipiv;
 };
 
-void search_direction(QP& q, const Residuals& R, const Vec& L, const Vec& Dd, Vec* out) {
+void search_direction(QP& q, const Residuals& R, const Factor& F, Vec* out) {
   const int64_t N = q.N(), n = q.n, m = q.m;
   Vec b(N);
   augmented_rhs(q, R, b.data());
-  solve_ldlt(N, L.data(), N, Dd.data(), b.data());
+  if (q.eq_none) bk_solve(N, F.L.data(), N, F.ipiv.data(), b.data());
+  else solve_ldlt(N, F.L.data(), N, F.Dd.data(), b.data());
   for (int s = 0; s < NSLOT; ++s) out[s].assign(q.size(s), 0.0);
   std::memcpy(out[X].data(), b.data(), sizeof(double) * n);
   std::memcpy(out[LA].data(), b.data() + n, sizeof(double) * m);
@@ -352,11 +372,20 @@ int iterate(QP& q, double* rec, double* phase_s) {
   rec[2] = mu_of(q);
   rec[7] = (rec[1] < 1e-8 && rec[2] < 1e-8) ? 1.0 : 0.0;
   if (rec[7] != 0.0) return 1;
-  Vec K((size_t)(N * N)), L((size_t)(N * N)), Dd(N);
+  Vec K((size_t)(N * N));
+  Factor F;
   const auto t0 = std::chrono::steady_clock::now();
   assemble(q, K.data());
   const auto t1 = std::chrono::steady_clock::now();
-  ldlt(N, K.data(), N, L.data(), N, Dd.data());
+  if (q.eq_none) {
+    F.ipiv.assign(N, 0);
+    bk_factor(N, K.data(), N, F.ipiv.data(), false);
+    F.L = std::move(K);
+  } else {
+    F.L.assign((size_t)(N * N), 0.0);
+    F.Dd.assign(N, 0.0);
+    ldlt(N, K.data(), N, F.L.data(), N, F.Dd.data());
+  }
   const auto t2 = std::chrono::steady_clock::now();
   if (phase_s) {
     phase_s[0] = std::chrono::duration<double>(t1 - t0).count();
@@ -365,7 +394,7 @@ int iterate(QP& q, double* rec, double* phase_s) {
   const double mu = rec[2];
   Residuals R;
   residuals(q, 0.0, R);
-  search_direction(q, R, L, Dd, q.daff);
+  search_direction(q, R, F, q.daff);
   const double a_aff = max_step(q, q.daff);
   Vec saved[NSLOT];
   for (int s = 0; s < NSLOT; ++s) saved[s] = q.v[s];
@@ -381,7 +410,7 @@ int iterate(QP& q, double* rec, double* phase_s) {
   for (int k = 0; k < 4; ++k)
     for (int64_t i = 0; i < q.size(comp[k]); ++i)
       R.r[comp[k]][i] = R.r[comp[k]][i] + (q.daff[comp[k]][i] * q.daff[dual[k]][i] + (-(0.0 * 1.0)));
-  search_direction(q, R, L, Dd, q.dir);
+  search_direction(q, R, F, q.dir);
   const double alpha = max_step(q, q.dir);
   axpy_all(q, 0.995 * alpha, q.dir);
   if (phase_s) phase_s[2] = std::chrono::duration<double>(std::chrono::steady_clock::now() - t2).count();
@@ -614,6 +643,16 @@ void* ipmzo_create(int64_t n, int64_t m, int64_t p, const double* Q, const doubl
 }
 
 void ipmzo_destroy(void* h) { delete static_cast<QP*>(h); }
+
+// EqualityHandling::None (call right after ipmzo_create): drops p, zero
+// (lambda_C, lambda_C) block, Bunch-Kaufman factor.
+void ipmzo_set_equality_none(void* h) {
+  QP& q = *static_cast<QP*>(h);
+  q.eq_none = true;
+  q.v[P].clear();
+  q.daff[P].clear();
+  q.dir[P].clear();
+}
 
 int64_t ipmzo_kkt_dim(void* h) { return static_cast<QP*>(h)->N(); }
 

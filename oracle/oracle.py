@@ -22,17 +22,19 @@ SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_
 NONNEG = {"lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"}
 
 
-def slot_size(name, n, m, p):
+def slot_size(name, n, m, p, eq_none=False):
     if name in ("x", "lambda_y", "lambda_z", "y", "z"):
         return n
     if name in ("lambda_A", "s", "lambda_g", "lambda_h", "g", "h"):
         return m
+    if name == "p" and eq_none:
+        return 0
     return p
 
 
-def newton_order(n, m, p):
+def newton_order(n, m, p, eq_none=False):
     """Reference Newton-variable order with absent blocks dropped."""
-    return [s for s in SLOTS if slot_size(s, n, m, p) > 0]
+    return [s for s in SLOTS if slot_size(s, n, m, p, eq_none) > 0]
 
 
 def _dp(a):
@@ -46,6 +48,7 @@ def _load():
     lib.ipmzo_create.restype = ctypes.c_void_p
     lib.ipmzo_create.argtypes = [_i64, _i64, _i64] + [_P] * 9
     lib.ipmzo_destroy.argtypes = [ctypes.c_void_p]
+    lib.ipmzo_set_equality_none.argtypes = [ctypes.c_void_p]
     lib.ipmzo_iterate.argtypes = [ctypes.c_void_p, _P]
     lib.ipmzo_iterate.restype = ctypes.c_int
     lib.ipmzo_iterate_timed.argtypes = [ctypes.c_void_p, _P, _P]
@@ -137,17 +140,21 @@ def bk_solve(F, ipiv, b):
 
 class OracleQP:
     """CPU restatement of Optimizer (SlackedSlacks inequalities, Regularization
-    equalities) from build_environment's initial iterate."""
+    equalities -- or, eq_none=True, EqualityHandling::None with the
+    Bunch-Kaufman factor) from build_environment's initial iterate."""
 
-    def __init__(self, qp):
+    def __init__(self, qp, eq_none=False):
         self.qp = qp
+        self.eq_none = bool(eq_none)
         n, m, p = qp["n"], qp["m"], qp["p"]
         self._keep = [np.ascontiguousarray(qp[k], dtype=np.float64).reshape(-1) if np.size(qp[k]) else np.zeros(1)
                       for k in ("Q", "c", "A", "lA", "uA", "C", "d", "lx", "ux")]
         self.h = ctypes.c_void_p(lib().ipmzo_create(n, m, p, *[_dp(a) for a in self._keep]))
+        if self.eq_none:
+            lib().ipmzo_set_equality_none(self.h)
         self.N = lib().ipmzo_kkt_dim(self.h)
         self.L = lib().ipmzo_state_len(self.h)
-        self.order = newton_order(n, m, p)
+        self.order = newton_order(n, m, p, self.eq_none)
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -208,7 +215,7 @@ class OracleQP:
         n, m, p = self.qp["n"], self.qp["m"], self.qp["p"]
         out, off = {}, 0
         for s in self.order:
-            k = slot_size(s, n, m, p)
+            k = slot_size(s, n, m, p, self.eq_none)
             out[s] = flat[off:off + k]
             off += k
         return out

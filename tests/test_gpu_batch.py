@@ -17,7 +17,7 @@ def ctx():
 
 
 @pytest.mark.parametrize("n,m,p,B,seed0", [(64, 16, 0, 5, 100), (256, 64, 0, 12, 0), (96, 24, 8, 4, 7),
-                                           (300, 60, 0, 3, 50)])
+                                           (300, 60, 0, 3, 50), (700, 90, 10, 2, 60)])
 def test_batch_steps_vs_oracle(ctx, n, m, p, B, seed0):
     bt = I.Batch(n, m, p, B, ctx)
     bt.generate(seed0)
