@@ -175,6 +175,8 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
 #define IPMZ_EQ_NONE 1           /* zero (lambda_C, lambda_C) block, no p: the reference's
                                     "indefinite" case (Optimizer.cpp:63-75), factored with
                                     Bunch-Kaufman (LinearSolvers.cpp:76-318); N <= 4096 */
+#define IPMZ_EQ_PENALTY 2        /* PenaltyFunction: -mu (lambda_C, lambda_C) block (mu I,
+                                    mu = the iterate's environment mu), no p: LDL^T */
 typedef struct ipmz_qp_config {
   int n;         /* primal dimension                                  */
   int m;         /* inequality rows  l_A <= A x <= u_A (SlackedSlacks) */

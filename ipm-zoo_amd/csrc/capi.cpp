@@ -598,6 +598,7 @@ struct ipmz_qp {
   bool normal = false;
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
+  bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   int* ipiv = nullptr;
   int64_t sP = 0;
   char* nws = nullptr;
@@ -619,7 +620,7 @@ int64_t slot_len(const ipmz_qp* s, int slot) {
   switch (slot) {
     case X: case LY: case LZ: case Y: case Z: return s->n;
     case LA: case S: case LG: case LH: case G: case H: return s->m;
-    case P: return s->eqnone ? 0 : s->p;
+    case P: return (s->eqnone || s->eqpen) ? 0 : s->p;
     default: return s->p;
   }
 }
@@ -758,7 +759,8 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   *out = nullptr;
   if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0 || B <= 0)
     return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
-  if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE)
+  if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE &&
+      cfg->equality_handling != IPMZ_EQ_PENALTY)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
   if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + cfg->m + cfg->p > IPMZ_BK_NMAX)
     return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
@@ -773,9 +775,10 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->N = cfg->n + cfg->m + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
+  s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY;
   s->ldn = round_up(s->n, 8);
   s->ldk = round_up(s->N, 64);
-  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + (s->eqnone ? 1 : 2) * (int64_t)s->p;
+  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + ((s->eqnone || s->eqpen) ? 1 : 2) * (int64_t)s->p;
   const int n = s->n, m = s->m, p = s->p, N = s->N;
   int64_t sQ, sA, sC, sn, sm, sp, sS, sNb, sScal, sPart, sT;
   double* Q = dev_array(s, (int64_t)n * s->ldn, &sQ);
@@ -852,6 +855,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.state_len = s->state_len;
     q.delta = s->delta;
     q.eqnone = s->eqnone ? 1 : 0;
+    q.eqpen = s->eqpen ? 1 : 0;
     q.Q = Q + i * sQ;
     q.A = A + i * sA;
     q.C = C + i * sC;
@@ -1116,7 +1120,7 @@ int ipmz_qp_get_kkt(ipmz_qp* s, double* out) {
 
 int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refine) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
-  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0 || s->normal || s->eqnone))
+  if (enable && (s->B != 1 || !(tol > 0.0) || max_refine < 0 || s->normal || s->eqnone || s->eqpen))
     return fail(IPMZ_ERR_INVALID, "mixed precision: single QPs, tol > 0, max_refine >= 0, augmented reduction, "
                                   "Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
@@ -1144,7 +1148,7 @@ int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
   if (reduction != IPMZ_REDUCTION_AUGMENTED && reduction != IPMZ_REDUCTION_NORMAL)
     return fail(IPMZ_ERR_INVALID, "unknown reduction");
-  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed || s->eqnone))
+  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed || s->eqnone || s->eqpen))
     return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision, Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (reduction == IPMZ_REDUCTION_NORMAL && !s->nws) {

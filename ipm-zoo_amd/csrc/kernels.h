@@ -157,6 +157,7 @@ struct QPDev {
   int64_t state_len;
   double delta;
   int eqnone;  // EqualityHandling::None: no p, zero (lambda_C, lambda_C) block
+  int eqpen;   // EqualityHandling::PenaltyFunction: no p, -mu (lambda_C, lambda_C) block
   // problem data (row-major, ld = ldn)
   const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;
   double* v[NSLOT];

@@ -141,8 +141,9 @@ __global__ void k_init_iterate(const QPDev* __restrict__ qs) {
   }
   if (t < q.p) {
     q.v[LC][t] = 1.0;
-    if (!q.eqnone) q.v[P][t] = 1.0;
+    if (!q.eqnone && !q.eqpen) q.v[P][t] = 1.0;
   }
+  if (t == 0) q.scal[SC_MU_NEW] = 1.0;  // the environment's mu (EnvironmentBuilder.cpp:49)
 }
 
 hipError_t qp_init_iterate(const QPBatch& qb, hipStream_t st) {
@@ -273,6 +274,10 @@ __global__ __launch_bounds__(NT) void k_residuals(const QPDev* __restrict__ qs, 
         const double rlc = q.Cx[i] + (-q.d[i]);
         q.r[LC][i] = rlc;
         res2 += rlc * rlc;
+      } else if (q.eqpen) {  // -(d + (mu*lambda_C) - (C*x))
+        const double rlc = -((q.d[i] + mu * q.v[LC][i]) + (-q.Cx[i]));
+        q.r[LC][i] = rlc;
+        res2 += rlc * rlc;
       } else {  // ((C*x) + (delta*p) - d), (p + (delta*lambda_C))
         const double rlc = (q.Cx[i] + q.delta * q.v[P][i]) + (-q.d[i]);
         const double rp = q.v[P][i] + q.delta * q.v[LC][i];
@@ -369,7 +374,7 @@ __global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
     const double* Cr = q.C + (int64_t)r * q.ldn;
     for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Cr[j];
     for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
-    if (threadIdx.x == 0) Kr[i] = q.eqnone ? 0.0 : -(q.delta * q.delta);
+    if (threadIdx.x == 0) Kr[i] = q.eqnone ? 0.0 : q.eqpen ? -q.scal[SC_MU_NEW] : -(q.delta * q.delta);
   }
 }
 
@@ -396,7 +401,7 @@ __global__ void k_rhs(const QPDev* __restrict__ qs) {
     q.b[t] = ds_inv(q, i) * ((th + (-q.r[S][i])) + (-tg)) + (-q.r[LA][i]);
   } else if (t < q.N) {
     const int i = t - n - m;
-    q.b[t] = q.eqnone ? -q.r[LC][i] : q.delta * q.r[P][i] + (-q.r[LC][i]);
+    q.b[t] = (q.eqnone || q.eqpen) ? -q.r[LC][i] : q.delta * q.r[P][i] + (-q.r[LC][i]);
   }
 }
 
@@ -447,7 +452,7 @@ __global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
     const int i = t - n - m;
     const double dlc = q.b[t];
     D.d[LC][i] = dlc;
-    if (!q.eqnone) D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
+    if (!q.eqnone && !q.eqpen) D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
   }
 }
 
@@ -571,6 +576,9 @@ __global__ void k_corrector(const QPDev* __restrict__ qs) {
     i = t - n;
     c0 = G; d0 = LG; c1 = H; d1 = LH;
   } else {
+    // PenaltyFunction: r_lambda_C carries mu (no e, so no affine correction)
+    i = t - n - m;
+    if (q.eqpen && i < q.p) q.r[LC][i] = -((q.d[i] + mu * q.v[LC][i]) + (-q.Cx[i]));
     return;
   }
   q.r[c0][i] = (q.v[c0][i] * q.v[d0][i] + (-(mu * 1.0))) + (q.daff[c0][i] * q.daff[d0][i] + (-(0.0 * 1.0)));
@@ -578,7 +586,8 @@ __global__ void k_corrector(const QPDev* __restrict__ qs) {
 }
 
 hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st) {
-  hipLaunchKernelGGL(k_corrector, grid2((qb.h.n + qb.h.m + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
+  const int rows = qb.h.n + qb.h.m + (qb.h.eqpen ? qb.h.p : 0);
+  hipLaunchKernelGGL(k_corrector, grid2((rows + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
 }
 
@@ -603,7 +612,7 @@ __global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
   }
   if (t < p) {
     q.v[LC][t] = q.v[LC][t] + s * q.dir[LC][t];
-    if (!q.eqnone) q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
+    if (!q.eqnone && !q.eqpen) q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
   }
 }
 

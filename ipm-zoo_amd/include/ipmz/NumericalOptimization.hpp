@@ -104,11 +104,16 @@ struct IterationRecord {
   double f, res, mu, alpha_aff, mu_aff, sigma, alpha;
 };
 
-// Settings::EqualityHandling (SymbolicOptimization.h:28-64), the two the
-// numeric path supports: Regularization (quasi-definite, LDL^T) and None
-// (zero diagonal block: Optimizer::solve's indefinite branch,
-// Optimizer.cpp:63-75, on the Bunch-Kaufman factor)
-enum class EqualityHandling { Regularization = IPMZ_EQ_REGULARIZATION, None = IPMZ_EQ_NONE };
+// Settings::EqualityHandling (SymbolicOptimization.h:41-49), the three the
+// numeric path supports: Regularization (quasi-definite, LDL^T), None (the
+// reference's default: zero diagonal block, Optimizer::solve's indefinite
+// branch, Optimizer.cpp:63-75, on the Bunch-Kaufman factor) and
+// PenaltyFunction (-mu I block, LDL^T)
+enum class EqualityHandling {
+  Regularization = IPMZ_EQ_REGULARIZATION,
+  None = IPMZ_EQ_NONE,
+  PenaltyFunction = IPMZ_EQ_PENALTY
+};
 
 // build_environment + Optimizer: the iterate lives in device memory; solve()
 // runs Optimizer.cpp:124-219 (tolerance 1e-8, at most 100 iterations).

@@ -61,6 +61,7 @@ class IpmzError(AssertionError):
 
 EQ_REGULARIZATION = 0  # Settings::EqualityHandling::Regularization (include/ipmz.h IPMZ_EQ_*)
 EQ_NONE = 1            # zero (lambda_C, lambda_C) block, Bunch-Kaufman factor
+EQ_PENALTY = 2         # PenaltyFunction: -mu (lambda_C, lambda_C) block, LDL^T
 
 
 class _QPConfig(ctypes.Structure):

@@ -64,6 +64,12 @@ struct QP {
   // with Bunch-Kaufman (Optimizer.cpp:63-75; solve_indefinite_ is ASSERT(false)
   // there, this is the completion §8f row f3 asks for)
   bool eq_none = false;
+  // EqualityHandling::PenaltyFunction (formulations.txt): no p, a -mu
+  // (lambda_C, lambda_C) block (mu = the environment's mu when the KKT matrix
+  // is assembled), r_lambda_C := -(d + (mu*lambda_C) - (C*x)); LDL^T.  The
+  // reference's evaluator asserts on the scalar block (Evaluation.cpp:57-60);
+  // here it is mu * I (§8f row f4)
+  bool eq_pen = false;
   Vec Q, c, A, lA, uA, C, d, lx, ux;
   Vec v[NSLOT];       // iterate
   Vec daff[NSLOT], dir[NSLOT];
@@ -72,7 +78,7 @@ struct QP {
     switch (s) {
       case X: case LY: case LZ: case Y: case Z: return n;
       case LA: case S: case LG: case LH: case G: case H: return m;
-      case P: return eq_none ? 0 : p;
+      case P: return (eq_none || eq_pen) ? 0 : p;
       default: return p;
     }
   }
@@ -135,7 +141,9 @@ void residuals(const QP& q, double mu, Residuals& R) {
     R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
   }
   for (int64_t i = 0; i < p && q.eq_none; ++i) R.r[LC][i] = Cx[i] + (-q.d[i]);  // ((C*x) - d)
-  for (int64_t i = 0; i < p && !q.eq_none; ++i) {
+  for (int64_t i = 0; i < p && q.eq_pen; ++i)                                    // -(d + (mu*lambda_C) - (C*x))
+    R.r[LC][i] = -((q.d[i] + mu * v[LC][i]) + (-Cx[i]));
+  for (int64_t i = 0; i < p && !q.eq_none && !q.eq_pen; ++i) {
     R.r[LC][i] = (Cx[i] + q.delta * v[P][i]) + (-q.d[i]);          // ((C*x) + (delta*p) - d)
     R.r[P][i] = v[P][i] + q.delta * v[LC][i];                      // (p + (delta*lambda_C))
   }
@@ -222,7 +230,7 @@ void assemble(const QP& q, double* K) {
       K[(n + m + r) * N + j] = q.C[r * n + j];
       K[j * N + n + m + r] = q.C[r * n + j];
     }
-    K[(n + m + r) * N + n + m + r] = q.eq_none ? 0.0 : -(q.delta * q.delta);
+    K[(n + m + r) * N + n + m + r] = q.eq_none ? 0.0 : q.eq_pen ? -q.mu : -(q.delta * q.delta);
   }
 }
 
@@ -241,7 +249,7 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
     b[n + i] = ds_inv(q, i) * ((th + (-R.r[S][i])) + (-tg)) + (-R.r[LA][i]);
   }
   for (int64_t i = 0; i < p; ++i)  // None: -r_lambda_C ; Regularization: (delta*r_p) - r_lambda_C
-    b[n + m + i] = q.eq_none ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
+    b[n + m + i] = (q.eq_none || q.eq_pen) ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
 }
 
 // Eliminated-variable back-substitution (delta_definitions evaluated in
@@ -259,7 +267,7 @@ void back_substitute(const QP& q, const Residuals& R, Vec* D) {
     D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));
     D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
   }
-  for (int64_t i = 0; i < p && !q.eq_none; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
+  for (int64_t i = 0; i < p && !q.eq_none && !q.eq_pen; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
   for (int64_t i = 0; i < n; ++i) {
     const double dx = D[X][i];
     D[LY][i] = -((inv(v[Y][i]) * v[LY][i]) * ((dx + inv(v[LY][i]) * R.r[Y][i]) + (-R.r[LY][i])));
@@ -646,6 +654,13 @@ void ipmzo_destroy(void* h) { delete static_cast<QP*>(h); }
 
 // EqualityHandling::None (call right after ipmzo_create): drops p, zero
 // (lambda_C, lambda_C) block, Bunch-Kaufman factor.
+void ipmzo_set_equality_penalty(void* h) {
+  QP& q = *static_cast<QP*>(h);
+  q.eq_pen = true;
+  q.v[P].clear();
+  q.daff[P].clear();
+  q.dir[P].clear();
+}
 void ipmzo_set_equality_none(void* h) {
   QP& q = *static_cast<QP*>(h);
   q.eq_none = true;

@@ -23,6 +23,7 @@ NONNEG = {"lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"}
 
 
 def slot_size(name, n, m, p, eq_none=False):
+    """eq_none: any equality handling without the slack p (None, PenaltyFunction)."""
     if name in ("x", "lambda_y", "lambda_z", "y", "z"):
         return n
     if name in ("lambda_A", "s", "lambda_g", "lambda_h", "g", "h"):
@@ -49,6 +50,7 @@ def _load():
     lib.ipmzo_create.argtypes = [_i64, _i64, _i64] + [_P] * 9
     lib.ipmzo_destroy.argtypes = [ctypes.c_void_p]
     lib.ipmzo_set_equality_none.argtypes = [ctypes.c_void_p]
+    lib.ipmzo_set_equality_penalty.argtypes = [ctypes.c_void_p]
     lib.ipmzo_iterate.argtypes = [ctypes.c_void_p, _P]
     lib.ipmzo_iterate.restype = ctypes.c_int
     lib.ipmzo_iterate_timed.argtypes = [ctypes.c_void_p, _P, _P]
@@ -143,14 +145,16 @@ class OracleQP:
     equalities -- or, eq_none=True, EqualityHandling::None with the
     Bunch-Kaufman factor) from build_environment's initial iterate."""
 
-    def __init__(self, qp, eq_none=False):
+    def __init__(self, qp, eq_none=False, eq_penalty=False):
         self.qp = qp
-        self.eq_none = bool(eq_none)
+        self.eq_none = bool(eq_none) or bool(eq_penalty)  # no p block
         n, m, p = qp["n"], qp["m"], qp["p"]
         self._keep = [np.ascontiguousarray(qp[k], dtype=np.float64).reshape(-1) if np.size(qp[k]) else np.zeros(1)
                       for k in ("Q", "c", "A", "lA", "uA", "C", "d", "lx", "ux")]
         self.h = ctypes.c_void_p(lib().ipmzo_create(n, m, p, *[_dp(a) for a in self._keep]))
-        if self.eq_none:
+        if eq_penalty:
+            lib().ipmzo_set_equality_penalty(self.h)
+        elif eq_none:
             lib().ipmzo_set_equality_none(self.h)
         self.N = lib().ipmzo_kkt_dim(self.h)
         self.L = lib().ipmzo_state_len(self.h)

@@ -88,3 +88,40 @@ def test_limits_and_exclusions(ctx):
         g.set_reduction(I.REDUCTION_NORMAL)
     with pytest.raises(I.IpmzError):
         g.set_mixed_precision(True)
+
+
+# ---------------------------------------------------------------------------
+# EqualityHandling::PenaltyFunction (§8f row f4): -mu (lambda_C, lambda_C)
+# block (mu = the environment's mu at assembly), r_lambda_C carries mu; the
+# reference's evaluator asserts on the scalar block (Evaluation.cpp:57-60).
+@pytest.mark.parametrize("n,m,p,seed", [(40, 10, 6, 3), (300, 60, 40, 2)])
+def test_penalty_newton_steps_vs_oracle(ctx, n, m, p, seed):
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), eq_penalty=True)
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_PENALTY)
+    g.generate(seed)
+    assert np.array_equal(g.vars(), o.vars())
+    assert np.array_equal(g.kkt(), np.tril(o.kkt()))  # -mu block with mu = 1 at the start
+    for it in range(5):
+        done, rec = o.iterate()
+        if done:
+            break
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (it, k)
+        _compare(o, g, f"iter {it}")
+        g.set_vars(o.vars())
+
+
+def test_penalty_full_solve(ctx):
+    n, m, p, seed = 64, 16, 8, 1234
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), eq_penalty=True)
+    for it in range(100):
+        done, _ = o.iterate()
+        if done:
+            break
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_PENALTY)
+    g.generate(seed)
+    iters, tr = g.solve(100)
+    assert iters == it and tr[-1]["converged"] == 1.0
+    assert np.abs(g.vars() - o.vars()).max() < 1e-8

@@ -80,3 +80,18 @@ def test_converges_near_regularization():
         out[eq_none] = (it, o.split(o.vars())["x"])
     # same optimum up to the O(delta) regularization perturbation
     assert np.abs(out[True][1] - out[False][1]).max() < 1e-6
+
+
+def test_penalty_formulation_and_kkt():
+    sec = _section("=== inequality_handling=SlackedSlacks equalities=PenaltyFunction inequalities=Both")
+    aug = sec[sec.index("-- augmented system"):sec.index("-- normal equations")]
+    assert "| C | 0 | -\\mu" in aug and "    -r_{\\lambda_{C}}" in aug
+    assert "r_{\\lambda_{C}} := -(d + (\\mu * \\lambda_{C}) - (C * x))" in sec
+    n, m, p = 24, 8, 5
+    qp = oracle.gen_qp(n, m, p, 5)
+    o = oracle.OracleQP(qp, eq_penalty=True)
+    K = o.kkt()
+    assert np.array_equal(np.diag(K)[n + m:], -np.ones(p))  # environment mu = 1 at the start
+    o.iterate()
+    d = o.split(o.daff())
+    assert "p" not in o.order and len(d["lambda_C"]) == p
