@@ -223,7 +223,7 @@ def main():
         }
         traffic = None
         tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath):  # HBM bytes per trailing launch from the committed PMC passes
+        if os.path.exists(tpath) and not mixed and not nbatch:  # HBM bytes per trailing launch, committed PMC passes (fp64 C3 kernel)
             with open(tpath) as f:
                 traffic = json.load(f)
             traffic["source"] = os.path.relpath(tpath, REPO) + " (" + traffic.get("profile", "") + ")"
@@ -239,7 +239,7 @@ def main():
         if ph and nbatch:
             # batched factor: every launch serves the whole shard; the bound at
             # N = 320 is latency, priced here against the fp64 MFMA peak
-            out["roofline"] = {"bound": "mfma", "kernel": "batched blocked LDL^T (whole factor phase)",
+            out["roofline"] = {"bound": "mfma", "kernel": "ldlt_small_kernel (whole LDL^T of each QP in one 8-wave workgroup, fp64 MFMA)",
                                "achieved": out["factor_tflops"], "peak": peak, "unit": "TFLOP/s",
                                "frac": out["factor_tflops"] / peak, "traffic": None,
                                "note": "factor flops B*N^3/3 over the factor phase time (HIP events)"}

@@ -28,7 +28,10 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 // Linv: (ceil(N/nbi)) blocks of nbi x nbi (inverse unit-lower diagonal
 // blocks, consumed by ldlt_solve); W: N x nbo workspace.  info: device int,
 // preset to INT_MAX-ish; receives min(1-based index of a non-finite pivot).
-struct TrailTimer {  // HIP-event pairs around every trailing-update launch
+// trailing updates of order <= this run on 64 x 64 tiles, larger ones on the
+// 128 x 128 kernel (the one TrailTimer times: the roofline kernel of bench.py)
+#define IPMZ_TRAIL_SMALL_M 3072
+struct TrailTimer {  // HIP-event pairs around every dominant trailing-update launch
   hipEvent_t (*pairs)[2] = nullptr;
   int cap = 0, used = 0;
   double flops = 0.0;

@@ -735,7 +735,7 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // 64-wide tiles: 4x the workgroups, a quarter of the work per k-chunk
   // (kbench rank 256: strip M = 4096 46 -> 24 us, trailing R = 1536 51 -> 34 us)
   if (square_lower)
-    return M <= 3072 ? launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch)
+    return M <= IPMZ_TRAIL_SMALL_M ? launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch)
                      : launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
   if (M <= 4096) return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st, batch);
   if (M <= 8192) return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
@@ -927,11 +927,12 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     for (int k = 0; k < npan; ++k) {
       const int k0 = k * nbo, bo = pw(k), t0 = k0 + bo;
       if (t0 < N) {
-        hipEvent_t* te = timer ? timer->next() : nullptr;
+        // timed: the launches of the dominant 128 x 128 trailing kernel
+        hipEvent_t* te = timer && N - t0 > IPMZ_TRAIL_SMALL_M ? timer->next() : nullptr;
         if (te) hipEventRecord(te[0], st);
         e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, t0, N, true, st);
         if (te) hipEventRecord(te[1], st);
-        if (timer) timer->flops += (double)(N - t0) * (double)(N - t0 + 1) * (double)bo;
+        if (te) timer->flops += (double)(N - t0) * (double)(N - t0 + 1) * (double)bo;
         if (e != hipSuccess) return e;
         if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), t0, pw(k + 1), nbo, nbi, info, st, nullptr, pctrl)) != hipSuccess)
           return e;
@@ -956,11 +957,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
     if ((e = hipEventRecord(evN[k], st2)) != hipSuccess) return e;
     if (p3 < N) {
-      hipEvent_t* te = timer ? timer->next() : nullptr;
+      hipEvent_t* te = timer && N - p3 > IPMZ_TRAIL_SMALL_M ? timer->next() : nullptr;
       if (te) hipEventRecord(te[0], st2);
       e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p3, N, true, st2);
       if (te) hipEventRecord(te[1], st2);
-      if (timer) timer->flops += (double)(N - p3) * (double)(N - p3 + 1) * (double)bo;
+      if (te) timer->flops += (double)(N - p3) * (double)(N - p3 + 1) * (double)bo;
       if (e != hipSuccess) return e;
     }
     // ---- stream A: update P_{k+1} with P_k, factor P_{k+1}
