@@ -695,6 +695,8 @@ __global__ __launch_bounds__(512) void mfma_probe_kernel(double* out, int iters)
 hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st) {
   if (nacc == 16) hipLaunchKernelGGL(mfma_probe_kernel<16>, dim3(blocks), dim3(threads), 0, st, out, iters);
   else if (nacc == 8) hipLaunchKernelGGL(mfma_probe_kernel<8>, dim3(blocks), dim3(threads), 0, st, out, iters);
+  else if (nacc == 2) hipLaunchKernelGGL(mfma_probe_kernel<2>, dim3(blocks), dim3(threads), 0, st, out, iters);
+  else if (nacc == 1) hipLaunchKernelGGL(mfma_probe_kernel<1>, dim3(blocks), dim3(threads), 0, st, out, iters);
   else hipLaunchKernelGGL(mfma_probe_kernel<4>, dim3(blocks), dim3(threads), 0, st, out, iters);
   return hipGetLastError();
 }

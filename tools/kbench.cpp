@@ -70,6 +70,20 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&pctrl, IPMZ_PANEL_CTRL_WORDS * 4));
   CK(hipMemset(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * 4));
   Timer t;
+  if (argc > 2 && std::string(argv[2]) == "probe") {  // f64 MFMA throughput vs independent chains, 1 WG per CU
+    for (int threads : {256, 512})
+      for (int nacc : {1, 2, 4, 8, 16}) {
+        const int iters = 4000, blocks = 256;
+        CK(ipmz::mfma_probe(D, blocks, 10, threads, nacc, st));
+        t.start(st);
+        CK(ipmz::mfma_probe(D, blocks, iters, threads, nacc, st));
+        const float ms = t.stop(st);
+        const double n_per_simd = (double)(threads / 64) / 4 * iters * nacc;
+        std::printf("probe threads=%d nacc=%d: %.1f ns per MFMA per SIMD (%.2f TFLOP/s chip)\n", threads, nacc,
+                    ms * 1e6 / n_per_simd, (double)blocks * (threads / 64) * iters * nacc * 2048.0 / ms / 1e9);
+      }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "small") {  // batched one-workgroup factor (C4)
     for (int B : {1, 128, 256, 1024}) {
       double *Kb, *Db, *Lb, *Wb;
@@ -92,6 +106,9 @@ int main(int argc, char** argv) {
         std::printf("small N=%d stage clocks (diag / trsm / update per block):", N);
         for (unsigned i = 1; i < clk[63] && i < 63; ++i) std::printf(" %llu", clk[i] - clk[i - 1]);
         std::printf("  total %llu\n", clk[clk[63] - 1] - clk[0]);
+        for (int w = 0; w < 8; ++w)
+          std::printf("  J=0 trailing, wave %d: mma issue %llu, staging %llu, C store %llu, barrier %llu\n", w,
+                      clk[24 + 4 * w], clk[25 + 4 * w], clk[26 + 4 * w], clk[27 + 4 * w]);
       }
       for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
       t.start(st);
