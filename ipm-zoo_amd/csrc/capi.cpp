@@ -144,10 +144,10 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
 
 // ---------------------------------------------------------------------------
 // Workspace: [info int (256 B)] [panel ctrl words] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
-//            [ybuf N] [zbuf N] [ctrl 2 + 2*nblk64 uint]
+//            [ybuf N] [zbuf N] [sbuf N] [tbuf N] [ctrl 2 + 2*nblk64 uint]
 namespace {
 struct WsLayout {
-  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
+  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, s_off, t_off, ctrl_off, total;
 };
 WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
@@ -159,7 +159,9 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
   l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)
   l.z_off = l.y_off + round_up((int64_t)N * 8, 256);
-  l.ctrl_off = l.z_off + round_up((int64_t)N * 8, 256);
+  l.s_off = l.z_off + round_up((int64_t)N * 8, 256);
+  l.t_off = l.s_off + round_up((int64_t)N * 8, 256);
+  l.ctrl_off = l.t_off + round_up((int64_t)N * 8, 256);
   l.total = l.ctrl_off + round_up((2 + 2 * ((int64_t)N + 63) / 64) * 4, 256);
   return l;
 }
@@ -173,6 +175,17 @@ hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const c
   const WsLayout l = ws_layout(N, nbo, nbi);
   char* w = const_cast<char*>(ws);
   const double* Linv = reinterpret_cast<const double*>(w + l.linv_off);
+  // IPMZ_SOLVE=chain: one chain workgroup + helpers (trsv_chain.hip) --
+  // correct, but 1.3 ms per C3 solve against the dequeued solve's 0.82 ms
+  // (helpers and register spills bound it); not the default
+  static const bool chain = [] {
+    const char* e = std::getenv("IPMZ_SOLVE");
+    return e && !std::strcmp(e, "chain");
+  }();
+  if (chain && nbi == 64)
+    return ldlt_solve_chain(K, ld, N, D, Linv, b, reinterpret_cast<double*>(w + l.y_off),
+                            reinterpret_cast<double*>(w + l.s_off), reinterpret_cast<double*>(w + l.z_off),
+                            reinterpret_cast<double*>(w + l.t_off), reinterpret_cast<unsigned*>(w + l.ctrl_off), st);
   if (use_persistent_solve(nbi))
     return ldlt_solve_persistent(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.y_off),
                                  reinterpret_cast<double*>(w + l.z_off), reinterpret_cast<unsigned*>(w + l.ctrl_off),

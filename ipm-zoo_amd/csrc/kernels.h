@@ -75,6 +75,9 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                          double* C, int64_t ldc, hipStream_t st);
 
+// trsv_chain.hip: one chain workgroup + helpers (4 N-vectors of scratch, ctrl: 2 words)
+hipError_t ldlt_solve_chain(const double* K, int64_t ld, int N, const double* D, const double* Linv, double* b,
+                            double* ybuf, double* sbuf, double* xbuf, double* tbuf, unsigned* ctrl, hipStream_t st);
 // trsv.hip -------------------------------------------------------------------
 // In-place b <- L^{-T} D^{-1} L^{-1} b; side: 2*nbi doubles of scratch.
 hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,

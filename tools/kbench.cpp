@@ -106,9 +106,6 @@ int main(int argc, char** argv) {
         std::printf("small N=%d stage clocks (diag / trsm / update per block):", N);
         for (unsigned i = 1; i < clk[63] && i < 63; ++i) std::printf(" %llu", clk[i] - clk[i - 1]);
         std::printf("  total %llu\n", clk[clk[63] - 1] - clk[0]);
-        for (int w = 0; w < 8; ++w)
-          std::printf("  J=0 trailing, wave %d: mma issue %llu, staging %llu, C store %llu, barrier %llu\n", w,
-                      clk[24 + 4 * w], clk[25 + 4 * w], clk[26 + 4 * w], clk[27 + 4 * w]);
       }
       for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
       t.start(st);
