@@ -118,9 +118,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    # IPMZ_BENCH_SHARED_DEVICE=1: every rank on cuda:0 with the gloo backend --
+    # a rehearsal of the multi-rank path on a one-GPU box (not a measurement)
+    shared = os.environ.get("IPMZ_BENCH_SHARED_DEVICE") == "1"
+    if shared:
+        local_rank = 0
     if world > 1:
         torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if shared:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
     else:
         torch.cuda.set_device(0)
 
