@@ -10,69 +10,25 @@ namespace ipmz {
 // Diagonal block, NB = 64, blocked on fp64 MFMA (the default for nbi = 64).
 //
 // The 64 pivots are sequential whatever the kernel does, so the design goal is
-// the shortest chain per pivot: the block is split into 4 x 4 tiles of 16 and
-// only the 16-pivot leaves run element by element, inside ONE wave with no
-// memory traffic at all (row-per-lane, DPP row_share broadcasts, readlane of
-// the pivot).  Everything between leaves is 16 x 16 x 16 tile products on
-// v_mfma_f64_16x16x4 spread over the 4 waves (A/B fragment: row l&15,
-// k l>>4; C/D: col l&15, row (l>>4) + 4 reg), with one workgroup barrier per
-// stage (8 in all):
-//   leaf  p : L_pp, D_p, X_pp = L_pp^{-1}                       (wave 0)
-//   panel p : T = A_ip X_pp^T, L_ip = T / D_p              (i > p)
-//             X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj       (j < p)
-//   update p: A_ij -= L_ip (L_jp D_p)^T (p < j <= i); wave 0 takes (p+1, p+1) first
-//             and goes straight on to leaf p+1
-// X = L^{-1} (the block inverse the panel TRSM and the solve use) falls out of
-// the same tiles.  Leaf arithmetic is the reference's order
-// (LinearSolvers.cpp:26-36: zero-pivot rule, A[r][c] -= l_r w_c); across
-// tiles the MFMA sums 16-term chunks first (1e-16-level rounding changes).
+// the shortest chain per pivot.  The block is split into 4 block columns of
+// 16; the chain is four COLUMN PASSES on wave 0 (colpass16: every remaining
+// row of the block column eliminated element by element at once, row per
+// lane, pivot column broadcast with v_readlane -- no TRSM step, no inverse
+// on the chain) separated by the v_mfma_f64_16x16x4 update of the next block
+// column's tiles (A: row l&15, k l>>4; C/D: col l&15, row (l>>4) + 4 reg):
+//   pass p   : L[16p:, 16p:16p+16], D_p                          (wave 0)
+//   A(p)     : A_i,p+1 -= L_ip (L_p+1,p D_p)^T, i > p            (3 - p waves)
+//   B(p)     : pass p+1 on wave 0; the other tiles A_ij, p+2 <= j <= i, and
+//              the inverse tiles X_pp (inv16), X_pj = -X_pp sum L_pk X_kj on
+//              waves 1..3 in the pass's shadow
+// X = L^{-1} is an output (the panel TRSM and the solve use it), not an
+// input of the factor.  Stage clocks (kbench pieces): 36 k -> 32-36 k cycles
+// for the block against the earlier leaf16 + TRSM-panel chain.  Arithmetic is
+// the reference's order within a block column (LinearSolvers.cpp:26-36:
+// zero-pivot rule, A[r][c] -= l_r w_c); across block columns the MFMA sums
+// 16-term chunks first (1e-16-level rounding changes).
 namespace diag64 {
 constexpr int DS = 65;  // LDS row stride (doubles) of the 64 x 64 staging arrays
-
-// Wave-level 16 x 16 LDL^T + inverse of the tile at T (row stride DS).  All
-// four 16-lane row groups compute the same thing (lane l: row l & 15); row
-// group 0 stores L (strict lower) back into T, D into dout, X = L^{-1} into Xt.
-__device__ __forceinline__ void leaf16(double* T, double* Xt, double* dout, int lane) {
-  const int r = lane & 15;
-  double v[16];
-#pragma unroll
-  for (int j = 0; j < 16; ++j) v[j] = T[r * DS + j];
-  double dreg = 1.0;
-  static_for<16>([&](auto kc) {
-    constexpr int k = decltype(kc)::value;
-    const double draw = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v[k]), k),
-                                         __builtin_amdgcn_readlane(__double2loint(v[k]), k));
-    const double dk = draw == 0.0 ? 1e-8 : draw;  // LinearSolvers.cpp:26-28
-    const double rdk = fast_rcp(dk);
-    dreg = r == k ? dk : dreg;
-    const double l = v[k] * rdk;
-    static_for<15 - k>([&](auto jc) {
-      constexpr int j = k + 1 + decltype(jc)::value;
-      v[j] = fma(-l, dpp_bcast<0x150 + j>(v[k]), v[j]);  // row_share:j -> w_j
-    });
-    v[k] = l;
-  });
-  // X = L^{-1}, row r: x_r -= L[r][j] x_j for j < r (right-looking over j)
-  double x[16];
-#pragma unroll
-  for (int c = 0; c < 16; ++c) x[c] = c == r ? 1.0 : 0.0;
-  static_for<15>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const double m = r > j ? v[j] : 0.0;
-    static_for<j + 1>([&](auto cc) {
-      constexpr int c = decltype(cc)::value;
-      x[c] = fma(-m, dpp_bcast<0x150 + j>(x[c]), x[c]);
-    });
-  });
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      if (j < r) T[r * DS + j] = v[j];
-      Xt[r * DS + j] = x[j];
-    }
-    dout[r] = dreg;
-  }
-}
 
 // acc += P Q^T over 16 (NT: both operands row-major 16 x 16 tiles, stride DS)
 __device__ __forceinline__ double4_t tile_nt(const double* P, const double* Q, double4_t acc, int lane, bool negP) {
@@ -113,6 +69,59 @@ __device__ __forceinline__ double4_t tile_load(const double* C, int lane) {
 __device__ __forceinline__ void tile_store(double* C, double4_t v, int lane) {
 #pragma unroll
   for (int g = 0; g < 4; ++g) C[((lane >> 4) + 4 * g) * DS + (lane & 15)] = v[g];
+}
+// One wave eliminates block column p (columns 16p .. 16p+15) of rows
+// 16p .. 63 (lane l: row 16p + l): the reference's right-looking update
+// A[r][j] -= l_r w_j with l_r = A[r][k] / d_k, w_j = A[j][k] (LinearSolvers.cpp:
+// 22-36; zero-pivot rule), the pivot and the w_j read from the pivot
+// column's lanes (v_readlane, wave-uniform), every row of the column updated
+// together.  Writes L (strict lower part of the column) back to M and the
+// pivots to dsh.  Upper entries of the diagonal tile are not meaningful.
+__device__ __forceinline__ void colpass16(double* M, double* dsh, int p, int lane) {
+  const int row = 16 * p + lane;
+  const bool act = row < 64;
+  const int rr = act ? row : 63;
+  double v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = M[rr * DS + 16 * p + j];
+  double dreg = 1.0;
+  static_for<16>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const double draw = readlane_t(v[k], k);
+    const double dk = draw == 0.0 ? 1e-8 : draw;  // LinearSolvers.cpp:26-28
+    const double rdk = fast_rcp(dk);
+    dreg = lane == k ? dk : dreg;
+    const double l = lane > k ? v[k] * rdk : 0.0;
+    static_for<15 - k>([&](auto jc) {
+      constexpr int j = k + 1 + decltype(jc)::value;
+      v[j] = fma(-l, readlane_t(v[k], j), v[j]);  // w_j = A[j][k], row j = lane j
+    });
+    v[k] = lane > k ? l : v[k];
+  });
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) M[rr * DS + 16 * p + j] = v[j];
+  }
+  if (lane < 16) dsh[16 * p + lane] = dreg;
+}
+// X_pp = L_pp^{-1} of a unit-lower 16 x 16 tile: lane c (mod 16) solves
+// L x = e_c right-looking (L entries are wave-uniform LDS broadcasts)
+__device__ __forceinline__ void inv16(const double* Lt, double* Xt, int lane) {
+  const int c = lane & 15;
+  double x[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) x[r] = r == c ? 1.0 : 0.0;
+  static_for<15>([&](auto jc) {
+    constexpr int j = decltype(jc)::value;
+    static_for<15 - j>([&](auto rc) {
+      constexpr int r = j + 1 + decltype(rc)::value;
+      x[r] = fma(-Lt[r * DS + j], x[j], x[r]);
+    });
+  });
+  if (lane < 16) {
+#pragma unroll
+    for (int r = 0; r < 16; ++r) Xt[r * DS + c] = x[r];
+  }
 }
 }  // namespace diag64
 using namespace diag64;
@@ -163,61 +172,66 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   }
   __syncthreads();
   clk();
-  if (wave == 0) leaf16(Mt(0, 0), Xt(0, 0), &dsh[0], lane);
+  // Critical chain: four COLUMN PASSES (wave 0), each eliminating a 16-column
+  // block column of every remaining row at once (so no TRSM step and no
+  // inverse on the chain), separated by the MFMA update of the next block
+  // column.  The inverse X = L^{-1} (a consumer output, not an input of the
+  // factor) and the non-critical tile updates run on the other waves in the
+  // shadow of the passes.
+  auto upd = [&](int i, int j, int p) {  // A_ij -= L_ip (L_jp D_p)^T
+    double4_t acc = tile_load(Mt(i, j), lane);
+    acc = tile_nt_lds(Mt(i, p), Mt(j, p), &dsh[16 * p], acc, lane);
+    tile_store(Mt(i, j), acc, lane);
+  };
+  auto xoff = [&](int p, int j) {  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
+    double4_t sacc = {0.0, 0.0, 0.0, 0.0};
+    for (int k = j; k < p; ++k) sacc = tile_nn(Mt(p, k), Xt(k, j), sacc, lane);
+    // S in accumulator layout IS the NN B-fragment
+    double4_t acc = {0.0, 0.0, 0.0, 0.0};
+    const double* xp = Xt(p, p);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) acc = mfma_f64_16x16x4(-xp[(lane & 15) * DS + 4 * q + (lane >> 4)], sacc[q], acc);
+    tile_store(Xt(p, j), acc, lane);
+  };
+  if (wave == 0) colpass16(M, dsh, 0, lane);
   __syncthreads();
   clk();
-  for (int p = 0; p < 4; ++p) {
-    // ---- panel p: TRSM tiles i > p and inverse tiles X_pj, j < p (3 in all)
-    {
-      const int t = wave;  // tiles 0..2
-      if (t < 3) {
-        if (t < 3 - p) {
-          const int i = p + 1 + t;
-          double4_t acc = tile_nt(Mt(i, p), Xt(p, p), (double4_t){0.0, 0.0, 0.0, 0.0}, lane, false);
-          const double rc = 1.0 / dsh[16 * p + (lane & 15)];
-#pragma unroll
-          for (int g = 0; g < 4; ++g) acc[g] = acc[g] * rc;
-          tile_store(Mt(i, p), acc, lane);
-        } else {
-          const int j = t - (3 - p);  // 0 .. p-1
-          double4_t s = {0.0, 0.0, 0.0, 0.0};
-          for (int k = j; k < p; ++k) s = tile_nn(Mt(p, k), Xt(k, j), s, lane);
-          // X_pj = -X_pp S: S in accumulator layout IS the NN B-fragment
-          double4_t acc = {0.0, 0.0, 0.0, 0.0};
-          const double* xp = Xt(p, p);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) acc = mfma_f64_16x16x4(-xp[(lane & 15) * DS + 4 * q + (lane >> 4)], s[q], acc);
-          tile_store(Xt(p, j), acc, lane);
+  for (int p = 0; p < 3; ++p) {
+    // ---- A(p): the critical tiles (i, p+1), i > p, with block column p
+    if (wave < 3 - p) upd(p + 1 + wave, p + 1, p);
+    __syncthreads();
+    clk();
+    // ---- B(p): pass p+1 on wave 0; the other tiles (i, j), p+2 <= j <= i,
+    // with block column p, and the inverse tiles of block row p (X_pp, then
+    // X_pj, j < p, on one wave: they depend on X_pp) -- all in the pass's shadow
+    if (wave == 0) {
+      colpass16(M, dsh, p + 1, lane);
+    } else if (wave < 4) {
+      if (p == 0) {  // tiles (2,2), (3,2), (3,3) on waves 1..3; X_00 after wave 1's tile
+        const int i = wave == 1 ? 2 : 3, j = wave == 3 ? 3 : 2;
+        upd(i, j, 0);
+        if (wave == 1) inv16(Mt(0, 0), Xt(0, 0), lane);
+      } else if (p == 1) {  // tile (3,3); X_11, X_10
+        if (wave == 1) upd(3, 3, 1);
+        if (wave == 2) {
+          inv16(Mt(1, 1), Xt(1, 1), lane);
+          xoff(1, 0);
         }
+      } else if (wave == 1) {  // X_22, X_20, X_21
+        inv16(Mt(2, 2), Xt(2, 2), lane);
+        xoff(2, 0);
+        xoff(2, 1);
       }
     }
     __syncthreads();
     clk();
-    if (p == 3) break;
-    // ---- update p: A_ij -= L_ip W_jp^T, p < j <= i; wave 0: (p+1, p+1) then leaf p+1
-    if (wave == 0) {
-      const int d = p + 1;
-      double4_t acc = tile_load(Mt(d, d), lane);
-      acc = tile_nt_lds(Mt(d, p), Mt(d, p), &dsh[16 * p], acc, lane);
-      tile_store(Mt(d, d), acc, lane);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      clk();
-      leaf16(Mt(d, d), Xt(d, d), &dsh[16 * d], lane);
-    } else {
-      int t = 0;
-      for (int i = p + 1; i < 4; ++i)
-        for (int j = p + 1; j <= i; ++j) {
-          if (i == p + 1 && j == p + 1) continue;
-          if (t++ % 3 != wave - 1) continue;
-          double4_t acc = tile_load(Mt(i, j), lane);
-          acc = tile_nt_lds(Mt(i, p), Mt(j, p), &dsh[16 * p], acc, lane);
-          tile_store(Mt(i, j), acc, lane);
-        }
-    }
-    __syncthreads();
-    clk();
   }
+  // ---- the last row of inverse tiles
+  if (wave == 0) inv16(Mt(3, 3), Xt(3, 3), lane);
+  __syncthreads();
+  if (wave < 3) xoff(3, wave);
+  __syncthreads();
+  clk();
   // write back L (strict lower), D, and L^{-1} (64 x 64 row-major, identity-padded)
 #pragma unroll 4
   for (int idx = tid; idx < 64 * 64; idx += 64 * NW) {
