@@ -103,7 +103,8 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="c3", choices=sorted(WORKLOADS))
-    ap.add_argument("--nbo", type=int, default=int(os.environ.get("IPMZ_NBO", 256)))
+    ap.add_argument("--nbo", type=int, default=int(os.environ.get("IPMZ_NBO", 0)),
+                    help="outer panel width; 0 = libipmz's choice by matrix order (384 for N >= 8192, else 256)")
     ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 64)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--ir-tol", type=float, default=1e-12, help="c5: refinement tolerance")
@@ -225,7 +226,8 @@ def main():
                        "parallelism": (f"batch sharded over {world} rank(s), {B} QPs on rank 0" if nbatch else
                                        f"replicas x{world} (independent QPs)") +
                                       ", RCCL all-reduce of the convergence summary only",
-                       "blocking": {"nbo": args.nbo, "nbi": args.nbi},
+                       "blocking": {"nbo": args.nbo or (384 if Nk >= 8192 and args.nbi == 64 else 256),
+                                    "nbi": args.nbi},
                        "description": wl["desc"]},
             "restarts": s["restarts"],
         }

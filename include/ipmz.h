@@ -99,8 +99,10 @@ int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* hip_stream);
 int ipmz_ctx_reset_stream(ipmz_ctx* ctx);
 int ipmz_ctx_sync(ipmz_ctx* ctx);
 const char* ipmz_last_error(void);
-/* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512),
- * inner diagonal block nbi (64 or 128).  Defaults 256 / 64. */
+/* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512;
+ * 0 = by matrix order: 384 for N >= 8192 with nbi 64, else 256), inner
+ * diagonal block nbi (64 or 128).  Defaults 0 / 64.  Workspace sizes depend
+ * on it: query them after setting the blocking. */
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);
 
 /* ---- LinearSolvers on device memory ------------------------------------ */

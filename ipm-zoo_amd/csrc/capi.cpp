@@ -41,13 +41,22 @@ struct ipmz_ctx {
   int device = 0;
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
-  int nbo = 256, nbi = 64;
+  int nbo = 0, nbi = 64;  // nbo 0: by matrix order (nbo_for)
   // factorization look-ahead: panel path on sA (high priority), trailing
   // updates on sB; forked from / joined to `stream` with events
   hipStream_t sA = nullptr, sB = nullptr;
   std::vector<hipEvent_t> evpool;
   bool lookahead = true;
 };
+
+// outer panel width for an order-N factor: the context's, or by size --
+// 384 for N >= 8192 (C3: 59.7 -> 61.1 steps/s, C5: 31.3 -> 32.4), 256 below
+// (C2: 277 vs 260 at 384).  Every workspace layout and every factor / solve
+// of an order-N matrix uses this same value.
+static int nbo_for(const ipmz_ctx* ctx, int N) {
+  if (ctx->nbo > 0) return ctx->nbo;
+  return N >= 8192 && ctx->nbi == 64 ? 384 : 256;
+}
 
 static int ensure_events(ipmz_ctx* ctx, size_t n) {
   while (ctx->evpool.size() < n) {
@@ -135,8 +144,8 @@ int ipmz_ctx_sync(ipmz_ctx* ctx) {
 
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
   if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
-  if ((nbi != 64 && nbi != 128) || nbo < nbi || nbo % nbi != 0 || nbo > IPMZ_NBO_MAX)
-    return fail(IPMZ_ERR_INVALID, "blocking: nbi in {64,128}, nbo a multiple of nbi, <= 512");
+  if ((nbi != 64 && nbi != 128) || (nbo != 0 && (nbo < nbi || nbo % nbi != 0 || nbo > IPMZ_NBO_MAX)))
+    return fail(IPMZ_ERR_INVALID, "blocking: nbi in {64,128}, nbo 0 (auto) or a multiple of nbi, <= 512");
   ctx->nbo = nbo;
   ctx->nbi = nbi;
   return IPMZ_OK;
@@ -196,20 +205,21 @@ hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const c
 
 int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N) {
   if (!ctx || N < 0) return 0;
-  return ws_layout(N, ctx->nbo, ctx->nbi).total;
+  return ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
 }
 
 static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, char* ws, TrailTimer* timer) {
-  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
+  const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
   int* info = reinterpret_cast<int*>(ws + l.info_off);
   double* Linv = reinterpret_cast<double*>(ws + l.linv_off);
   double* W = reinterpret_cast<double*>(ws + l.w_off);
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
   HIP_OK(hipMemsetAsync(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), ctx->stream));
-  const int npan = (N + ctx->nbo - 1) / ctx->nbo;
+  const int nbo = nbo_for(ctx, N);
+  const int npan = (N + nbo - 1) / nbo;
   if (!ctx->lookahead || npan < 3) {
-    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, 0,
+    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, 0,
                        pctrl));
     return IPMZ_OK;
   }
@@ -221,7 +231,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
   HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
   HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, ctx->nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2, pctrl));
+  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2, pctrl));
   // join (A has already waited for B's tail)
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
@@ -239,7 +249,7 @@ int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, voi
   if (!ctx || N < 0 || (N > 0 && (!K || !D || !ws)) || ld < N || (ld & 1))
     return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_factor: bad arguments (ld >= N, ld even)");
   if (N == 0) return IPMZ_OK;
-  if (ws_bytes < ws_layout(N, ctx->nbo, ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  if (ws_bytes < ws_layout(N, nbo_for(ctx, N), ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
   HIP_OK(hipSetDevice(ctx->device));
   int rc = factor_impl(ctx, N, K, ld, D, static_cast<char*>(ws), nullptr);
   if (rc) return rc;
@@ -250,16 +260,16 @@ int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const dou
   if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_solve: bad arguments");
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
-  HIP_OK(solve_ws(K, ld, N, D, static_cast<const char*>(ws), ctx->nbo, ctx->nbi, b, ctx->stream));
+  HIP_OK(solve_ws(K, ld, N, D, static_cast<const char*>(ws), nbo_for(ctx, N), ctx->nbi, b, ctx->stream));
   return IPMZ_OK;
 }
 
 int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, void* ws, int64_t ws_bytes) {
   if (!ctx || N < 0 || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_ldlt_prepare_solve: bad arguments");
   if (N == 0) return IPMZ_OK;
-  if (ws_bytes < ws_layout(N, ctx->nbo, ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  if (ws_bytes < ws_layout(N, nbo_for(ctx, N), ctx->nbi).total) return fail(IPMZ_ERR_INVALID, "workspace too small");
   HIP_OK(hipSetDevice(ctx->device));
-  const WsLayout l = ws_layout(N, ctx->nbo, ctx->nbi);
+  const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
   HIP_OK(linv_from_l(L, ld, N, ctx->nbi, reinterpret_cast<double*>(static_cast<char*>(ws) + l.linv_off),
                      ctx->stream));
   return IPMZ_OK;
@@ -292,16 +302,16 @@ extern "C" {
 
 int64_t ipmz_mixed_workspace_bytes(ipmz_ctx* ctx, int N) {
   if (!ctx || N < 0) return 0;
-  return mixed_ws_bytes(N, ctx->nbo);
+  return mixed_ws_bytes(N, nbo_for(ctx, N));
 }
 
 int ipmz_mixed_factor(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws, int64_t ws_bytes) {
   if (!ctx || N < 0 || (N > 0 && (!K || !ws)) || ld < N) return fail(IPMZ_ERR_INVALID, "ipmz_mixed_factor: bad arguments");
   if (N == 0) return IPMZ_OK;
-  if (ws_bytes < mixed_ws_bytes(N, ctx->nbo)) return fail(IPMZ_ERR_INVALID, "workspace too small");
+  if (ws_bytes < mixed_ws_bytes(N, nbo_for(ctx, N))) return fail(IPMZ_ERR_INVALID, "workspace too small");
   HIP_OK(hipSetDevice(ctx->device));
   MixedWs w;
-  mixed_ws_carve(static_cast<char*>(ws), N, ctx->nbo, w);
+  mixed_ws_carve(static_cast<char*>(ws), N, nbo_for(ctx, N), w);
   int rc = mixed_factor_impl(ctx, K, ld, w, nullptr);
   if (rc) return rc;
   int info = 0;
@@ -317,7 +327,7 @@ int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws
   if (!K || !ws || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
   HIP_OK(hipSetDevice(ctx->device));
   MixedWs w;
-  mixed_ws_carve(static_cast<char*>(ws), N, ctx->nbo, w);
+  mixed_ws_carve(static_cast<char*>(ws), N, nbo_for(ctx, N), w);
   HIP_OK(mixed_solve(K, ld, w, b, tol, max_refine, ctx->stream));
   if (stat) {
     HIP_OK(hipMemcpyAsync(stat, w.stat, 2 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
@@ -338,7 +348,8 @@ struct NormalWs {
   double *Vt = nullptr, *W = nullptr, *u = nullptr, *part = nullptr;
   int64_t ldv = 0, total = 0;
 };
-NormalWs normal_ws(char* base, int n, int mp, int nbo, int nbi) {
+NormalWs normal_ws(char* base, int n, int mp, const ipmz_ctx* ctx) {
+  const int nbi = ctx->nbi;
   NormalWs w;
   int64_t off = 0;
   auto take = [&](int64_t bytes) {
@@ -348,8 +359,8 @@ NormalWs normal_ws(char* base, int n, int mp, int nbo, int nbi) {
   };
   w.ldv = round_up(n, 8);
   w.info = reinterpret_cast<int*>(take(256));
-  w.wsH = take(ws_layout(n, nbo, nbi).total);
-  w.wsS = take(ws_layout(mp > 0 ? mp : 1, nbo, nbi).total);
+  w.wsH = take(ws_layout(n, nbo_for(ctx, n), nbi).total);
+  w.wsS = take(ws_layout(mp > 0 ? mp : 1, nbo_for(ctx, mp > 0 ? mp : 1), nbi).total);
   w.Vt = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
   w.W = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
   w.u = reinterpret_cast<double*>(take((int64_t)n * 8));
@@ -369,7 +380,7 @@ static int normal_factor_impl(ipmz_ctx* ctx, int n, int mp, double* K, int64_t l
   HIP_OK(ne_check_pos(D, n, 0, w.info, st));
   if (mp == 0) return IPMZ_OK;
   // Vt = B L^{-T}, S = E + Vt D^{-1} Vt^T (into the (2,2) block), Cholesky of S
-  const WsLayout lh = ws_layout(n, ctx->nbo, ctx->nbi);
+  const WsLayout lh = ws_layout(n, nbo_for(ctx, n), ctx->nbi);
   const double* LinvH = reinterpret_cast<const double*>(w.wsH + lh.linv_off);
   HIP_OK(hipMemcpy2DAsync(w.Vt, w.ldv * 8, K + (int64_t)n * ld, ld * 8, (size_t)n * 8, mp, hipMemcpyDeviceToDevice,
                           st));
@@ -385,16 +396,16 @@ static int normal_solve_impl(ipmz_ctx* ctx, int n, int mp, const double* K, int6
                              const NormalWs& w, double* b) {
   hipStream_t st = ctx->stream;
   HIP_OK(hipMemcpyAsync(w.u, b, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-  HIP_OK(solve_ws(K, ld, n, D, w.wsH, ctx->nbo, ctx->nbi, w.u, st));  // u = H^{-1} r0
+  HIP_OK(solve_ws(K, ld, n, D, w.wsH, nbo_for(ctx, n), ctx->nbi, w.u, st));  // u = H^{-1} r0
   if (mp == 0) {
     HIP_OK(hipMemcpyAsync(b, w.u, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
     return IPMZ_OK;
   }
   const double* Bm = K + (int64_t)n * ld;
   HIP_OK(ne_gemv(Bm, ld, mp, n, w.u, b + n, b + n, st));                                     // B u - r1
-  HIP_OK(solve_ws(K + (int64_t)n * ld + n, ld, mp, D + n, w.wsS, ctx->nbo, ctx->nbi, b + n, st));  // l
+  HIP_OK(solve_ws(K + (int64_t)n * ld + n, ld, mp, D + n, w.wsS, nbo_for(ctx, mp), ctx->nbi, b + n, st));  // l
   HIP_OK(ne_gemvt(Bm, ld, mp, n, b + n, w.part, b, st));                                    // r0 - B^T l
-  HIP_OK(solve_ws(K, ld, n, D, w.wsH, ctx->nbo, ctx->nbi, b, st));                           // x
+  HIP_OK(solve_ws(K, ld, n, D, w.wsH, nbo_for(ctx, n), ctx->nbi, b, st));                           // x
   return IPMZ_OK;
 }
 
@@ -402,13 +413,13 @@ extern "C" {
 
 int64_t ipmz_normal_workspace_bytes(ipmz_ctx* ctx, int n, int mp) {
   if (!ctx || n <= 0 || mp < 0) return 0;
-  return normal_ws(nullptr, n, mp, ctx->nbo, ctx->nbi).total;
+  return normal_ws(nullptr, n, mp, ctx).total;
 }
 
 int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes) {
   if (!ctx || n <= 0 || mp < 0 || !K || !D || !ws || ld < n + mp || (ld & 1))
     return fail(IPMZ_ERR_INVALID, "ipmz_normal_factor: bad arguments (n > 0, ld >= n + mp, ld even)");
-  const NormalWs w = normal_ws(static_cast<char*>(ws), n, mp, ctx->nbo, ctx->nbi);
+  const NormalWs w = normal_ws(static_cast<char*>(ws), n, mp, ctx);
   if (ws_bytes < w.total) return fail(IPMZ_ERR_INVALID, "workspace too small");
   HIP_OK(hipSetDevice(ctx->device));
   int rc = normal_factor_impl(ctx, n, mp, K, ld, D, w, nullptr);
@@ -429,7 +440,7 @@ int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld,
   if (!ctx || n <= 0 || mp < 0 || !K || !D || !ws || !b || ld < n + mp)
     return fail(IPMZ_ERR_INVALID, "ipmz_normal_solve: bad arguments");
   HIP_OK(hipSetDevice(ctx->device));
-  return normal_solve_impl(ctx, n, mp, K, ld, D, normal_ws(static_cast<char*>(ws), n, mp, ctx->nbo, ctx->nbi), b);
+  return normal_solve_impl(ctx, n, mp, K, ld, D, normal_ws(static_cast<char*>(ws), n, mp, ctx), b);
 }
 
 // Bunch-Kaufman (f3) ----------------------------------------------------------
@@ -511,7 +522,7 @@ int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, do
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
   const int64_t ld = round_up(N, 64);
-  const int64_t wsb = ws_layout(N, ctx->nbo, ctx->nbi).total;
+  const int64_t wsb = ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
   double *dK = nullptr, *dD = nullptr;
   char* ws = nullptr;
   HIP_OK(hipMalloc(&dK, (size_t)(ld * N * 8)));
@@ -553,7 +564,7 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
   if (!L || !D || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
   HIP_OK(hipSetDevice(ctx->device));
   const int64_t ld = round_up(N, 64);
-  const int64_t wsb = ws_layout(N, ctx->nbo, ctx->nbi).total;
+  const int64_t wsb = ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
   double *dL = nullptr, *dD = nullptr, *db = nullptr;
   char* ws = nullptr;
   bool ok = hipMalloc(&dL, (size_t)(ld * N * 8)) == hipSuccess && hipMalloc(&dD, (size_t)N * 8) == hipSuccess &&
@@ -664,13 +675,13 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
     HIP_OK(bk_solve(s->K, s->ldk, s->N, s->ipiv, q0(s).b, s->B, s->sK, s->sP, s->sb, st));
   } else if (s->normal) {
     return normal_solve_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
-                             normal_ws(s->nws, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi), q0(s).b);
+                             normal_ws(s->nws, s->n, s->m + s->p, s->ctx), q0(s).b);
   } else if (s->mixed) {
     HIP_OK(mixed_solve(s->K, s->ldk, s->mw, q0(s).b, s->ir_tol, s->ir_max, st));
     HIP_OK(hipMemcpyAsync(q0(s).scal + IPMZ_SC_IR_RATIO_AFF + 2 * which, s->mw.stat, 2 * sizeof(double),
                           hipMemcpyDeviceToDevice, st));
   } else if (s->B == 1) {
-    HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, s->ctx->nbo, s->ctx->nbi, q0(s).b, st));
+    HIP_OK(solve_ws(s->K, s->ldk, s->N, s->D, s->ws, nbo_for(s->ctx, s->N), s->ctx->nbi, q0(s).b, st));
   } else {
     HIP_OK(ldlt_solve_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->ctx->nbi, q0(s).b, s->B, s->sK, s->sD, s->sL,
                               s->sb, st));
@@ -686,7 +697,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt) {
   if (s->mixed) return mixed_factor_impl(s->ctx, s->K, s->ldk, s->mw, tt);
   if (s->normal)
     return normal_factor_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
-                              normal_ws(s->nws, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi), tt);
+                              normal_ws(s->nws, s->n, s->m + s->p, s->ctx), tt);
   if (s->B == 1) return factor_impl(s->ctx, s->N, s->K, s->ldk, s->D, s->ws, tt);
   BatchStrides bs;
   bs.B = s->B;
@@ -695,7 +706,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt) {
   bs.sL = s->sL;
   bs.sW = s->sW;
   HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
-  HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, s->ctx->nbo, s->ctx->nbi, s->binfo,
+  HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
                              s->ctx->stream, bs));
   return IPMZ_OK;
 }
@@ -825,7 +836,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   bool ok = Q && A && C && c && lx && ux && Qx && ATl && CTl && lA && uA && Ax && d && Cx && v && r && da && di &&
             v0 && r0 && bvec && scal && scal0 && part && tpart && s->K && s->D;
   if (ok && B == 1) {
-    s->ws_bytes = ws_layout(N, ctx->nbo, ctx->nbi).total;
+    s->ws_bytes = ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
     void* w = nullptr;
     ok = hipMalloc(&w, (size_t)s->ws_bytes) == hipSuccess;
     if (ok) s->allocs.push_back(w);
@@ -833,7 +844,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   } else if (ok) {
     const int64_t nblk = (N + ctx->nbi - 1) / ctx->nbi;
     s->bLinv = dev_array(s, nblk * ctx->nbi * ctx->nbi, &s->sL);
-    s->bW = dev_array(s, (int64_t)N * ctx->nbo, &s->sW);
+    s->bW = dev_array(s, (int64_t)N * nbo_for(ctx, N), &s->sW);
     void* w = nullptr;
     ok = s->bLinv && s->bW && hipMalloc(&w, 256) == hipSuccess;
     if (ok) s->allocs.push_back(w);
@@ -1138,12 +1149,12 @@ int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refi
                                   "Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (enable && !s->mws) {
-    const int64_t bytes = mixed_ws_bytes(s->N, s->ctx->nbo);
+    const int64_t bytes = mixed_ws_bytes(s->N, nbo_for(s->ctx, s->N));
     void* w = nullptr;
     if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
     s->allocs.push_back(w);
     s->mws = static_cast<char*>(w);
-    mixed_ws_carve(s->mws, s->N, s->ctx->nbo, s->mw);
+    mixed_ws_carve(s->mws, s->N, nbo_for(s->ctx, s->N), s->mw);
   }
   s->mixed = enable != 0;
   s->ir_tol = tol;
@@ -1165,7 +1176,7 @@ int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
     return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision, Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (reduction == IPMZ_REDUCTION_NORMAL && !s->nws) {
-    const int64_t bytes = normal_ws(nullptr, s->n, s->m + s->p, s->ctx->nbo, s->ctx->nbi).total;
+    const int64_t bytes = normal_ws(nullptr, s->n, s->m + s->p, s->ctx).total;
     void* w = nullptr;
     if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
     s->allocs.push_back(w);

@@ -165,8 +165,8 @@ class Context:
         self.device = device
         if stream is not None:
             self.set_stream(stream)
-        if nbo or nbi:
-            self.set_blocking(nbo or 256, nbi or 128)
+        if nbo or nbi:  # nbo 0 / None: by matrix order (libipmz's default)
+            self.set_blocking(nbo or 0, nbi or 64)
 
     def set_stream(self, stream):
         """Enqueue on an external HIP stream handle (0 = the null stream,
