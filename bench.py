@@ -233,7 +233,7 @@ def main():
         }
         traffic = None
         tpath = os.path.join(REPO, "profiles", "pmc_traffic.json")
-        if os.path.exists(tpath) and not mixed and not nbatch:  # HBM bytes per trailing launch, committed PMC passes (fp64 C3 kernel)
+        if os.path.exists(tpath) and args.workload == "c3":  # HBM bytes per trailing launch, committed PMC passes of C3
             with open(tpath) as f:
                 traffic = json.load(f)
             traffic["source"] = os.path.relpath(tpath, REPO) + " (" + traffic.get("profile", "") + ")"
@@ -246,7 +246,20 @@ def main():
             launches = ph["trailing_launches"]
             achieved = ph["trailing_flops"] / tr_s / 1e12 if tr_s > 0 else 0.0
             peak = FP32_MFMA_PEAK_TFLOPS if mixed else FP64_MFMA_PEAK_TFLOPS
-        if ph and nbatch:
+        if ph and not nbatch and ph["trailing_launches"] == 0:
+            # no trailing update reaches the 128 x 128 kernel (C2: orders 2048
+            # and 512): the whole factor phase against the fp64 MFMA peak
+            if wl.get("normal"):
+                fl = n ** 3 / 3.0 + n * n * (m + p) + n * (m + p) ** 2 + (m + p) ** 3 / 3.0
+                what = "normal-equations factor phase: LDL^T(H) + TRSM + SYRK + LDL^T(S)"
+            else:
+                fl = Nk ** 3 / 3.0
+                what = "LDL^T factor phase"
+            ach = fl / (factor_ms * 1e-3) / 1e12
+            out["roofline"] = {"bound": "mfma", "kernel": what, "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                               "frac": ach / peak, "traffic": None,
+                               "note": "algorithmic flops over the factor phase time (HIP events)"}
+        elif ph and nbatch:
             # batched factor: every launch serves the whole shard; the bound at
             # N = 320 is latency, priced here against the fp64 MFMA peak
             out["roofline"] = {"bound": "mfma", "kernel": "ldlt_small_kernel (whole LDL^T of each QP in one 8-wave workgroup, fp64 MFMA)",

@@ -14,6 +14,7 @@ R per launch is recovered from the grid size (triangular grid of 128 x 128
 tiles, 512 threads per workgroup).
 
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write <profile label> > profiles/pmc_traffic.json
+(IPMZ_PMC_NBO: the outer panel width of the profiled run, default 384 = C3's)
 """
 import csv
 import json
@@ -21,7 +22,7 @@ import math
 import sys
 
 KERNEL = "gemm_nt_kernel<double, 128, 128, 0, 2, 4, 6>"
-NBO = 256
+NBO = int(__import__("os").environ.get("IPMZ_PMC_NBO", 384))  # the bench's outer panel width (C3: 384)
 
 
 def rows(d):
@@ -55,6 +56,7 @@ def main():
         "algorithmic_bytes_per_launch": tot_alg / n,
         "traffic_over_algorithmic": per / (tot_alg / n),
         "profile": sys.argv[3] if len(sys.argv) > 3 else "",
+        "nbo": NBO,
         "note": "FETCH_SIZE x2 (gfx950 correction) + WRITE_SIZE, KiB->B; one bench.py step, "
                 "separate --pmc passes; algorithmic = C lower triangle read+write + W, L panels",
     }
