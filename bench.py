@@ -269,8 +269,9 @@ def main():
         elif ph:
             out["roofline"] = {
                 "bound": "mfma",
-                "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB> (trailing update "
-                           f"A22 -= W21 L21^T, {'fp32' if mixed else 'fp64'} MFMA)"),
+                "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB,"
+                           f"{'2,4' if mixed else '4,4'}> (trailing update A22 -= W21 L21^T, "
+                           f"{'fp32' if mixed else 'fp64'} MFMA)"),
                 "achieved": achieved,
                 "peak": peak,
                 "unit": "TFLOP/s",

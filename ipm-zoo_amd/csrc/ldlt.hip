@@ -586,6 +586,8 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 9: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2>(g, st);
     case 10: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_GRP>(g, st);  // (these two spill one VGPR)
     case 14: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st);
+    case 15: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st);
+    case 16: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_GRP>(g, st);
     case 23: return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st);
     default: break;
   }
@@ -595,6 +597,9 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 20: return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st);
     case 21: return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st);
     case 22: return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st);
+    case 24: return launch_gemm<128, 128, EPI_SUB_STRIP, 4, 4, OPT_NOR2>(g, st);
+    case 25: return launch_gemm<64, 128, EPI_SUB_STRIP, 4, 4, OPT_NOR2>(g, st);
+    case 26: return launch_gemm<64, 64, EPI_SUB_STRIP, 4, 4, OPT_NOR2>(g, st);
     default: return hipErrorInvalidValue;
   }
 }
@@ -736,9 +741,16 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // the trailing updates of the last panels, all latency-bound -- take
   // 64-wide tiles: 4x the workgroups, a quarter of the work per k-chunk
   // (kbench rank 256: strip M = 4096 46 -> 24 us, trailing R = 1536 51 -> 34 us)
-  if (square_lower)
-    return M <= IPMZ_TRAIL_SMALL_M ? launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch)
-                     : launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
+  // fp64 trailing update: 16 waves as 4 x 4 (32 x 32 per wave, 64 VGPRs,
+  // two workgroups = 32 waves per CU): 56.6 vs 55.2 TFLOP/s alone (kbench
+  // gvar, R = 10880, rank 384), 40.8 vs 38.9 in situ, C3 60.6 -> 61.8
+  // steps/s; the fp32 factor (C5) keeps 2 x 4 (71 vs 67 TFLOP/s in situ)
+  if (square_lower) {
+    if (M <= IPMZ_TRAIL_SMALL_M) return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch);
+    if constexpr (std::is_same<T, double>::value)
+      return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
+    return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
+  }
   if (M <= 4096) return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st, batch);
   if (M <= 8192) return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);
   return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st, batch);

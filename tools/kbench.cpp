@@ -118,6 +118,35 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (argc > 3 && std::string(argv[2]) == "gvar") {  // trailing-GEMM variants: kbench N gvar v1 v2 ...
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+    for (int a = 3; a < argc; ++a) {
+      const int var = std::atoi(argv[a]);
+      if (var >= 20) {  // strip: M rows x 384 columns, rank 384
+        for (int M : {3072, 6144, 8192, 10496}) {
+          CK(ipmz::gemm_nt_sub_variant(var, M, 384, 384, W, 384, K, ld, K + 384 * ld + 384, ld, st));
+          t.start(st);
+          for (int r = 0; r < 10; ++r)
+            CK(ipmz::gemm_nt_sub_variant(var, M, 384, 384, W, 384, K, ld, K + 384 * ld + 384, ld, st));
+          const float us = t.stop(st) / 10 * 1e3;
+          std::printf("gvar %2d strip M=%5d x 384 rank=384: %.1f us %.2f TFLOP/s\n", var, M, us,
+                      2.0 * M * 384 * 384 / us / 1e6);
+        }
+        continue;
+      }
+      for (int rank : {256, 384})
+        for (int R : {5632, N - rank}) {
+          CK(ipmz::gemm_nt_sub_variant(var, R, R, rank, W, rank, K, ld, K + (int64_t)rank * ld + rank, ld, st));
+          t.start(st);
+          for (int r = 0; r < 5; ++r)
+            CK(ipmz::gemm_nt_sub_variant(var, R, R, rank, W, rank, K, ld, K + (int64_t)rank * ld + rank, ld, st));
+          const float ms = t.stop(st) / 5;
+          std::printf("gvar %2d R=%5d rank=%d: %.3f ms %.2f TFLOP/s\n", var, R, rank, ms,
+                      (double)R * (R + 1) * rank / ms / 1e9);
+        }
+    }
+    return 0;
+  }
   if (argc > 2 && std::string(argv[2]) == "gemm") {  // trailing GEMM alone (PMC passes)
     hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
     const int R = N - 256;

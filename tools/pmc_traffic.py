@@ -21,7 +21,7 @@ import json
 import math
 import sys
 
-KERNEL = "gemm_nt_kernel<double, 128, 128, 0, 2, 4, 6>"
+KERNEL = "gemm_nt_kernel<double, 128, 128, 0, 4, 4, 6>"
 NBO = int(__import__("os").environ.get("IPMZ_PMC_NBO", 384))  # the bench's outer panel width (C3: 384)
 
 
