@@ -11,7 +11,7 @@ Algorithmic bytes of one trailing launch (rank-nbo update of an R x R lower
 triangle): C read + written once, W and L panels read once:
     16 * R (R + 1) / 2 + 2 * 8 * R * nbo
 R per launch is recovered from the grid size (triangular grid of 128 x 128
-tiles, 512 threads per workgroup).
+tiles; grid / workgroup size).
 
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write <profile label> > profiles/pmc_traffic.json
 (IPMZ_PMC_NBO: the outer panel width of the profiled run, default 384 = C3's)
@@ -39,7 +39,7 @@ def main():
     assert len(fr) == len(wr)
     tot_f = tot_w = tot_alg = 0.0
     for a, b in zip(fr, wr):
-        wgs = int(a["Grid_Size"]) // 512
+        wgs = int(a["Grid_Size"]) // int(a["Workgroup_Size"])
         t = int((math.isqrt(8 * wgs + 1) - 1) // 2)  # tiles per side
         R = t * 128  # tile-rounded trailing order (upper bound of R)
         tot_f += 2.0 * float(a["Counter_Value"]) * 1024
