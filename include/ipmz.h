@@ -99,6 +99,13 @@ int ipmz_ctx_set_stream(ipmz_ctx* ctx, void* hip_stream);
 int ipmz_ctx_reset_stream(ipmz_ctx* ctx);
 int ipmz_ctx_sync(ipmz_ctx* ctx);
 const char* ipmz_last_error(void);
+/* Test hook: while bit 1 (solve) / bit 2 (outer-panel factor) is set, the
+ * persistent kernels launched drop their first cross-workgroup hand-off, so
+ * their consumers hit the 0.5 s spin limit -- the path by which a stuck
+ * hand-off surfaces as IPMZ_ERR_HIP from ipmz_ldlt_factor, ipmz_ctx_sync,
+ * ipmz_qp_scalars, ipmz_qp_solve (sticky error words, cleared when a
+ * factorization starts).  0 (default) for normal operation. */
+int ipmz_debug_inject(int mask);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512;
  * 0 = by matrix order: 384 for N >= 8192 with nbi 64, else 256), inner
  * diagonal block nbi (64 or 128).  Defaults 0 / 64.  Workspace sizes depend

@@ -88,7 +88,11 @@ __global__ __launch_bounds__(BKT) void k_bk_factor(double* __restrict__ Ab, int6
   const double alpha = 0x1.47e0f66afed07p-1;  // (1 + sqrt(17)) / 8, LinearSolvers.cpp:82
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto a = [&](int i, int j) -> double& { return A[(int64_t)i * ld + j]; };
-  int info = 0;
+  // ref_info: the reference's own info word, 0-based (LinearSolvers.cpp:113-116
+  // sets info = k), which also decides kp -- a first zero column at k = 0
+  // leaves it 0, so the NEXT zero column again takes kp = k.  info: the
+  // 1-based first zero column this kernel reports (0 = none).
+  int info = 0, ref_info = 0;
   for (int k = 0; k < n;) {
     // ---- pivot search (LinearSolvers.cpp:98-136)
     double cmax = 0.0;
@@ -110,8 +114,9 @@ __global__ __launch_bounds__(BKT) void k_bk_factor(double* __restrict__ Ab, int6
     bool zero_col = false;
     if (akk == 0.0 && cmax == 0.0) {
       zero_col = true;
-      if (info == 0) {
-        info = k + 1;
+      if (info == 0) info = k + 1;
+      if (ref_info == 0) {
+        ref_info = k;
         kp = k;
       } else if (fix_kp) {
         kp = k;

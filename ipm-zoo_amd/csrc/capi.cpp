@@ -34,6 +34,7 @@ int fail(int code, const std::string& msg) {
   } while (0)
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
+int ws_status(hipStream_t st, const char* ws, int N, int nbo, int nbi, const char* what);
 
 }  // namespace
 
@@ -46,7 +47,10 @@ struct ipmz_ctx {
   // updates on sB; forked from / joined to `stream` with events
   hipStream_t sA = nullptr, sB = nullptr;
   std::vector<hipEvent_t> evpool;
-  bool lookahead = true;
+  // the last workspace a device-memory factor / solve used: ipmz_ctx_sync
+  // checks its sticky error words (spin timeouts of the persistent kernels)
+  const char* check_ws = nullptr;
+  int check_N = 0;
 };
 
 // outer panel width for an order-N factor: the context's, or by size --
@@ -104,8 +108,6 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
     ipmz_ctx_destroy(c);
     return fail(IPMZ_ERR_HIP, "hipStreamCreateWithPriority failed");
   }
-  const char* la = std::getenv("IPMZ_LOOKAHEAD");
-  c->lookahead = !(la && la[0] == '0');
   *out = c;
   return IPMZ_OK;
 }
@@ -139,6 +141,16 @@ int ipmz_ctx_reset_stream(ipmz_ctx* ctx) {
 int ipmz_ctx_sync(ipmz_ctx* ctx) {
   if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
   HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (ctx->check_ws) {
+    const char* ws = ctx->check_ws;
+    ctx->check_ws = nullptr;
+    return ws_status(ctx->stream, ws, ctx->check_N, nbo_for(ctx, ctx->check_N), ctx->nbi, "ipmz_ctx_sync");
+  }
+  return IPMZ_OK;
+}
+
+int ipmz_debug_inject(int mask) {
+  set_debug_inject_mask(mask);
   return IPMZ_OK;
 }
 
@@ -152,11 +164,11 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
 }
 
 // ---------------------------------------------------------------------------
-// Workspace: [info int (256 B)] [panel ctrl words] [side 2*nbi] [Linv nblk*nbi^2] [W N*nbo]
-//            [ybuf N] [zbuf N] [sbuf N] [tbuf N] [ctrl 2 + 2*nblk64 uint]
+// Workspace: [info int (256 B)] [panel ctrl words] [side 2*nbi] [Linv nblk*nbi^2] [W 3*N*nbo]
+//            [ybuf N] [zbuf N] [ctrl: ticket, sticky error]
 namespace {
 struct WsLayout {
-  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, s_off, t_off, ctrl_off, total;
+  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
 };
 WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
@@ -168,38 +180,37 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
   l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)
   l.z_off = l.y_off + round_up((int64_t)N * 8, 256);
-  l.s_off = l.z_off + round_up((int64_t)N * 8, 256);
-  l.t_off = l.s_off + round_up((int64_t)N * 8, 256);
-  l.ctrl_off = l.t_off + round_up((int64_t)N * 8, 256);
-  l.total = l.ctrl_off + round_up((2 + 2 * ((int64_t)N + 63) / 64) * 4, 256);
+  l.ctrl_off = l.z_off + round_up((int64_t)N * 8, 256);
+  l.total = l.ctrl_off + 256;
   return l;
 }
-bool use_persistent_solve(int nbi) {
-  static const char* env = std::getenv("IPMZ_SOLVE");
-  return nbi == 64 && !(env && std::strcmp(env, "blocked") == 0);
-}
-// the solve (persistent single launch for nbi == 64, else block-step chain)
+// the solve: one persistent launch for nbi == 64 (trsv_persist.hip), else
+// the block-step kernel chain (trsv.hip)
 hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const char* ws, int nbo, int nbi, double* b,
                     hipStream_t st) {
   const WsLayout l = ws_layout(N, nbo, nbi);
   char* w = const_cast<char*>(ws);
   const double* Linv = reinterpret_cast<const double*>(w + l.linv_off);
-  // IPMZ_SOLVE=chain: one chain workgroup + helpers (trsv_chain.hip) --
-  // correct, but 1.3 ms per C3 solve against the dequeued solve's 0.82 ms
-  // (helpers and register spills bound it); not the default
-  static const bool chain = [] {
-    const char* e = std::getenv("IPMZ_SOLVE");
-    return e && !std::strcmp(e, "chain");
-  }();
-  if (chain && nbi == 64)
-    return ldlt_solve_chain(K, ld, N, D, Linv, b, reinterpret_cast<double*>(w + l.y_off),
-                            reinterpret_cast<double*>(w + l.s_off), reinterpret_cast<double*>(w + l.z_off),
-                            reinterpret_cast<double*>(w + l.t_off), reinterpret_cast<unsigned*>(w + l.ctrl_off), st);
-  if (use_persistent_solve(nbi))
+  if (nbi == 64)
     return ldlt_solve_persistent(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.y_off),
                                  reinterpret_cast<double*>(w + l.z_off), reinterpret_cast<unsigned*>(w + l.ctrl_off),
                                  st);
   return ldlt_solve(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.side_off), st);
+}
+// Sticky error words of a workspace (synchronizes): a spin that timed out in
+// the outer-panel factor or the persistent solve (sync.h, 0.5 s) means the
+// results are invalid -- reported as IPMZ_ERR_HIP, never as success.
+int ws_status(hipStream_t st, const char* ws, int N, int nbo, int nbi, const char* what) {
+  const WsLayout l = ws_layout(N, nbo, nbi);
+  unsigned pe = 0, se = 0;
+  HIP_OK(hipMemcpyAsync(&pe, ws + l.pctrl_off + 4 * PANEL_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&se, ws + l.ctrl_off + 4 * SOLVE_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipStreamSynchronize(st));
+  if (pe) return fail(IPMZ_ERR_HIP, std::string(what) + ": a hand-off inside the outer-panel factor kernel timed out "
+                                                        "(spin limit 0.5 s); the factor is invalid");
+  if (se) return fail(IPMZ_ERR_HIP, std::string(what) + ": a hand-off inside the persistent triangular solve timed out "
+                                                        "(spin limit 0.5 s); the solution is invalid");
+  return IPMZ_OK;
 }
 }  // namespace
 
@@ -216,9 +227,10 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
   HIP_OK(hipMemsetAsync(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), ctx->stream));
+  HIP_OK(hipMemsetAsync(ws + l.ctrl_off, 0, 2 * sizeof(unsigned), ctx->stream));  // solve: ticket + sticky error
   const int nbo = nbo_for(ctx, N);
   const int npan = (N + nbo - 1) / nbo;
-  if (!ctx->lookahead || npan < 3) {
+  if (npan < 3) {
     HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, 0,
                        pctrl));
     return IPMZ_OK;
@@ -238,7 +250,10 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   return IPMZ_OK;
 }
 
-static int read_info(ipmz_ctx* ctx, const char* ws) {
+// info word (first non-finite pivot) + the sticky error words of ws
+static int read_info(ipmz_ctx* ctx, const char* ws, int N) {
+  int rc = ws_status(ctx->stream, ws, N, nbo_for(ctx, N), ctx->nbi, "ipmz_ldlt_factor");
+  if (rc) return rc;
   int info = 0;
   HIP_OK(hipMemcpyAsync(&info, ws, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
@@ -253,7 +268,9 @@ int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, voi
   HIP_OK(hipSetDevice(ctx->device));
   int rc = factor_impl(ctx, N, K, ld, D, static_cast<char*>(ws), nullptr);
   if (rc) return rc;
-  return read_info(ctx, static_cast<char*>(ws));
+  ctx->check_ws = static_cast<const char*>(ws);
+  ctx->check_N = N;
+  return read_info(ctx, static_cast<char*>(ws), N);
 }
 
 int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b) {
@@ -261,6 +278,8 @@ int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const dou
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
   HIP_OK(solve_ws(K, ld, N, D, static_cast<const char*>(ws), nbo_for(ctx, N), ctx->nbi, b, ctx->stream));
+  ctx->check_ws = static_cast<const char*>(ws);  // its error word is checked by ipmz_ctx_sync
+  ctx->check_N = N;
   return IPMZ_OK;
 }
 
@@ -281,7 +300,7 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
 // factor of S K S in fp32, with the same two-stream look-ahead as the fp64 factor
 static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs& w, TrailTimer* timer) {
   const int npan = (w.N + w.nbo - 1) / w.nbo;
-  if (!ctx->lookahead || npan < 3) {
+  if (npan < 3) {
     HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, 0, timer));
     return IPMZ_OK;
   }
@@ -429,9 +448,9 @@ int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, doub
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (info != 0x7f7f7f7f) return info;
   // non-finite pivots of the two LDL^T factors (their own info words)
-  const int ih = read_info(ctx, w.wsH);
+  const int ih = read_info(ctx, w.wsH, n);
   if (ih) return ih;
-  const int is = mp ? read_info(ctx, w.wsS) : 0;
+  const int is = mp ? read_info(ctx, w.wsS, mp) : 0;
   return is > 0 ? n + is : is;
 }
 
@@ -538,7 +557,7 @@ int ipmz_ldlt_decomposition(ipmz_ctx* ctx, int N, const double* A, double* L, do
   if (!rc) rc = factor_impl(ctx, N, dK, ld, dD, ws, nullptr);
   int info = 0;
   if (!rc) {
-    info = read_info(ctx, ws);
+    info = read_info(ctx, ws, N);
     if (info < 0) rc = info;
   }
   if (!rc) {
@@ -989,13 +1008,38 @@ int step_impl(ipmz_qp* s, int flags) {
   return IPMZ_OK;
 }
 
+// sticky error words of every persistent-kernel workspace the step uses
+int qp_status(ipmz_qp* s) {
+  hipStream_t st = s->ctx->stream;
+  if (s->mixed) {
+    unsigned e[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(&e[0], s->mw.pctrl + PANEL_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipMemcpyAsync(&e[1], s->mw.ctrl + SOLVE_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (e[0] || e[1]) return fail(IPMZ_ERR_HIP, "Newton step: a hand-off inside a persistent kernel of the "
+                                                 "mixed-precision factor / solve timed out; the step is invalid");
+    return IPMZ_OK;
+  }
+  if (s->normal) {
+    const NormalWs w = normal_ws(s->nws, s->n, s->m + s->p, s->ctx);
+    int rc = ws_status(st, w.wsH, s->n, nbo_for(s->ctx, s->n), s->ctx->nbi, "Newton step (normal equations, H)");
+    if (!rc && s->m + s->p)
+      rc = ws_status(st, w.wsS, s->m + s->p, nbo_for(s->ctx, s->m + s->p), s->ctx->nbi,
+                     "Newton step (normal equations, S)");
+    return rc;
+  }
+  if (s->B == 1 && !s->eqnone) return ws_status(st, s->ws, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step");
+  return IPMZ_OK;  // batched / Bunch-Kaufman kernels have no cross-workgroup spins
+}
+
 int scalars_impl(ipmz_qp* s, double* out, int count) {
   HIP_OK(hipSetDevice(s->ctx->device));
-  for (int i = 0; i < count; ++i)
-    HIP_OK(hipMemcpyAsync(out + (int64_t)i * SC_COUNT, s->hq[i].scal, SC_COUNT * 8, hipMemcpyDeviceToHost,
+  // the B scalar blocks are one allocation with a stride: one 2-D copy
+  const size_t pitch = (s->B > 1 ? (s->hq[1].scal - s->hq[0].scal) : SC_COUNT) * 8;
+  HIP_OK(hipMemcpy2DAsync(out, SC_COUNT * 8, s->hq[0].scal, pitch, SC_COUNT * 8, count, hipMemcpyDeviceToHost,
                           s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
-  return IPMZ_OK;
+  return s->loaded ? qp_status(s) : IPMZ_OK;
 }
 
 int get_state_impl(ipmz_qp* s, int i, int which, double* out) {

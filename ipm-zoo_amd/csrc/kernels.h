@@ -8,6 +8,17 @@
 
 namespace ipmz {
 
+// Fault injection for the tests of the spin-timeout path (ipmz_debug_inject):
+// a persistent kernel launched while its bit is set drops its first
+// hand-off, so every consumer times out and raises the sticky error word.
+enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2 };
+int debug_inject_mask();
+void set_debug_inject_mask(int mask);
+// error words the persistent kernels raise on a spin timeout (sync.h): the
+// panel kernel's ctrl[PANEL_ERR_WORD], the solve's ctrl[1]
+constexpr int PANEL_ERR_WORD = 2;
+constexpr int SOLVE_ERR_WORD = 1;
+
 // ldlt.hip -------------------------------------------------------------------
 // Batched factorization: element strides between consecutive QPs' K, D,
 // L^{-1} blocks and W panels.
@@ -20,8 +31,6 @@ struct BatchStrides {
 #define IPMZ_SMALL_NMAX 1024
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs);
-hipError_t small_clock_probe(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
-                             hipStream_t st, const BatchStrides& bs, unsigned long long* out);
 hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                                int* info, hipStream_t st, const BatchStrides& bs);
 // In-place blocked LDL^T of the lower triangle of K (row-major, ld).
@@ -49,10 +58,6 @@ hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, do
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
                        hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
                        unsigned* pctrl = nullptr);
-// one fused diag + TRSM + strip launch for the inner block [j0, j0 + bi) of an
-// outer panel ending at column c1 (panel.hip); Wc = W + (j0 - k0), row-indexed
-hipError_t panel_step(double* K, int64_t ld, int N, int j0, int bi, int c1, double* D, double* Lb, double* Wc,
-                      int ldw, int* info, unsigned* ctrl, hipStream_t st);
 // the whole outer panel [k0, k0 + bo) in ONE launch (panel.hip): the nbo/64
 // inner blocks pipelined by flags instead of launch boundaries.  Lb0: L^{-1}
 // block of the panel's first inner block; Wp: the panel's W buffer (N x ldw)
@@ -60,14 +65,6 @@ hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, 
                        int* info, unsigned* ctrl, hipStream_t st);
 hipError_t outer_panel(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                        int* info, unsigned* ctrl, hipStream_t st);
-hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* A, int64_t lda, const double* B,
-                               int64_t ldb, double* C, int64_t ldc, hipStream_t st);
-hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,
-                            hipStream_t st);
-hipError_t diag_probe(double* K, int64_t ld, int k0, int nbi, double* D, double* Linv, int* info, hipStream_t st);
-hipError_t trsm_probe(double* K, int64_t ld, int N, int j0, double* D, const double* Linv, double* W, int nbo,
-                      hipStream_t st);
-hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
@@ -75,9 +72,6 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
 hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                          double* C, int64_t ldc, hipStream_t st);
 
-// trsv_chain.hip: one chain workgroup + helpers (4 N-vectors of scratch, ctrl: 2 words)
-hipError_t ldlt_solve_chain(const double* K, int64_t ld, int N, const double* D, const double* Linv, double* b,
-                            double* ybuf, double* sbuf, double* xbuf, double* tbuf, unsigned* ctrl, hipStream_t st);
 // trsv.hip -------------------------------------------------------------------
 // In-place b <- L^{-T} D^{-1} L^{-1} b; side: 2*nbi doubles of scratch.
 hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi, double* b,
@@ -88,7 +82,8 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
                               double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st);
 
 // trsv_persist.hip: the same solve as ONE persistent launch (nbi == 64);
-// ybuf, zbuf: N doubles; ctrl: 2 + 2*ceil(N/64) unsigned (zeroed inside).
+// ybuf, zbuf: N doubles; ctrl: 2 unsigned (ticket counter zeroed inside,
+// ctrl[1] a sticky error word the caller clears).
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
                                  double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st);
 // fp32 variant; skip (device flag, may be null): return at once when set

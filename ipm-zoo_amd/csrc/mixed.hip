@@ -211,7 +211,7 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   w.y32 = reinterpret_cast<float*>(take((int64_t)N * 4));
   w.z32 = reinterpret_cast<float*>(take((int64_t)N * 4));
   w.r32 = reinterpret_cast<float*>(take((int64_t)N * 4));
-  w.ctrl = reinterpret_cast<unsigned*>(take((2 + 2 * nblk) * 4));
+  w.ctrl = reinterpret_cast<unsigned*>(take(2 * 4));
   w.state = reinterpret_cast<unsigned*>(take(64));
   w.info = reinterpret_cast<int*>(take(64));
   w.pctrl = reinterpret_cast<unsigned*>(take(IPMZ_PANEL_CTRL_WORDS * 4));
@@ -233,6 +233,7 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   hipError_t e = hipMemsetAsync(w.info, 0x7f, sizeof(int), st);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(w.pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(w.ctrl, 0, 2 * sizeof(unsigned), st)) != hipSuccess) return e;  // solve: counter + error
   return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, ev, nev, w.pctrl);
 }
 

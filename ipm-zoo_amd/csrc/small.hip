@@ -69,8 +69,6 @@ __device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc
 }
 }  // namespace
 
-__device__ unsigned long long g_small_clk[64];  // PROF: stage clocks of workgroup 0 (kbench)
-template <bool PROF>
 __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
                                                          double* __restrict__ D, double* __restrict__ Linv,
                                                          double* __restrict__ W, int* __restrict__ info, int64_t sK,
@@ -87,17 +85,10 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
   double* Bs = smem + 64 * DS;
   const int nblk = (N + 63) / 64;
   auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
-  int nclk = 0;
-  auto clk = [&]() {
-    if (PROF && blockIdx.x == 0 && threadIdx.x == 0 && nclk < 63) g_small_clk[nclk] = __builtin_amdgcn_s_memtime();
-    ++nclk;
-  };
-  clk();
   for (int J = 0; J < nblk; ++J) {
     const int J0 = 64 * J;
     diag64_body<false, false, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
                                                   smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
-    clk();
     if (J == nblk - 1) break;
     __syncthreads();  // diag64_body's LDS is free; its L, D, L^{-1} stores are visible to the workgroup
     // ---- TRSM of the chunks below (block J is full: J0 + 64 < N)
@@ -131,7 +122,6 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
       }
       __syncthreads();  // As / Bs reads done before the next tile is staged
     }
-    clk();
     // ---- trailing update of the lower triangle below block J, tile (c, q)
     // in row order (the next diagonal block first); L[c, J] staged once per
     // row of tiles
@@ -188,29 +178,15 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
       c = cn;
       q = qn;
     }
-    clk();
   }
-  if (PROF && blockIdx.x == 0 && threadIdx.x == 0) g_small_clk[63] = nclk;
 }
 
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs) {
   if (N <= 0 || bs.B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ldlt_small_kernel<false>, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD, bs.sL,
+  hipLaunchKernelGGL(ldlt_small_kernel, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD, bs.sL,
                      bs.sW);
   return hipGetLastError();
-}
-
-// stage clocks of workgroup 0 (s_memtime): [0] start, then per block J:
-// after diag, after TRSM, after the trailing update; [63] = count
-hipError_t small_clock_probe(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
-                             hipStream_t st, const BatchStrides& bs, unsigned long long* out) {
-  hipLaunchKernelGGL(ldlt_small_kernel<true>, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
-                     bs.sL, bs.sW);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return e;
-  return hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_small_clk), sizeof(unsigned long long) * 64, 0,
-                                  hipMemcpyDeviceToHost, st);
 }
 
 }  // namespace ipmz

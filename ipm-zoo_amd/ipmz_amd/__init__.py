@@ -45,7 +45,7 @@ EXPORTS = [
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
     "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
-    "ipmz_overwriting_solve_bunch_kaufman",
+    "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
@@ -133,6 +133,7 @@ def _load():
         "ipmz_bk_solve": ([_VP, _I, _VP, _I64, _VP, _VP], _I),
         "ipmz_symmetric_indefinite_factorization": ([_VP, _I, _P, _P, ctypes.POINTER(ctypes.c_int)], _I),
         "ipmz_overwriting_solve_bunch_kaufman": ([_VP, _I, _P, ctypes.POINTER(ctypes.c_int), _P], _I),
+        "ipmz_debug_inject": ([_I], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -180,6 +181,8 @@ class Context:
         _check(lib.ipmz_ctx_set_blocking(self.h, nbo, nbi), "ipmz_ctx_set_blocking")
 
     def sync(self):
+        """Synchronize; raises IpmzError when the last device-memory factor /
+        solve hit a hand-off timeout (its sticky error words)."""
         _check(lib.ipmz_ctx_sync(self.h), "ipmz_ctx_sync")
 
     def close(self):
@@ -238,6 +241,14 @@ class Context:
         return _check(lib.ipmz_normal_solve(self.h, n, mp, _VP(K_ptr), ld, _VP(D_ptr), _VP(ws_ptr), _VP(b_ptr)),
                       "ipmz_normal_solve")
 
+
+def debug_inject(mask):
+    """Test hook (ipmz_debug_inject): 1 = drop the persistent solve's first
+    hand-off, 2 = the outer-panel factor's; 0 = normal operation."""
+    _check(lib.ipmz_debug_inject(int(mask)), "ipmz_debug_inject")
+
+
+INJECT_SOLVE, INJECT_PANEL = 1, 2
 
 _default_ctx = None
 

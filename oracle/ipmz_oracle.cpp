@@ -298,6 +298,73 @@ void ldlt(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, doubl
   }
 }
 
+// The same factorization, bit for bit, reorganised for large N (the C3 / C5
+// parity tests run the oracle at N = 11264 / 8192 on the GPU box's host).
+// Every element's running sum S[j][i] = A[j][i] - sum_k (L[j][k] * L[i][k]) *
+// D[k] still subtracts its terms one at a time in increasing k with the same
+// operations -- only WHEN each (j, i, k) term is applied changes:
+//   for each block of nb columns [I0, I1):
+//     1. the diagonal block, exactly the loop above restricted to k in [I0, i);
+//     2. the rows below it (parallel over rows): k in [I0, i), then / D[i];
+//     3. the trailing triangle (parallel over rows): S[j][i] -= (L[j][k] *
+//        L[i][k]) * D[k] for k in [I0, I1) in order -- a right-looking update
+//        whose inner loop runs over i with an identical scalar expression per
+//        element (SSE2 lanes do the same IEEE operations; no contraction).
+// L's lower triangle holds the running sums until a column is final.
+// tests/test_oracle_golden.py pins it bitwise to ldlt() and to the reference.
+void ldlt_blocked(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, double* D) {
+  constexpr int64_t NB = 96;
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < n; ++j) {
+    for (int64_t i = 0; i <= j; ++i) L[j * ldl + i] = A[j * lda + i];
+    for (int64_t i = j + 1; i < n; ++i) L[j * ldl + i] = 0.0;
+  }
+  std::vector<double> Pt((size_t)(NB * n));  // Pt[kk][i] = L[i][I0 + kk]
+  for (int64_t I0 = 0; I0 < n; I0 += NB) {
+    const int64_t I1 = std::min(I0 + NB, n);
+    for (int64_t i = I0; i < I1; ++i) {  // 1. diagonal block
+      const double* Li = L + i * ldl;
+      double sum_d = Li[i];
+      for (int64_t k = I0; k < i; ++k) sum_d -= Li[k] * Li[k] * D[k];
+      D[i] = sum_d == 0.0 ? 1e-8 : sum_d;
+      for (int64_t j = i + 1; j < I1; ++j) {
+        double* Lj = L + j * ldl;
+        double sum = Lj[i];
+        for (int64_t k = I0; k < i; ++k) sum -= Lj[k] * Li[k] * D[k];
+        Lj[i] = sum / D[i];
+      }
+      L[i * ldl + i] = 1.0;
+    }
+    if (I1 >= n) break;
+#pragma omp parallel for schedule(static)
+    for (int64_t j = I1; j < n; ++j) {  // 2. the panel rows below the block
+      double* Lj = L + j * ldl;
+      for (int64_t i = I0; i < I1; ++i) {
+        const double* Li = L + i * ldl;
+        double sum = Lj[i];
+        for (int64_t k = I0; k < i; ++k) sum -= Lj[k] * Li[k] * D[k];
+        Lj[i] = sum / D[i];
+        Pt[(size_t)((i - I0) * n + j)] = Lj[i];
+      }
+    }
+    // 3. trailing triangle, rows in reverse so the long rows start first
+#pragma omp parallel for schedule(dynamic, 16)
+    for (int64_t jj = 0; jj < n - I1; ++jj) {
+      const int64_t j = n - 1 - jj;
+      double* Sj = L + j * ldl;
+      constexpr int64_t IC = 512;  // keep the row chunk in L1 across the k loop
+      for (int64_t c0 = I1; c0 <= j; c0 += IC) {
+        const int64_t c1 = std::min(c0 + IC, j + 1);
+        for (int64_t k = I0; k < I1; ++k) {
+          const double ljk = Sj[k], dk = D[k];
+          const double* P = Pt.data() + (size_t)((k - I0) * n);
+          for (int64_t i = c0; i < c1; ++i) Sj[i] -= ljk * P[i] * dk;
+        }
+      }
+    }
+  }
+}
+
 void solve_ldlt(int64_t n, const double* L, int64_t ldl, const double* D, double* b) {
   if (n == 0) return;
   for (int64_t i = 0; i < n; ++i) {  // std::inner_product from 0.0
@@ -353,6 +420,10 @@ namespace {
 // symmetric_indefinite_factorization + overwriting_solve_bunch_kaufman, with
 // the reference's kp = 0 behaviour (fix_kp = false).  L holds F, ipiv the
 // pivots, in that case.
+// bench.py's cpu_baseline times the reference's own loop order on one core;
+// the parity tests take the (bitwise identical) blocked, threaded form
+bool g_serial_ldlt = false;
+
 struct Factor {
   Vec L, Dd;
   std::vector<int64_t> ipiv;
@@ -392,7 +463,8 @@ int iterate(QP& q, double* rec, double* phase_s) {
   } else {
     F.L.assign((size_t)(N * N), 0.0);
     F.Dd.assign(N, 0.0);
-    ldlt(N, K.data(), N, F.L.data(), N, F.Dd.data());
+    if (g_serial_ldlt) ldlt(N, K.data(), N, F.L.data(), N, F.Dd.data());  // the reference's loop order
+    else ldlt_blocked(N, K.data(), N, F.L.data(), N, F.Dd.data());    // == ldlt() bit for bit
   }
   const auto t2 = std::chrono::steady_clock::now();
   if (phase_s) {
@@ -616,6 +688,10 @@ double ipmzo_u01(uint64_t seed, uint64_t tag, uint64_t i, uint64_t j) { return u
 
 void ipmzo_ldlt(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, double* D) {
   ldlt(n, A, lda, L, ldl, D);
+}
+void ipmzo_set_serial_ldlt(int serial) { g_serial_ldlt = serial != 0; }
+void ipmzo_ldlt_blocked(int64_t n, const double* A, int64_t lda, double* L, int64_t ldl, double* D) {
+  ldlt_blocked(n, A, lda, L, ldl, D);
 }
 void ipmzo_solve_ldlt(int64_t n, const double* L, int64_t ldl, const double* D, double* b) {
   solve_ldlt(n, L, ldl, D, b);

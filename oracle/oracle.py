@@ -66,6 +66,8 @@ def _load():
         getattr(lib, fn).argtypes = [ctypes.c_void_p]
     lib.ipmzo_gen_qp.argtypes = [_i64, _i64, _i64, _u64] + [_P] * 9
     lib.ipmzo_ldlt.argtypes = [_i64, _P, _i64, _P, _i64, _P]
+    lib.ipmzo_ldlt_blocked.argtypes = [_i64, _P, _i64, _P, _i64, _P]
+    lib.ipmzo_set_serial_ldlt.argtypes = [ctypes.c_int]
     lib.ipmzo_solve_ldlt.argtypes = [_i64, _P, _i64, _P, _P]
     lib.ipmzo_bk_factor.argtypes = [_i64, _P, _i64, ctypes.POINTER(ctypes.c_int64), ctypes.c_int]
     lib.ipmzo_bk_factor.restype = ctypes.c_int
@@ -109,6 +111,23 @@ def ldlt(K):
     D = np.zeros(N)
     lib().ipmzo_ldlt(N, _dp(K), N, _dp(L), N, _dp(D))
     return L, D
+
+
+def ldlt_blocked(K):
+    """The blocked, OpenMP-threaded form of the same factorization (bitwise
+    equal to ldlt(); what OracleQP uses unless set_serial_ldlt(True))."""
+    K = np.ascontiguousarray(K, dtype=np.float64)
+    N = K.shape[0]
+    L = np.zeros((N, N))
+    D = np.zeros(N)
+    lib().ipmzo_ldlt_blocked(N, _dp(K), N, _dp(L), N, _dp(D))
+    return L, D
+
+
+def set_serial_ldlt(serial):
+    """True: OracleQP factors with the reference's own loop order on one core
+    (bench.py's cpu_baseline); False (default): the blocked threaded form."""
+    lib().ipmzo_set_serial_ldlt(int(bool(serial)))
 
 
 def solve_ldlt(L, D, b):

@@ -17,6 +17,8 @@
 //   bk_rand <dir> <N> <seed> <zeros> <tag>
 //                                   the same pair on a dense indefinite K that
 //                                   forces interchanges and 2 x 2 pivots
+//   bk_zeros_at <dir> <N> <seed> <i,j,..> <tag>
+//                                   the same with zero rows/columns at i, j, ..
 //   newton <dir> <n> <m> <seed> <iters> <tag>
 //                                   SlackedSlacks (box [+ ineq]) Newton
 //                                   iterations through the reference's own
@@ -251,6 +253,49 @@ static int mode_bk(const std::string& dir, size_t N, uint64_t seed, const std::s
 // rows/columns (indices N/2, N/2 + 1, ...) are set to zero, which exercises
 // the zero-column branch (and, for a second zero column, the kp = 0 defect,
 // LinearSolvers.cpp:111-116).
+static int write_bk(const std::string& dir, const Mat& K, uint64_t seed, const std::string& tag);
+static Mat bk_dense(size_t N, uint64_t seed) {
+  Mat K(N, Vec(N, 0.0));
+  for (size_t i = 0; i < N; ++i) {
+    for (size_t j = 0; j < i; ++j) {
+      const double v = 2.0 * u01(seed, TAG_K, i, j) - 1.0;
+      K[i][j] = v;
+      K[j][i] = v;
+    }
+    K[i][i] = 0.05 * (2.0 * u01(seed, TAG_K, i, i) - 1.0);
+  }
+  return K;
+}
+// The same dense indefinite K with zero rows/columns at the listed indices
+// (comma-separated): a zero column 0 keeps the reference's 0-based info at 0
+// (LinearSolvers.cpp:113-116), so a later zero column again takes kp = k.
+static int mode_bk_zeros_at(const std::string& dir, size_t N, uint64_t seed, const std::string& list,
+                            const std::string& tag) {
+  Mat K = bk_dense(N, seed);
+  std::stringstream ss(list);
+  std::string item;
+  while (std::getline(ss, item, ',')) {
+    const size_t r = std::stoul(item);
+    for (size_t j = 0; j < N; ++j) K[r][j] = K[j][r] = 0.0;
+  }
+  return write_bk(dir, K, seed, tag);
+}
+static int write_bk(const std::string& dir, const Mat& K, uint64_t seed, const std::string& tag) {
+  const size_t N = K.size();
+  Vec b(N);
+  for (size_t i = 0; i < N; ++i) b[i] = 2.0 * u01(seed, TAG_B, i, 0) - 1.0;
+  auto [F, ipiv] = NO::LinearSolvers::symmetric_indefinite_factorization(K);
+  Vec x = b;
+  NO::LinearSolvers::overwriting_solve_bunch_kaufman(F, ipiv, x);
+  Vec piv(ipiv.begin(), ipiv.end());
+  write_bin(dir + "/" + tag + "_K.bin", flatten(K));
+  write_bin(dir + "/" + tag + "_F.bin", flatten(F));
+  write_bin(dir + "/" + tag + "_ipiv.bin", piv);
+  write_bin(dir + "/" + tag + "_b.bin", b);
+  write_bin(dir + "/" + tag + "_x.bin", x);
+  return 0;
+}
+
 static int mode_bk_rand(const std::string& dir, size_t N, uint64_t seed, size_t zeros, const std::string& tag) {
   Mat K(N, Vec(N, 0.0));
   for (size_t i = 0; i < N; ++i) {
@@ -465,6 +510,8 @@ int main(int argc, char** argv) {
     if (mode == "formulation") return mode_formulation(dir);
     if (mode == "ldlt" && argc == 6) return mode_ldlt(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk" && argc == 6) return mode_bk(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
+    if (mode == "bk_zeros_at" && argc == 7)
+      return mode_bk_zeros_at(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5], argv[6]);
     if (mode == "bk_rand" && argc == 7)
       return mode_bk_rand(dir, std::stoul(argv[3]), std::stoull(argv[4]), std::stoul(argv[5]), argv[6]);
     if (mode == "newton" && argc == 8)

@@ -37,6 +37,9 @@ CASES = [
     ("bk_rand", 64, 32, 0, "bkr64"),
     ("bk_rand", 200, 33, 0, "bkr200"),
     ("bk_rand", 16, 34, 2, "bkz16"),
+    # zero column 0 plus later zero columns: the reference's 0-based info stays
+    # 0 after column 0, so column 5 takes kp = 5 and column 9 the kp = 0 defect
+    ("bk_zeros_at", 16, 35, "0,5,9", "bkz0_16"),
     # C1: box-only SlackedSlacks, n=64, seed 1234, full solve trace
     ("newton", 64, 0, 1234, 100, "c1"),
     # C4-size QP: n=256, m=64 (N=320), seed 0, iterates 0-3

@@ -4,7 +4,9 @@ against the reference's golden vectors and the CPU oracle.
 The factor updates every element with the reference's own expression and
 operand order, so F and ipiv are compared BITWISE -- including the fixtures
 that force interchanges and 2x2 pivots (bkr*) and the one with two zero
-columns that trips the reference's kp = 0 defect (bkz16).  The solve's
+columns that trips the reference's kp = 0 defect (bkz16), and the one whose
+first zero column is column 0 (bkz0_16: the reference's 0-based info stays 0,
+LinearSolvers.cpp:113-116, so the next zero column still takes kp = k).  The solve's
 backward dot products are tree reductions: x within 1e-13 relative.
 """
 import numpy as np
@@ -24,7 +26,7 @@ def ctx():
 
 
 @pytest.mark.parametrize("N,tag", [(8, "bk8"), (64, "bk64"), (8, "bkr8"), (64, "bkr64"), (200, "bkr200"),
-                                   (16, "bkz16")])
+                                   (16, "bkz16"), (16, "bkz0_16")])
 def test_bk_golden(ctx, N, tag):
     K = load(f"{tag}_K.bin").reshape(N, N)
     F, ipiv = I.LinearSolvers.symmetric_indefinite_factorization(K, ctx)
@@ -75,3 +77,16 @@ def test_bk_device_fix_kp(ctx):
     _, po, info_o = oracle.bk_factor(K, fix_kp=True)
     assert info == info_o + 1
     assert np.array_equal(piv.cpu().numpy(), po.astype(np.int32))
+
+
+def test_bk_zero_column0_device_info(ctx):
+    # info = 1 + the first zero column (column 0 here), while ipiv follows the
+    # reference's 0-based bookkeeping bit for bit
+    N = 16
+    K = load("bkz0_16_K.bin").reshape(N, N)
+    A = torch.from_numpy(K.copy()).cuda()
+    piv = torch.zeros(N, dtype=torch.int32, device="cuda")
+    info = ctx.bk_factor(N, A.data_ptr(), N, piv.data_ptr(), fix_kp=False)
+    assert info == 1
+    assert np.array_equal(piv.cpu().numpy(), load("bkz0_16_ipiv.bin").astype(np.int32))
+    assert np.array_equal(A.cpu().numpy(), load("bkz0_16_F.bin").reshape(N, N))
