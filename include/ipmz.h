@@ -205,7 +205,9 @@ int ipmz_qp_load_host(ipmz_qp* qp, const double* Q, const double* c, const doubl
 int ipmz_qp_generate(ipmz_qp* qp, uint64_t seed);
 /* Enqueue one Newton step (asynchronous).  flags: */
 #define IPMZ_STEP_RESTART_IF_CONVERGED 1 /* reset a converged iterate to the initial one first */
-#define IPMZ_STEP_GRAPH 2                /* capture once into a hipGraph, then replay */
+#define IPMZ_STEP_GRAPH 2                /* capture once into a hipGraph, then replay (steps whose
+                                            factor forks onto the look-ahead streams -- >= 3 outer
+                                            panels -- are enqueued eagerly instead) */
 int ipmz_qp_step(ipmz_qp* qp, int flags);
 /* Synchronize and copy the IPMZ_SC_COUNT scalars to host memory. */
 int ipmz_qp_scalars(ipmz_qp* qp, double* out);
@@ -264,6 +266,13 @@ int ipmz_batch_set_state(ipmz_qp* qp, int index, const double* host_vars);
 /* Enqueue a device-to-device copy of all batch * IPMZ_SC_COUNT scalars
  * (QP-major) to dst (device): the input of the cross-GPU convergence summary. */
 int ipmz_batch_copy_scalars(ipmz_qp* qp, double* dst_device);
+/* Enqueue ONE kernel writing the batch's convergence summary to dst (device,
+ * 3 doubles): {max res, max mu, unconverged count} over its QPs -- the
+ * stopping rule of Optimizer.cpp:124-135 in MAX-reducible form, so a single
+ * all-reduce (MAX) across the ranks of a sharded batch decides the stop
+ * (reduced dst[2] == 0 <=> every QP of the job converged).  For the RCCL
+ * driver loop of ipmz_amd.dist.solve_sharded. */
+int ipmz_batch_summary(ipmz_qp* qp, double* dst_device);
 /* Step until every QP converged (converged QPs keep their iterate). */
 int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
 

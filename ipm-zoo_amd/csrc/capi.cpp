@@ -291,6 +291,9 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
   const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
   HIP_OK(linv_from_l(L, ld, N, ctx->nbi, reinterpret_cast<double*>(static_cast<char*>(ws) + l.linv_off),
                      ctx->stream));
+  // no factorization ran in this workspace: clear its sticky error words
+  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, IPMZ_PANEL_CTRL_WORDS * 4, ctx->stream));
+  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.ctrl_off, 0, 8, ctx->stream));
   return IPMZ_OK;
 }
 
@@ -857,7 +860,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   if (ok && B == 1) {
     s->ws_bytes = ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
     void* w = nullptr;
-    ok = hipMalloc(&w, (size_t)s->ws_bytes) == hipSuccess;
+    ok = hipMalloc(&w, (size_t)s->ws_bytes) == hipSuccess && hipMemset(w, 0, (size_t)s->ws_bytes) == hipSuccess;
     if (ok) s->allocs.push_back(w);
     s->ws = static_cast<char*>(w);
   } else if (ok) {
@@ -975,10 +978,22 @@ int load_one(ipmz_qp* s, int i, const double* Q, const double* c, const double* 
   return IPMZ_OK;
 }
 
+// Does the step's factorization fork onto the look-ahead streams?  Such a
+// step is enqueued eagerly even when IPMZ_STEP_GRAPH is asked for: capturing
+// the two-stream fork/join crashes inside hipGraph on ROCm 7.2 (segfault at
+// the first capture, N >= 3 outer panels), and a multi-millisecond step hides
+// its launch latency anyway.
+bool step_forks(const ipmz_qp* s) {
+  auto npan = [&](int N) { return (N + nbo_for(s->ctx, N) - 1) / nbo_for(s->ctx, N); };
+  if (s->eqnone || s->B > 1) return false;
+  if (s->normal) return npan(s->n) >= 3 || npan(s->m + s->p) >= 3;
+  return npan(s->N) >= 3;
+}
+
 int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
-  if (!(flags & IPMZ_STEP_GRAPH) || s->timing) return run_step(s, flags);
+  if (!(flags & IPMZ_STEP_GRAPH) || s->timing || step_forks(s)) return run_step(s, flags);
   hipStream_t st = s->ctx->stream;
   if (!s->gexec || s->graph_flags != flags) {
     if (s->gexec) hipGraphExecDestroy(s->gexec);
@@ -1197,6 +1212,7 @@ int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refi
     void* w = nullptr;
     if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
     s->allocs.push_back(w);
+    HIP_OK(hipMemset(w, 0, (size_t)bytes));  // sticky error words start clear
     s->mws = static_cast<char*>(w);
     mixed_ws_carve(s->mws, s->N, nbo_for(s->ctx, s->N), s->mw);
   }
@@ -1224,6 +1240,7 @@ int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
     void* w = nullptr;
     if (hipMalloc(&w, (size_t)bytes) != hipSuccess) return fail(IPMZ_ERR_NOMEM, "device allocation failed");
     s->allocs.push_back(w);
+    HIP_OK(hipMemset(w, 0, (size_t)bytes));  // sticky error words start clear
     s->nws = static_cast<char*>(w);
   }
   s->normal = reduction == IPMZ_REDUCTION_NORMAL;
@@ -1311,6 +1328,12 @@ int ipmz_batch_copy_scalars(ipmz_qp* s, double* dst) {
   // the B scalar blocks are one allocation with a stride of SC_COUNT doubles
   HIP_OK(hipMemcpy2DAsync(dst, SC_COUNT * 8, s->hq[0].scal, (s->B > 1 ? (s->hq[1].scal - s->hq[0].scal) : SC_COUNT) * 8,
                           SC_COUNT * 8, s->B, hipMemcpyDeviceToDevice, s->ctx->stream));
+  return IPMZ_OK;
+}
+int ipmz_batch_summary(ipmz_qp* s, double* dst) {
+  if (!s || !dst) return fail(IPMZ_ERR_INVALID, "null argument");
+  HIP_OK(hipSetDevice(s->ctx->device));
+  HIP_OK(qp_batch_summary(s->qb, dst, s->ctx->stream));
   return IPMZ_OK;
 }
 // Steps until every QP converged or max_iter; a converged QP keeps its

@@ -197,5 +197,7 @@ hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st);
 hipError_t qp_update(const QPBatch& qb, int freeze, hipStream_t st);
 hipError_t qp_restart_if_converged(const QPBatch& qb, hipStream_t st);
 hipError_t qp_save_initial(const QPBatch& qb, hipStream_t st);
+// out (device, 3 doubles) = {max res, max mu, unconverged count} over the batch
+hipError_t qp_batch_summary(const QPBatch& qb, double* out, hipStream_t st);
 
 }  // namespace ipmz

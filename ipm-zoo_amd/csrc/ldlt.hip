@@ -29,6 +29,7 @@
 namespace ipmz {
 
 static int g_inject = 0;
+
 int debug_inject_mask() { return g_inject; }
 void set_debug_inject_mask(int mask) { g_inject = mask; }
 

@@ -647,6 +647,39 @@ hipError_t qp_restart_if_converged(const QPBatch& qb, hipStream_t st) {
   return hipGetLastError();
 }
 
+// Convergence summary of a batch (the input of the cross-GPU all-reduce,
+// SURVEY.md §8e; the stopping rule res < 1e-8 and mu < 1e-8 of
+// Optimizer.cpp:124-135): out = {max res, max mu, unconverged count} -- all
+// three MAX-reducible, so ONE all-reduce (MAX) over the ranks decides the
+// stop: every QP of the job converged <=> the reduced out[2] == 0.
+__global__ __launch_bounds__(NT) void k_batch_summary(const QPDev* __restrict__ qs, int B, double* __restrict__ out) {
+  __shared__ double sh[3][NT];
+  double r = 0.0, m = 0.0, u = 0.0;
+  for (int b = threadIdx.x; b < B; b += NT) {
+    const double* sc = qs[b].scal;
+    r = fmax(r, sc[SC_RES]);
+    m = fmax(m, sc[SC_MU]);
+    u += sc[SC_CONVERGED] != 0.0 ? 0.0 : 1.0;
+  }
+  sh[0][threadIdx.x] = r;
+  sh[1][threadIdx.x] = m;
+  sh[2][threadIdx.x] = u;
+  __syncthreads();
+  for (int s = NT / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) {
+      sh[0][threadIdx.x] = fmax(sh[0][threadIdx.x], sh[0][threadIdx.x + s]);
+      sh[1][threadIdx.x] = fmax(sh[1][threadIdx.x], sh[1][threadIdx.x + s]);
+      sh[2][threadIdx.x] += sh[2][threadIdx.x + s];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) out[threadIdx.x] = sh[threadIdx.x][0];
+}
+hipError_t qp_batch_summary(const QPBatch& qb, double* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_batch_summary, dim3(1), dim3(NT), 0, st, qb.d, qb.B, out);
+  return hipGetLastError();
+}
+
 // snapshot of the initial iterate (restart source)
 __global__ void k_save_initial(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];

@@ -45,7 +45,7 @@ EXPORTS = [
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
     "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
-    "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject",
+    "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject", "ipmz_batch_summary",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
@@ -134,6 +134,7 @@ def _load():
         "ipmz_symmetric_indefinite_factorization": ([_VP, _I, _P, _P, ctypes.POINTER(ctypes.c_int)], _I),
         "ipmz_overwriting_solve_bunch_kaufman": ([_VP, _I, _P, ctypes.POINTER(ctypes.c_int), _P], _I),
         "ipmz_debug_inject": ([_I], _I),
+        "ipmz_batch_summary": ([_VP, _VP], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -486,6 +487,16 @@ class Batch(Optimizer):
     def copy_batch_scalars(self, dst_ptr):
         """Async device copy of all batch x SC_COUNT scalars (ctx stream)."""
         _check(lib.ipmz_batch_copy_scalars(self.h, _VP(dst_ptr)), "ipmz_batch_copy_scalars")
+
+    def summary(self, dst_ptr):
+        """Enqueue the convergence summary {max res, max mu, unconverged}
+        into 3 device doubles at dst_ptr (one kernel, ctx stream)."""
+        _check(lib.ipmz_batch_summary(self.h, _VP(dst_ptr)), "ipmz_batch_summary")
+
+    def summary_into(self, t):
+        """Device tensor t (>= 3 float64): the summary, enqueued on the ctx
+        stream (the stepper protocol of ipmz_amd.dist.solve_sharded)."""
+        self.summary(t.data_ptr())
 
     def batch_scalars(self):
         out = np.zeros(self.batch * SC_COUNT)

@@ -29,6 +29,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmc_fetch) step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_write) step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
+    trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;
+    counters) step counters 120 rocprofv3 -L ;;
     *) step "$s" 600 $s ;;
   esac
 done
