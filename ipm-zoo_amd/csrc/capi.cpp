@@ -43,9 +43,9 @@ struct ipmz_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   int nbo = 0, nbi = 64;  // nbo 0: by matrix order (nbo_for)
-  // factorization look-ahead: panel path on sA (high priority), trailing
-  // updates on sB; forked from / joined to `stream` with events
-  hipStream_t sA = nullptr, sB = nullptr;
+  // factorization look-ahead: panel chain on sA and panel rows on sC (high
+  // priority), trailing updates on sB; forked from / joined to `stream`
+  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr;
   std::vector<hipEvent_t> evpool;
   // the last workspace a device-memory factor / solve used: ipmz_ctx_sync
   // checks its sticky error words (spin timeouts of the persistent kernels)
@@ -104,7 +104,8 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
   int least = 0, greatest = 0;
   hipDeviceGetStreamPriorityRange(&least, &greatest);
   if (hipStreamCreateWithPriority(&c->sA, hipStreamNonBlocking, greatest) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->sC, hipStreamNonBlocking, greatest) != hipSuccess) {
     ipmz_ctx_destroy(c);
     return fail(IPMZ_ERR_HIP, "hipStreamCreateWithPriority failed");
   }
@@ -116,7 +117,7 @@ int ipmz_ctx_destroy(ipmz_ctx* ctx) {
   if (!ctx) return IPMZ_OK;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB})
+  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB, ctx->sC})
     if (s) {
       hipStreamSynchronize(s);
       hipStreamDestroy(s);
@@ -174,8 +175,8 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
   const int64_t nblk = (N + nbi - 1) / nbi;
   l.info_off = 0;
-  l.pctrl_off = 256;  // IPMZ_PANEL_CTRL_WORDS words
-  l.side_off = l.pctrl_off + round_up(IPMZ_PANEL_CTRL_WORDS * 4, 256);
+  l.pctrl_off = 256;  // panel_ctrl_words(N, nbo) words
+  l.side_off = l.pctrl_off + round_up(panel_ctrl_words(N, nbo) * 4, 256);
   l.linv_off = l.side_off + round_up(2 * nbi * 8, 256);
   l.w_off = l.linv_off + round_up(nblk * nbi * nbi * 8, 256);
   l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)
@@ -226,24 +227,26 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   double* W = reinterpret_cast<double*>(ws + l.w_off);
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
-  HIP_OK(hipMemsetAsync(pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), ctx->stream));
+  HIP_OK(hipMemsetAsync(pctrl, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * sizeof(unsigned), ctx->stream));
   HIP_OK(hipMemsetAsync(ws + l.ctrl_off, 0, 2 * sizeof(unsigned), ctx->stream));  // solve: ticket + sticky error
   const int nbo = nbo_for(ctx, N);
   const int npan = (N + nbo - 1) / nbo;
   if (npan < 3) {
-    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, 0,
+    HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, nullptr, 0,
                        pctrl));
     return IPMZ_OK;
   }
-  const int nev = 2 * npan + 4;
+  const int nev = 3 * npan + 4;
   int rc = ensure_events(ctx, (size_t)nev);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
-  // fork: A (panel path) and B (trailing updates) start after the caller's stream
+  // fork: A, C (panel path) and B (trailing updates) start after the caller's stream
   HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
   HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
   HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ev, nev - 2, pctrl));
+  HIP_OK(hipStreamWaitEvent(ctx->sC, ev[nev - 2], 0));
+  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
+                     pctrl));
   // join (A has already waited for B's tail)
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
@@ -292,7 +295,8 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
   HIP_OK(linv_from_l(L, ld, N, ctx->nbi, reinterpret_cast<double*>(static_cast<char*>(ws) + l.linv_off),
                      ctx->stream));
   // no factorization ran in this workspace: clear its sticky error words
-  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, IPMZ_PANEL_CTRL_WORDS * 4, ctx->stream));
+  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * 4,
+                        ctx->stream));
   HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.ctrl_off, 0, 8, ctx->stream));
   return IPMZ_OK;
 }
@@ -304,17 +308,18 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
 static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs& w, TrailTimer* timer) {
   const int npan = (w.N + w.nbo - 1) / w.nbo;
   if (npan < 3) {
-    HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, 0, timer));
+    HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, nullptr, 0, timer));
     return IPMZ_OK;
   }
-  const int nev = 2 * npan + 4;
+  const int nev = 3 * npan + 4;
   int rc = ensure_events(ctx, (size_t)nev);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
   HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
   HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
   HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ev, nev - 2, timer));
+  HIP_OK(hipStreamWaitEvent(ctx->sC, ev[nev - 2], 0));
+  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer));
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
   return IPMZ_OK;

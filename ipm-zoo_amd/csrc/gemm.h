@@ -31,6 +31,7 @@ struct GemmArgsT {
   int64_t row0, col0;
   int lower;  // 0: full rectangle, 1: skip strictly-upper tiles, 2: triangular grid (row0==col0, BM==BN)
   int ntm, ntn;
+  int persist;  // OPT_PERSIST: grid size (0: one workgroup per tile)
   // batch (blockIdx.y = QP): element strides between the QPs' operands
   int64_t sA, sB, sC, sW, sD;
 };
@@ -95,7 +96,11 @@ struct TileLoader {
 //   OPT_GRP   grouped triangular enumeration: bands of GRP tile rows walked
 //             column by column, so an XCD's ~64 resident tiles share ~8 W and
 //             ~8 L row panels in its L2 instead of one W and ~64 L panels
-enum { OPT_NOR2 = 2, OPT_GRP = 4 };
+//   OPT_PERSIST  a bounded grid (GemmArgs::persist workgroups) that loops over
+//             the tiles: the launch never holds every CU slot, so panel
+//             workgroups launched beside it are dispatched at once instead of
+//             waiting for the whole GEMM to drain
+enum { OPT_NOR2 = 2, OPT_GRP = 4, OPT_PERSIST = 8 };
 constexpr int GRP = 8;
 
 // grouped enumeration of the lower tiles (tm >= tn) of an ntm x ntm grid
@@ -151,11 +156,13 @@ __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_n
   // XCD-aware remap (cdna_hip_programming.md T1, bijective form): blocks
   // b and b+8 share an XCD, so consecutive logical tiles -- which share W
   // (A) rows in both enumerations -- are handed to one XCD's L2.
-  int bid = blockIdx.x;
+  int bid0 = blockIdx.x;
   {
-    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = bid % 8;
-    bid = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid / 8;
+    const int nwg = gridDim.x, q = nwg / 8, r = nwg % 8, x = bid0 % 8;
+    bid0 = (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + bid0 / 8;
   }
+  const int ntiles = (OPT & OPT_PERSIST) ? (g.lower == 2 ? g.ntm * (g.ntm + 1) / 2 : g.ntm * g.ntn) : bid0 + 1;
+  for (int bid = bid0; bid < ntiles; bid += gridDim.x) {
   int tm, tn;
   if (g.lower == 2) {
     if constexpr ((OPT & OPT_GRP) != 0) {
@@ -173,8 +180,7 @@ __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_n
     tm = bid / g.ntn;
   }
   const int i0 = tm * BM, j0 = tn * BN;
-  if (g.lower == 1 && g.row0 + i0 + BM - 1 < g.col0 + j0) return;
-
+  if (g.lower == 1 && g.row0 + i0 + BM - 1 < g.col0 + j0) continue;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave / WGN, wc = wave % WGN;
   typename MF::acc_t acc[TM][TN];
@@ -239,6 +245,7 @@ __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_n
         }
       }
     }
+  }  // tiles
 }
 
 template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2, typename T = double>
@@ -253,6 +260,7 @@ static hipError_t launch_gemm(GemmArgsT<T> g, hipStream_t st, int batch = 1) {
     if (BM == BN) nblk = (int64_t)g.ntm * (g.ntm + 1) / 2;
     else g.lower = 1;
   }
+  if ((OPT & OPT_PERSIST) && g.persist > 0 && nblk > g.persist) nblk = g.persist;
   hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, EPI, WGM, WGN, OPT>), dim3((unsigned)nblk, (unsigned)batch),
                      dim3(64 * WGM * WGN), 0, st, g);
   return hipGetLastError();

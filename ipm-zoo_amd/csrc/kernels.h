@@ -4,7 +4,7 @@
 #include <stdint.h>
 
 #define IPMZ_NBO_MAX 512
-#define IPMZ_PANEL_CTRL_WORDS 128
+#define IPMZ_PANEL_CTRL_WORDS 256
 
 namespace ipmz {
 
@@ -14,6 +14,8 @@ namespace ipmz {
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2 };
 int debug_inject_mask();
 void set_debug_inject_mask(int mask);
+void set_trail_persist(int wgs);  // EXPERIMENT (kbench A/B)
+hipError_t panel_stamps(unsigned long long* out, bool reset);  // DEBUG
 // error words the persistent kernels raise on a spin timeout (sync.h): the
 // panel kernel's ctrl[PANEL_ERR_WORD], the solve's ctrl[1]
 constexpr int PANEL_ERR_WORD = 2;
@@ -46,25 +48,37 @@ struct TrailTimer {  // HIP-event pairs around every dominant trailing-update la
   double flops = 0.0;
   hipEvent_t* next() { return used < cap ? pairs[used++] : nullptr; }
 };
-// Two-stream look-ahead when st2 and ev (>= 2*ceil(N/nbo)+2 events) are
-// given; W must then hold 3 * N * nbo doubles (else N * nbo).
-// pctrl: IPMZ_PANEL_CTRL_WORDS zeroed words for the fused panel-step kernel
-// (nbi == 64); nullptr selects the diag / TRSM / strip kernel chain.
+// Look-ahead when st2 (and, for the panel path, st3) and ev (>= 3 *
+// ceil(N/nbo) + 2 events) are given; W must then hold 3 * N * nbo doubles
+// (else N * nbo).  pctrl: panel_ctrl_words(N, nbo) zeroed words for the
+// panel path of panel.hip (nbi == 64); nullptr selects the diag / TRSM /
+// strip kernel chain.
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                        int* info, hipStream_t st, TrailTimer* timer = nullptr, hipStream_t st2 = nullptr,
-                       hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr);
-// the same blocked LDL^T in fp32 (fp32 MFMA trailing update, kernel-chain
-// panel path): the factor of the mixed-precision solve (C5)
+                       hipStream_t st3 = nullptr, hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr);
+// the same blocked LDL^T in fp32 (fp32 MFMA trailing update): the factor of
+// the mixed-precision solve (C5)
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
-                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
                        unsigned* pctrl = nullptr);
-// the whole outer panel [k0, k0 + bo) in ONE launch (panel.hip): the nbo/64
-// inner blocks pipelined by flags instead of launch boundaries.  Lb0: L^{-1}
-// block of the panel's first inner block; Wp: the panel's W buffer (N x ldw)
-hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
-                       int* info, unsigned* ctrl, hipStream_t st);
-hipError_t outer_panel(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
-                       int* info, unsigned* ctrl, hipStream_t st);
+// ctrl words of the panel path: a shared area (sticky error word) + one
+// area per outer panel
+inline int64_t panel_ctrl_words(int N, int nbo) {
+  return (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + (N + nbo - 1) / nbo);
+}
+// one outer panel [k0, k0 + bo) of the panel path (panel.hip): the chain
+// launch on st_chain, the rows launch on st_rows (flags in `area`, sticky
+// error word `err`).  Lb0: L^{-1} block of the panel's first inner block; Wp:
+// the panel's W buffer (N x ldw, row-indexed).  Wprev != nullptr: the chain
+// launch first applies the look-ahead update with the previous panel
+// [kprev, kprev + boprev) (W_prev rows, ld ldw) to the panel's diagonal
+// region (and, rows_prev, the rows launch to its rows).
+hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                        int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
+hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
+                        int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
@@ -105,8 +119,8 @@ struct MixedWs {
 int64_t mixed_ws_bytes(int N, int nbo);
 int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w);  // base == nullptr: size only
 // scale + convert + fp32 factor of the lower triangle of K (fp64, row-major)
-hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipEvent_t* ev,
-                        int nev, TrailTimer* timer = nullptr);
+hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipStream_t st3,
+                        hipEvent_t* ev, int nev, TrailTimer* timer = nullptr);
 // b <- K^{-1} b by iterative refinement (device-side stop test)
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,
                        hipStream_t st);

@@ -29,6 +29,8 @@
 namespace ipmz {
 
 static int g_inject = 0;
+static int g_trail_persist = 0;  // EXPERIMENT: persistent trailing GEMM grid (0 = off)
+void set_trail_persist(int wgs) { g_trail_persist = wgs; }
 
 int debug_inject_mask() { return g_inject; }
 void set_debug_inject_mask(int mask) { g_inject = mask; }
@@ -259,8 +261,13 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // steps/s; the fp32 factor (C5) keeps 2 x 4 (71 vs 67 TFLOP/s in situ)
   if (square_lower) {
     if (M <= IPMZ_TRAIL_SMALL_M) return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch);
-    if constexpr (std::is_same<T, double>::value)
+    if constexpr (std::is_same<T, double>::value) {
+      if (g_trail_persist > 0 && batch == 1) {
+        g.persist = g_trail_persist;
+        return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st, batch);
+      }
       return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
+    }
     return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
   }
   if (M <= 4096) return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st, batch);
@@ -306,28 +313,17 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
 }
 
 // ---------------------------------------------------------------------------
-// Factor the outer panel [k0, k0 + bo): inner diag / TRSM / strip steps, all
-// on stream st.  Writes L (in K), D, the L11^{-1} blocks and W = L D for
-// the panel's rows below each inner block (W: N x nbo, this panel's buffer).
-// Single-QP factors with nbi = 64 take the whole outer panel in ONE launch
-// (panel.hip); batched factors and nbi = 128 the diag / TRSM / strip chain.
-static hipError_t fused_panel(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int k0, int bo, int nbo,
-                              int nbi, int* info, unsigned* pctrl, hipStream_t st) {
-  return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
-}
-static hipError_t fused_panel(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int k0, int bo, int nbo,
-                              int nbi, int* info, unsigned* pctrl, hipStream_t st) {
-  return outer_panel(K, ld, N, k0, bo, D, Linv + (int64_t)(k0 / nbi) * nbi * nbi, W, nbo, info, pctrl, st);
-}
-
+// Factor the outer panel [k0, k0 + bo) as a kernel chain (batched factors
+// and nbi = 128): inner diag / TRSM / strip steps, all on stream st.  Writes
+// L (in K), D, the L11^{-1} blocks and W = L D for the panel's rows below
+// each inner block (W: N x nbo, this panel's buffer).  Single-QP factors
+// with nbi = 64 take the two-launch panel path of panel.hip instead.
 template <typename T>
 static hipError_t factor_panel(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int k0, int bo, int nbo, int nbi,
-                               int* info, hipStream_t st, const BatchStrides* bs = nullptr, unsigned* pctrl = nullptr) {
+                               int* info, hipStream_t st, const BatchStrides* bs = nullptr) {
   hipError_t e = hipSuccess;
   const int B = bs ? bs->B : 1;
   const int64_t sK = bs ? bs->sK : 0, sD = bs ? bs->sD : 0, sL = bs ? bs->sL : 0, sW = bs ? bs->sW : 0;
-  if (pctrl && B == 1 && nbi == 64)
-    return fused_panel(K, ld, N, D, Linv, W, k0, bo, nbo, nbi, info, pctrl, st);
   for (int j0 = k0; j0 < k0 + bo; j0 += nbi) {
     const int bi = k0 + bo - j0 < nbi ? k0 + bo - j0 : nbi;
     T* Lb = Linv + (int64_t)(j0 / nbi) * nbi * nbi;
@@ -399,34 +395,55 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
   return hipSuccess;
 }
 
-// Blocked LDL^T with depth-1 look-ahead on two streams (Ws: 3 buffers of
-// N x nbo).  With P_k the k-th outer panel:
-//   stream A (st): [wait N_{k-1}] update P_{k+1} with P_k ; factor P_{k+1}
-//   stream B (st2): [wait P_k] update P_{k+2} with P_k -> event N_k ;
-//                   update everything beyond P_{k+2} with P_k (the big
-//                   trailing GEMM, overlapping A's panel factorization)
+// Blocked LDL^T with depth-1 look-ahead.  With P_k the k-th outer panel
+// (nbo columns), W_k = L_k D_k its rows below it (Ws: 3 buffers of N x nbo):
+//
+// Panel path of panel.hip (single QP, nbi = 64), THREE streams:
+//   A (st, high priority): [wait N_{k-1}] the chain launch of P_{k+1}
+//      (diagonal region, first updated with P_k; the factor's critical path
+//      on ~nb CUs)
+//   C (st3, high priority): [wait N_{k-1}] the look-ahead update of P_{k+1}'s
+//      rows below its region with P_k (strip GEMM), then the rows launch of
+//      P_{k+1}: their TRSMs / strips, pipelined behind the chain by flags ->
+//      event C_{k+1};
+//      A waits for it -> event P_{k+1} (the panel is complete)
+//   B (st2, low priority): [wait P_k] update P_{k+2} with P_k -> event N_k;
+//      the trailing update beyond P_{k+2} with P_k (the big GEMM, overlapping
+//      the next panels)
+// Kernel-chain path (batched / nbi = 128), two streams: A updates P_{k+1}
+// with P_k (all rows) and factors it with factor_panel; B as above.
 // Correctness: P_{k+1}'s columns get panel j <= k-1 contributions from B
-// (ordered on B before N_{k-1}) and panel k's from A; B never touches the
-// columns A is factoring; W is triple-buffered so A's P_{k+1} never
-// overwrites the W_{k-2} a late B_{k-2} could still read (B_{k-2} precedes
-// N_{k-1} on B).  A waits for B's tail at the end.
+// (ordered on B before N_{k-1}) and panel k's from A / C; B never touches the
+// columns A / C factor; W is triple-buffered so panel k+1 never overwrites
+// the W_{k-2} a late B_{k-2} could still read (B_{k-2} precedes N_{k-1}).
+// A waits for B's tail at the end.
 template <typename T>
 static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int nbo, int nbi, int* info,
-                                hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
-                                unsigned* pctrl) {
+                                hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev,
+                                int nev, unsigned* pctrl) {
   if (N <= 0) return hipSuccess;
   if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
   const int npan = (N + nbo - 1) / nbo;
-  const bool two = st2 != nullptr && ev != nullptr && nev >= 2 * npan + 2;
+  const bool fused = pctrl != nullptr && nbi == 64;
+  const bool two = st2 != nullptr && ev != nullptr && nev >= 3 * npan + 2 && (!fused || st3 != nullptr);
   const int64_t wsz = (int64_t)N * nbo;
   auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };  // T*
   auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
-  hipError_t e = factor_panel(K, ld, N, D, Linv, Wb(0), 0, pw(0), nbo, nbi, info, st, nullptr, pctrl);
-  if (e != hipSuccess) return e;
+  auto area = [&](int k) { return pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + k); };
+  unsigned* err = pctrl ? pctrl + PANEL_ERR_WORD : nullptr;
+  hipStream_t sC = (two && fused) ? st3 : st;  // rows launches
+  auto factor = [&](int k, bool prev) -> hipError_t {  // panel k (prev: with the look-ahead update from k - 1)
+    const int k0 = k * nbo;
+    if (!fused) return factor_panel(K, ld, N, D, Linv, Wb(k), k0, pw(k), nbo, nbi, info, st);
+    return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo, info, area(k), err,
+                        prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC);
+  };
+  hipError_t e = hipSuccess;
   if (!two) {  // single stream: factor, then the whole trailing update
     for (int k = 0; k < npan; ++k) {
       const int k0 = k * nbo, bo = pw(k), t0 = k0 + bo;
+      if ((e = factor(k, false)) != hipSuccess) return e;
       if (t0 < N) {
         // timed: the launches of the dominant 128 x 128 trailing kernel
         hipEvent_t* te = timer && N - t0 > IPMZ_TRAIL_SMALL_M ? timer->next() : nullptr;
@@ -435,15 +452,19 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
         if (te) hipEventRecord(te[1], st);
         if (te) timer->flops += (double)(N - t0) * (double)(N - t0 + 1) * (double)bo;
         if (e != hipSuccess) return e;
-        if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), t0, pw(k + 1), nbo, nbi, info, st, nullptr, pctrl)) != hipSuccess)
-          return e;
       }
     }
     return hipSuccess;
   }
-  hipEvent_t* evP = ev;         // panel k factored (A)
-  hipEvent_t* evN = ev + npan;  // P_{k+2} updated with P_k (B)
-  hipEvent_t evJoin = ev[2 * npan];
+  hipEvent_t* evP = ev;             // panel k complete (A)
+  hipEvent_t* evN = ev + npan;      // P_{k+2} updated with P_k (B)
+  hipEvent_t* evC = ev + 2 * npan;  // rows launch of panel k done (C)
+  hipEvent_t evJoin = ev[3 * npan];
+  if ((e = factor(0, false)) != hipSuccess) return e;
+  if (fused) {
+    if ((e = hipEventRecord(evC[0], sC)) != hipSuccess) return e;
+    if ((e = hipStreamWaitEvent(st, evC[0], 0)) != hipSuccess) return e;
+  }
   for (int k = 0; k < npan; ++k) {
     const int k0 = k * nbo, bo = pw(k);
     const int p1 = k0 + bo;                          // start of P_{k+1}
@@ -465,26 +486,41 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if (te) timer->flops += (double)(N - p3) * (double)(N - p3 + 1) * (double)bo;
       if (e != hipSuccess) return e;
     }
-    // ---- stream A: update P_{k+1} with P_k, factor P_{k+1}
+    // ---- streams A (and C): update P_{k+1} with P_k, factor P_{k+1}
     if (k >= 1) {
       if ((e = hipStreamWaitEvent(st, evN[k - 1], 0)) != hipSuccess) return e;
+      if (fused && (e = hipStreamWaitEvent(sC, evN[k - 1], 0)) != hipSuccess) return e;
     }
-    if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
-    if ((e = factor_panel(K, ld, N, D, Linv, Wb(k + 1), p1, pw(k + 1), nbo, nbi, info, st, nullptr, pctrl)) != hipSuccess)
-      return e;
+    if (fused) {
+      // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
+      // region as a strip GEMM on C (beside the chain launch, which updates
+      // the region itself)
+      if (p2 < N) {
+        if ((e = gemm_nt_sub_t<T>(N - p2, p2 - p1, bo, Wb(k) + (int64_t)p2 * nbo, nbo, K + (int64_t)p1 * ld + k0, ld,
+                                  K + (int64_t)p2 * ld + p1, ld, p2, p1, false, sC, nullptr)) != hipSuccess)
+          return e;
+      }
+      if ((e = factor(k + 1, true)) != hipSuccess) return e;
+      if ((e = hipEventRecord(evC[k + 1], sC)) != hipSuccess) return e;
+      if ((e = hipStreamWaitEvent(st, evC[k + 1], 0)) != hipSuccess) return e;
+    } else {
+      if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
+      if ((e = factor(k + 1, false)) != hipSuccess) return e;
+    }
   }
   if ((e = hipEventRecord(evJoin, st2)) != hipSuccess) return e;
   return hipStreamWaitEvent(st, evJoin, 0);
 }
 
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
-                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev,
-                       unsigned* pctrl) {
-  return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, pctrl);
+                       int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev,
+                       int nev, unsigned* pctrl) {
+  return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl);
 }
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
-                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipEvent_t* ev, int nev, unsigned* pctrl) {
-  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, ev, nev, pctrl);
+                       hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
+                       unsigned* pctrl) {
+  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl);
 }
 
 }  // namespace ipmz

@@ -214,7 +214,7 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   w.ctrl = reinterpret_cast<unsigned*>(take(2 * 4));
   w.state = reinterpret_cast<unsigned*>(take(64));
   w.info = reinterpret_cast<int*>(take(64));
-  w.pctrl = reinterpret_cast<unsigned*>(take(IPMZ_PANEL_CTRL_WORDS * 4));
+  w.pctrl = reinterpret_cast<unsigned*>(take(panel_ctrl_words(N, nbo) * 4));
   w.s = reinterpret_cast<double*>(take((int64_t)N * 8));
   w.x = reinterpret_cast<double*>(take((int64_t)N * 8));
   w.colp = reinterpret_cast<double*>(take(nblk * N * 8));
@@ -224,7 +224,8 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   return off;
 }
 
-hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipEvent_t* ev,
+hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipStream_t st3,
+                        hipEvent_t* ev,
                         int nev, TrailTimer* timer) {
   const int N = w.N;
   if (N <= 0) return hipSuccess;
@@ -232,9 +233,10 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   hipLaunchKernelGGL(k_mx_to_f32, dim3(N), dim3(MNT), 0, st, K, ld, N, w.s, w.K32, w.ld32);
   hipError_t e = hipMemsetAsync(w.info, 0x7f, sizeof(int), st);
   if (e != hipSuccess) return e;
-  if ((e = hipMemsetAsync(w.pctrl, 0, IPMZ_PANEL_CTRL_WORDS * sizeof(unsigned), st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(w.pctrl, 0, panel_ctrl_words(N, w.nbo) * sizeof(unsigned), st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(w.ctrl, 0, 2 * sizeof(unsigned), st)) != hipSuccess) return e;  // solve: counter + error
-  return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, ev, nev, w.pctrl);
+  return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, st3, ev, nev,
+                     w.pctrl);
 }
 
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,

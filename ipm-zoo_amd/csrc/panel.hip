@@ -1,7 +1,37 @@
-// The whole outer panel of the blocked LDL^T in ONE launch: replaces, for
-// nbo columns, the column loop of LinearSolvers::ldlt_decomposition
-// (LinearSolvers.cpp:20-40).  Inner 64-column blocks hand off to each other
-// by flags inside the launch instead of kernel boundaries.
+// The panel path of the blocked LDL^T: for one outer panel (columns
+// [k0, c1), nb <= 8 inner blocks of 64), the column loop of
+// LinearSolvers::ldlt_decomposition (LinearSolvers.cpp:20-40) restricted to
+// those columns, as TWO concurrent launches that hand off by flags:
+//
+//   panel_chain_kernel (nb workgroups, 66.5 KB of LDS, s_setprio 3): the
+//   panel's diagonal region, first updated with the previous panel (each
+//   workgroup its own row of blocks).
+//     ticket 0 = the CHAIN: for every inner block j, factor the 64 x 64
+//       diagonal block (diag64_body), publish DIAG[j], then -- still in its
+//       own LDS, no hand-off -- the TRSM of the next region block (j+1, j)
+//       and that block's own diagonal update; the result IS the next diagonal
+//       block.  The whole critical path of the panel lives on one CU.
+//     tickets >= nb = TILE WORKERS: one region block (c, q), c >= 1, each,
+//       updated with the previous panel (flag TILE[c][q]); the chain updates
+//       block (0, 0) itself, straight into its LDS image.
+//     ticket c = region HELPER c (rows of block c): the TRSMs of its blocks
+//       j <= c - 2 and their strip updates, then READY[c]: its blocks
+//       (c, c-1) and (c, c) carry every contribution but block c-1's, which
+//       the chain applies itself.
+//   panel_rows_kernel (one 256-thread workgroup per 64 rows below the region,
+//   66.5 KB): first the look-ahead update of its rows with the PREVIOUS
+//   panel (A[rows, panel] -= W_prev[rows] L_prev[panel rows]^T -- real work
+//   while the chain runs, instead of a separate strip launch), then for every
+//   j: TRSM with L_jj^{-1} (waits DIAG[j]), L = T / D, W = T, and the strip
+//   pieces A[rows, q] -= L W[q, j]^T (waits REG[j][q]).
+//
+// Flags: one area of IPMZ_PANEL_CTRL_WORDS words per outer panel (zeroed by
+// one memset when the factorization starts); the sticky error word is shared.
+// Hand-off protocol (cdna_hip_programming.md §6 Guideline 16, "Valid forms"
+// row 1): data for another workgroup of a running launch is stored with sc1
+// (relaxed agent-scope atomic stores), every storing wave drains vmcnt(0),
+// a workgroup barrier, then one lane stores the flag; consumers poll with
+// agent-scope loads and read the data with sc1 loads.
 #include "common.h"
 #include "diag64.h"
 #include "kernels.h"
@@ -9,258 +39,480 @@
 
 namespace ipmz {
 
-// ---------------------------------------------------------------------------
-// The whole outer panel in ONE launch.  Columns [k0, c1), c1 = k0 + bo, as
-// nb = ceil(bo/64) inner blocks j; rows [k0, N) as 64-row chunks c, one
-// workgroup each (ticket = chunk, so a chunk only ever waits on lower
-// tickets).  Chunk c walks the blocks j = 0 .. min(c, nb-1) in order:
-//   c == j (region chunk on the diagonal): factor the 64 x 64 block,
-//          publish DIAG[j]; done.
-//   c >  j: T = A[c, j] L_jj^{-T} (waits DIAG[j]); L[c, j] = T / D_j;
-//          W[c, j] = T; region chunks publish REG[j][c];
-//          strip: A[c, q] -= L[c, j] W[q, j]^T for q = j+1 .. min(c, nb-1)
-//          (waits REG[j][q]).
-// The chain between two diagonal factorizations is one 64-row TRSM and one
-// 64 x 64 strip piece of the next region chunk, instead of a kernel boundary
-// behind ALL rows of the previous inner block (panel_step_kernel).
-// Data written earlier in the same launch is read with agent-scope loads.
+// DEBUG stamps (s_memrealtime, 100 MHz): per panel p, [0] chain start,
+// [1] chain end, [2] first helper start, [3] last helper end, [4] first rows
+// start, [5] last rows prologue end, [6] last rows end
+__device__ unsigned long long g_pstamp[128][8];
+__device__ __forceinline__ void pstamp_min(int p, int i) {
+  if (threadIdx.x == 0 && p < 128) atomicMin(&g_pstamp[p][i], __builtin_amdgcn_s_memrealtime());
+}
+__device__ __forceinline__ void pstamp_max(int p, int i) {
+  if (threadIdx.x == 0 && p < 128) atomicMax(&g_pstamp[p][i], __builtin_amdgcn_s_memrealtime());
+}
+
 namespace {
-enum { OP_TICKET = 0, OP_DONE = 1, OP_ERR = PANEL_ERR_WORD, OP_DIAG = 4, OP_REG = 16 };
+enum { OP_TICKET = 0, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128 };
 constexpr int OP_NBMAX = IPMZ_NBO_MAX / 64;
-constexpr int OP_WORDS = OP_REG + OP_NBMAX * OP_NBMAX;
-static_assert(OP_DIAG + OP_NBMAX <= OP_REG, "ctrl layout");
-static_assert(OP_WORDS <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
+static_assert(OP_DIAG + OP_NBMAX <= OP_REG && OP_REG + OP_NBMAX * OP_NBMAX <= OP_READY, "ctrl layout");
+static_assert(OP_READY + OP_NBMAX <= OP_TILE, "ctrl layout");
+static_assert(OP_TILE + OP_NBMAX * OP_NBMAX <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
+
+// A 64 x 64 tile in MFMA accumulator layout: wave w holds rows 16w + row(lane, g),
+// columns 16n + (lane & 15), n, g in 0..3.
+template <typename T>
+using Acc4 = typename Mfma<T>::acc_t[4];
+
+// acc[n] (+)= sgn * A[16w.., :] B[16n.., :]^T over k in [0, 64): A, B row-major
+// 64 x DS tiles in LDS (B read through bf: a functor (row, k) -> T).
+template <typename T, bool NEG, typename BF>
+__device__ __forceinline__ void mma_tile(const T* As, BF bf, typename Mfma<T>::acc_t (&acc)[4]) {
+  typedef Mfma<T> MF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int arow = 16 * wave + (lane & 15);
+#pragma unroll 4
+  for (int s = 0; s < 16; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    const T a = NEG ? -As[arow * DS + k] : As[arow * DS + k];
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[n] = MF::mma(a, bf(16 * n + (lane & 15), k), acc[n]);
+  }
+}
+
+// 64 x 64 tile of a row-major matrix (ld) into LDS (rows < rows, columns <
+// cols; zeros elsewhere): 16 loads in flight per thread.  SC: agent-scope
+// loads (data written earlier in this launch, possibly by another CU).
+template <typename T, bool SC>
+__device__ __forceinline__ void stage_tile(T* dst, const T* src, int64_t ld, int rows, int cols) {
+  const int tid = threadIdx.x;
+  T v[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    const T* p = &src[(int64_t)(rr < rows ? rr : 0) * ld + (cc < cols ? cc : 0)];
+    v[q] = SC ? ld_sc1(p) : *p;
+  }
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    dst[rr * DS + cc] = (rr < rows && cc < cols) ? v[q] : T(0);
+  }
+}
+
+template <typename T, bool SC>
+__device__ __forceinline__ void fetch_tile(T (&v)[16], const T* src, int64_t ld, int rows, int cols) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    const T* p = &src[(int64_t)(rr < rows ? rr : 0) * ld + (cc < cols ? cc : 0)];
+    v[q] = SC ? ld_sc1(p) : *p;
+  }
+}
+template <typename T>
+__device__ __forceinline__ void put_tile(T* dst, const T (&v)[16], int rows, int cols) {
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
+    dst[rr * DS + cc] = (rr < rows && cc < cols) ? v[q] : T(0);
+  }
+}
+
+// acc += W_prev[rows, 0:bop) L_prev[qrows, 0:bop)^T: the look-ahead update of
+// one 64 x 64 tile with the previous outer panel (W_prev rows at Wr, ld ldw;
+// L_prev rows at Lr, ld ld; both written by earlier launches), 64-deep
+// chunks staged through As / Bs with the next chunk's loads in flight.
+template <typename T>
+__device__ __forceinline__ void prev_update(typename Mfma<T>::acc_t (&acc)[4], const T* Wr, int64_t ldw, const T* Lr,
+                                            int64_t ld, int rows, int qrows, int bop, T* As, T* Bs) {
+  T va[16], vb[16];
+  fetch_tile<T, false>(va, Wr, ldw, rows, bop < 64 ? bop : 64);
+  fetch_tile<T, false>(vb, Lr, ld, qrows, bop < 64 ? bop : 64);
+  for (int kk = 0; kk < bop; kk += 64) {
+    const int kw = bop - kk < 64 ? bop - kk : 64;
+    __syncthreads();  // previous chunk's reads of As / Bs done
+    put_tile<T>(As, va, rows, kw);
+    put_tile<T>(Bs, vb, qrows, kw);
+    __syncthreads();
+    if (kk + 64 < bop) {
+      const int kn = bop - kk - 64 < 64 ? bop - kk - 64 : 64;
+      fetch_tile<T, false>(va, Wr + kk + 64, ldw, rows, kn);
+      fetch_tile<T, false>(vb, Lr + kk + 64, ld, qrows, kn);
+    }
+    mma_tile<T, false>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
+  }
+  __syncthreads();
+}
+
+// accumulator-layout tile <-> global (lower part of a diagonal tile when DIAG)
+template <typename T, bool SC, bool DIAGT>
+__device__ __forceinline__ void load_acc(typename Mfma<T>::acc_t (&acc)[4], const T* src, int64_t ld, int rows,
+                                         int cols) {
+  typedef Mfma<T> MF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = 16 * n + (lane & 15);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 16 * wave + MF::row(lane, g);
+      const bool in = row < rows && col < cols && (!DIAGT || col <= row);
+      const T* p = &src[(int64_t)(in ? row : 0) * ld + (in ? col : 0)];
+      acc[n][g] = in ? (SC ? ld_sc1(p) : *p) : T(0);
+    }
+  }
+}
+template <typename T, bool SC, bool DIAGT>
+__device__ __forceinline__ void store_acc(const typename Mfma<T>::acc_t (&acc)[4], T* dst, int64_t ld, int rows,
+                                          int cols) {
+  typedef Mfma<T> MF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int n = 0; n < 4; ++n) {
+    const int col = 16 * n + (lane & 15);
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int row = 16 * wave + MF::row(lane, g);
+      if (row < rows && col < cols && (!DIAGT || col <= row)) {
+        if (SC) st_sc1(&dst[(int64_t)row * ld + col], acc[n][g]);
+        else dst[(int64_t)row * ld + col] = acc[n][g];
+      }
+    }
+  }
+}
+// accumulator-layout tile -> LDS (this wave's rows)
+template <typename T>
+__device__ __forceinline__ void put_acc(T* dst, const typename Mfma<T>::acc_t (&acc)[4]) {
+  typedef Mfma<T> MF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) dst[(16 * wave + MF::row(lane, g)) * DS + 16 * n + (lane & 15)] = acc[n][g];
+}
+template <typename T>
+__device__ __forceinline__ void zero_acc(typename Mfma<T>::acc_t (&acc)[4]) {
+#pragma unroll
+  for (int n = 0; n < 4; ++n) acc[n] = (typename Mfma<T>::acc_t){T(0), T(0), T(0), T(0)};
+}
 }  // namespace
 
-// T = float: the fp32 factor of the mixed-precision path (f32 MFMA TRSM and
-// strip pieces; the diagonal block is factored in fp64 and stored in fp32).
+// ---------------------------------------------------------------------------
+// T = float: the fp32 factor of the mixed-precision path (f32 MFMA TRSMs and
+// strip pieces; the 64 x 64 diagonal blocks are factored in fp64 and stored
+// in fp32).
+// amdgpu_waves_per_eu(2): <= 256 registers per lane (VGPR + AGPR), so a
+// panel workgroup fits beside a trailing-GEMM workgroup (64 per lane at 4
+// waves per SIMD) -- with more it waits for a CU with no GEMM at all
 template <typename T>
-__global__ __launch_bounds__(256) void outer_panel_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_chain_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
                                                           T* __restrict__ D, T* __restrict__ Lb0, T* __restrict__ Wp,
-                                                          int ldw, int* __restrict__ info,
-                                                          unsigned* __restrict__ ctrl, int inject) {
+                                                          int ldw, int* __restrict__ info, unsigned* __restrict__ area,
+                                                          unsigned* __restrict__ err, int inject,
+                                                          const T* __restrict__ Wprev, int kprev, int boprev) {
   typedef Mfma<T> MF;
   typedef typename MF::acc_t acc_t;
+  // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
+  // trailing-GEMM workgroup leaves free, so it is never starved of a CU);
+  // s_setprio 3: its waves win issue arbitration (matrix pipe included)
+  // against the GEMM waves that share the CU
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   __shared__ unsigned sh_ticket, sh_ok;
+  __builtin_amdgcn_s_setprio(3);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) sh_ticket = atomicAdd(&ctrl[OP_TICKET], 1u);
+  if (tid == 0) sh_ticket = atomicAdd(&area[OP_TICKET], 1u);
   __syncthreads();
-  const int c = (int)sh_ticket;
-  unsigned* err = &ctrl[OP_ERR];
-  const int ce = c1 < N ? c1 : N;  // end of the panel's columns
+  const int t = (int)sh_ticket;
+  const int ce = c1 < N ? c1 : N;
   const int nb = (ce - k0 + 63) / 64;
-  const int row0 = k0 + 64 * c;
-  const int rows = N - row0 < 64 ? N - row0 : 64;
-  const bool region = c < nb;
-  const int jend = region ? c : nb;  // blocks this chunk TRSMs: j < jend
-  T* As = reinterpret_cast<T*>(smem);              // A rows, then L rows (64 x DS)
-  T* Bs = reinterpret_cast<T*>(smem + 64 * DS);  // L_jj^{-1}, then W pieces (64 x DS)
-  const int arow = 16 * wave + (lane & 15);
-  bool ok = true;
-  for (int j = 0; j < jend && ok; ++j) {
+  const int pidx = k0 / (c1 - k0 > 0 ? c1 - k0 : 1);
+  pstamp_min(pidx, t == 0 ? 0 : 2);
+  double* M = smem;
+  double* X = smem + 64 * DS;
+  double* dsh = smem + 2 * 64 * DS;  // 64 doubles (diag64_body's pivots)
+  auto bsz = [&](int j) { return ce - (k0 + 64 * j) < 64 ? ce - (k0 + 64 * j) : 64; };
+
+  if (t == 0) {
+    // ================================================================ CHAIN
+    if (Wprev) {  // block (0, 0) with the previous panel's update, straight into M
+      acc_t own[4];
+      zero_acc<T>(own);
+      prev_update<T>(own, Wprev + (int64_t)k0 * ldw, ldw, K + (int64_t)k0 * ld + kprev, ld, bsz(0), bsz(0), boprev,
+                     reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+      acc_t a0[4];
+      load_acc<T, false, true>(a0, K + (int64_t)k0 * ld + k0, ld, bsz(0), bsz(0));
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int col = 16 * n + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = 16 * wave + MF::row(lane, g);
+          M[row * DS + col] = (row < bsz(0) && col <= row) ? (double)(a0[n][g] - own[n][g]) : (row == col ? 1.0 : 0.0);
+        }
+      }
+    }
+    for (int j = 0; j < nb; ++j) {
+      const int j0 = k0 + 64 * j, bj = bsz(j);
+      T* Lb = Lb0 + (int64_t)j * 64 * 64;
+      if (j == 0 && !Wprev) diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
+      else diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
+      if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);  // inject: the timeout tests only
+      if (j + 1 >= nb) break;
+      // ---- block row c = j + 1: (c, j) and (c, c) from helper c
+      const int c = j + 1, r0 = k0 + 64 * c, rows = bsz(c);
+      if (!wait_flag(&area[OP_READY + c], err, &sh_ok)) return;
+      // A(c, j) into M (free: L_jj is in K), the own block (c, c) into registers
+      stage_tile<T, true>(reinterpret_cast<T*>(M), K + (int64_t)r0 * ld + j0, ld, rows, 64);
+      acc_t own[4];
+      load_acc<T, true, true>(own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
+      T rd[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
+      __syncthreads();
+      // TRSM: T = A(c, j) X_jj^T with X lower triangular (its upper part in
+      // LDS is not meaningful: masked)
+      acc_t acc[4];
+      zero_acc<T>(acc);
+      mma_tile<T, false>(reinterpret_cast<const T*>(M), [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); },
+                         acc);
+      __syncthreads();  // M and X reads done
+      T* Lrow = K + (int64_t)r0 * ld + j0;
+      T* Wrow = Wp + (int64_t)r0 * ldw + 64 * j;
+      acc_t lacc[4];
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
+      store_acc<T, false, false>(lacc, Lrow, ld, rows, 64);
+      store_acc<T, true, false>(acc, Wrow, ldw, rows, 64);
+      publish(&area[OP_REG + j * OP_NBMAX + c]);  // W(c, j): helpers' and the rows kernel's strips
+      // own update (c, c) -= L(c, j) W(c, j)^T: L into X, W into M (both free:
+      // L_jj is in K, X_jj no longer needed)
+      T* Lx = reinterpret_cast<T*>(X);
+      T* Wm = reinterpret_cast<T*>(M);
+      put_acc<T>(Lx, lacc);
+      put_acc<T>(Wm, acc);
+      __syncthreads();
+      mma_tile<T, true>(Lx, [&](int r, int k) { return Wm[r * DS + k]; }, own);
+      __syncthreads();  // every wave done reading M and X
+      // the next diagonal block, straight into diag64_body's image
+#pragma unroll
+      for (int n = 0; n < 4; ++n) {
+        const int col = 16 * n + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = 16 * wave + MF::row(lane, g);
+          M[row * DS + col] = (row < rows && col <= row) ? (double)own[n][g] : (row == col ? 1.0 : 0.0);
+        }
+      }
+      // (diag64_body's first barrier orders these stores before its reads)
+    }
+    pstamp_max(pidx, 1);
+    return;
+  }
+  if (t >= nb) {
+    // ============================================================ TILE WORKER
+    // region block (c, q), 1 <= c < nb, q <= c: the look-ahead update with the
+    // previous panel, stored write-through, then TILE[c][q]
+    int w = t - nb, c = 1;
+    while (w > c) {
+      w -= c + 1;
+      ++c;
+    }
+    const int q = w, r0 = k0 + 64 * c, q0 = k0 + 64 * q, rows = bsz(c), qrows = bsz(q);
+    acc_t upd[4], tile[4];
+    zero_acc<T>(upd);
+    prev_update<T>(upd, Wprev + (int64_t)r0 * ldw, ldw, K + (int64_t)q0 * ld + kprev, ld, rows, qrows, boprev,
+                   reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+    if (q == c) load_acc<T, false, true>(tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
+    else load_acc<T, false, false>(tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) tile[n][g] = tile[n][g] - upd[n][g];
+    if (q == c) store_acc<T, true, true>(tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
+    else store_acc<T, true, false>(tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+    publish(&area[OP_TILE + c * OP_NBMAX + q]);
+    return;
+  }
+  // ================================================================= HELPER
+  const int c = t, r0 = k0 + 64 * c, rows = bsz(c);
+  T* As = reinterpret_cast<T*>(M);  // L(c, j) rows
+  T* Bs = reinterpret_cast<T*>(X);  // L_jj^{-1}, then W pieces
+  if (Wprev) {  // this row of region blocks, updated with the previous panel by the tile workers
+    for (int q = 0; q <= c; ++q)
+      if (!wait_flag(&area[OP_TILE + c * OP_NBMAX + q], err, &sh_ok)) return;
+  }
+  for (int j = 0; j + 2 <= c; ++j) {
     const int j0 = k0 + 64 * j;
-    const int bj = ce - j0 < 64 ? ce - j0 : 64;
     T* Lb = Lb0 + (int64_t)j * 64 * 64;
-    {  // this chunk's A rows of block j: loads in flight before the wait
-      T v[16];
+    if (j || Wprev) stage_tile<T, true>(As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+    else stage_tile<T, false>(As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+    if (!wait_flag(&area[OP_DIAG + j], err, &sh_ok)) return;
+    stage_tile<T, true>(Bs, Lb, 64, 64, 64);
+    T rd[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
-        const int r2 = rr < rows ? rr : 0, c2 = cc < bj ? cc : 0;
-        const T* src = &K[(int64_t)(row0 + r2) * ld + j0 + c2];
-        v[q] = j ? ld_sc1(src) : *src;
-      }
-      __syncthreads();  // previous block's strip finished reading As / Bs
+    for (int n = 0; n < 4; ++n) rd[n] = T(1) / ld_sc1(&D[j0 + 16 * n + (lane & 15)]);
+    __syncthreads();
+    acc_t acc[4];
+    zero_acc<T>(acc);
+    mma_tile<T, false>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
+    __syncthreads();
+    acc_t lacc[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
-        const int rr = (tid >> 6) + 4 * q, cc = tid & 63;
-        As[rr * DS + cc] = (rr < rows && cc < bj) ? v[q] : T(0);
+    for (int n = 0; n < 4; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
+    store_acc<T, false, false>(lacc, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+    store_acc<T, true, false>(acc, Wp + (int64_t)r0 * ldw + 64 * j, ldw, rows, 64);
+    publish(&area[OP_REG + j * OP_NBMAX + c]);
+    put_acc<T>(As, lacc);
+    // strips: (c, q) -= L(c, j) W(q, j)^T, q = j+1 .. c
+    for (int q = j + 1; q <= c; ++q) {
+      const int q0 = k0 + 64 * q, qrows = bsz(q);
+      if (q == c) {
+        put_acc<T>(Bs, acc);
+      } else {
+        if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], err, &sh_ok)) return;
+        stage_tile<T, true>(Bs, Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, 64);
       }
+      acc_t tile[4];
+      if (q == c) load_acc<T, true, true>(tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
+      else load_acc<T, true, false>(tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+      __syncthreads();
+      mma_tile<T, true>(As, [&](int r, int k) { return Bs[r * DS + k]; }, tile);
+      if (q == c) store_acc<T, true, true>(tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
+      else store_acc<T, true, false>(tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+      __syncthreads();  // Bs reused by the next piece
     }
-    if (!(ok = wait_flag(&ctrl[OP_DIAG + j], err, &sh_ok))) break;
-#pragma unroll 4
-    for (int q = 0; q < 16; ++q) {
-      const int idx = tid + 256 * q;
-      Bs[(idx >> 6) * DS + (idx & 63)] = ld_sc1(&Lb[idx]);
+  }
+  publish(&area[OP_READY + c]);
+  pstamp_max(pidx, 3);
+}
+
+// ---------------------------------------------------------------------------
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_rows_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
+                                                         const T* __restrict__ D, const T* __restrict__ Lb0,
+                                                         T* __restrict__ Wp, int ldw, unsigned* __restrict__ area,
+                                                         unsigned* __restrict__ err, const T* __restrict__ Wprev,
+                                                         int ldwp, int kprev, int boprev) {
+  typedef Mfma<T> MF;
+  typedef typename MF::acc_t acc_t;
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS];
+  __shared__ unsigned sh_ok;
+  const int lane = threadIdx.x & 63;
+  const int ce = c1 < N ? c1 : N;
+  const int nb = (ce - k0 + 63) / 64;
+  const int row0 = ce + 64 * blockIdx.x;
+  const int rows = N - row0 < 64 ? N - row0 : 64;
+  auto bsz = [&](int j) { return ce - (k0 + 64 * j) < 64 ? ce - (k0 + 64 * j) : 64; };
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
+  T* Krow = K + (int64_t)row0 * ld;
+  const int pidx = k0 / (c1 - k0 > 0 ? c1 - k0 : 1);
+  pstamp_min(pidx, 4);
+  // ---- look-ahead update with the previous panel (written by earlier launches)
+  if (Wprev) {
+    for (int q = 0; q < nb; ++q) {
+      const int q0 = k0 + 64 * q, qrows = bsz(q);
+      acc_t acc[4], tile[4];
+      zero_acc<T>(acc);
+      prev_update<T>(acc, Wprev + (int64_t)row0 * ldwp, ldwp, K + (int64_t)q0 * ld + kprev, ld, rows, qrows, boprev,
+                     As, Bs);
+      load_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) tile[n][g] = tile[n][g] - acc[n][g];
+      store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
     }
+  }
+  pstamp_max(pidx, 5);
+  // ---- TRSMs and strips of this chunk's rows
+  bool ok = true;
+  for (int j = 0; j < nb && ok; ++j) {
+    const int j0 = k0 + 64 * j, bj = bsz(j);
+    const T* Lb = Lb0 + (int64_t)j * 64 * 64;
+    __syncthreads();  // previous block's strip finished reading As / Bs
+    stage_tile<T, true>(As, Krow + j0, ld, rows, bj);
+    if (!(ok = wait_flag(&area[OP_DIAG + j], err, &sh_ok))) break;
+    stage_tile<T, true>(Bs, Lb, 64, 64, 64);
     T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int col = 16 * n + (lane & 15);
       rd[n] = col < bj ? T(1) / ld_sc1(&D[j0 + col]) : T(0);
     }
-    // region chunk: its own diagonal block (columns of block c), the target
-    // of this iteration's first strip piece -- loads in flight during the TRSM
-    acc_t own[4];
-    if (region) {
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int cabs = row0 + 16 * n + (lane & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int row = 16 * wave + MF::row(lane, g);
-          const bool in = row < rows && cabs < ce && cabs <= row0 + row;
-          const T* src = &K[(int64_t)(row0 + (in ? row : 0)) * ld + (in ? cabs : k0)];
-          own[n][g] = in ? (j ? ld_sc1(src) : *src) : T(0);
-        }
-      }
-    }
     __syncthreads();
-    // ---- TRSM: wave w owns rows 16w..16w+15, all 64 columns
     acc_t acc[4];
+    zero_acc<T>(acc);
+    mma_tile<T, false>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
+    __syncthreads();
+    acc_t lacc[4];
 #pragma unroll
-    for (int n = 0; n < 4; ++n) acc[n] = (acc_t){T(0), T(0), T(0), T(0)};
-#pragma unroll 4
-    for (int s = 0; s < 16; ++s) {
-      const int k = 4 * s + (lane >> 4);
-      const T a = As[arow * DS + k];
+    for (int n = 0; n < 4; ++n)
 #pragma unroll
-      for (int n = 0; n < 4; ++n) acc[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
-    }
-#pragma unroll
-    for (int n = 0; n < 4; ++n) {
-      const int col = 16 * n + (lane & 15);
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int row = 16 * wave + MF::row(lane, g);
-        const T w = acc[n][g], l = w * rd[n];
-        As[row * DS + col] = l;  // this wave's rows only
-        if (row < rows && col < bj) {
-          T* wp = &Wp[(int64_t)(row0 + row) * ldw + 64 * j + col];
-          if (region) st_sc1(wp, w);
-          else *wp = w;
-          K[(int64_t)(row0 + row) * ld + j0 + col] = l;
-        }
-      }
-    }
-    if (region) {
-      publish(&ctrl[OP_REG + j * OP_NBMAX + c]);  // (its barrier also frees Bs)
-      // ---- own piece first: A[c, c] -= L[c, j] W[c, j]^T with W from this
-      // workgroup's registers through LDS, no global round trip -- for
-      // j = c - 1 it is the last link of the chain to this chunk's diagonal
-      // factorization
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int col = 16 * n + (lane & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) Bs[(16 * wave + MF::row(lane, g)) * DS + col] = acc[n][g];
-      }
+      for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
+    store_acc<T, false, false>(lacc, Krow + j0, ld, rows, bj);
+    store_acc<T, false, false>(acc, Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
+    put_acc<T>(As, lacc);
+    // strips: (rows, q) -= L(rows, j) W(q, j)^T, q = j+1 .. nb-1
+    for (int q = j + 1; q < nb; ++q) {
+      const int q0 = k0 + 64 * q, qrows = bsz(q);
+      if (!(ok = wait_flag(&area[OP_REG + j * OP_NBMAX + q], err, &sh_ok))) break;  // (its barrier also frees Bs)
+      stage_tile<T, true>(Bs, Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, bj);
+      acc_t tile[4];
+      load_acc<T, true, false>(tile, Krow + q0, ld, rows, qrows);
       __syncthreads();
-#pragma unroll 4
-      for (int s = 0; s < 16; ++s) {
-        const int k = 4 * s + (lane >> 4);
-        const T a = -As[arow * DS + k];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) own[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], own[n]);
-      }
-      if (j + 1 < c) {  // more blocks to come: back to K (re-read with sc1)
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int cabs = row0 + 16 * n + (lane & 15);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int row = 16 * wave + MF::row(lane, g);
-            if (row < rows && cabs < ce && cabs <= row0 + row) K[(int64_t)(row0 + row) * ld + cabs] = own[n][g];
-          }
-        }
-      } else {  // final: straight into the diagonal factorization's LDS image
-        const int bc = ce - row0 < 64 ? ce - row0 : 64;
-        double* M = smem;
-        __syncthreads();  // every wave done reading As / Bs
-#pragma unroll
-        for (int n = 0; n < 4; ++n) {
-          const int col = 16 * n + (lane & 15);
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int row = 16 * wave + MF::row(lane, g);
-            M[row * DS + col] = (row < bc && col <= row) ? (double)own[n][g] : (row == col ? 1.0 : 0.0);
-          }
-        }
-      }
-    }
-    // ---- strip: A[c, q] -= L[c, j] W[q, j]^T, q = j+1 .. (region: c - 1; else nb-1)
-    const int qend = region ? c - 1 : nb - 1;
-    for (int q = j + 1; q <= qend; ++q) {
-      if (!(ok = wait_flag(&ctrl[OP_REG + j * OP_NBMAX + q], err, &sh_ok))) break;  // also: Bs is free
-      const int cbase = k0 + 64 * q;
-#pragma unroll 4
-      for (int u = 0; u < 16; ++u) {
-        const int kk = (tid >> 6) + 4 * u, cc = tid & 63;
-        const int wr = cbase + kk;
-        Bs[kk * DS + cc] = (wr < ce && cc < bj) ? ld_sc1(&Wp[(int64_t)wr * ldw + 64 * j + cc]) : T(0);
-      }
+      mma_tile<T, true>(As, [&](int r, int k) { return Bs[r * DS + k]; }, tile);
+      store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
       __syncthreads();
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int cabs = cbase + 16 * n + (lane & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int row = 16 * wave + MF::row(lane, g);
-          const bool in = row < rows && cabs < ce && cabs <= row0 + row;
-          const T* src = &K[(int64_t)(row0 + (in ? row : 0)) * ld + (in ? cabs : k0)];
-          acc[n][g] = in ? (j ? ld_sc1(src) : *src) : T(0);
-        }
-      }
-#pragma unroll 4
-      for (int s = 0; s < 16; ++s) {
-        const int k = 4 * s + (lane >> 4);
-        const T a = -As[arow * DS + k];
-#pragma unroll
-        for (int n = 0; n < 4; ++n) acc[n] = MF::mma(a, Bs[(16 * n + (lane & 15)) * DS + k], acc[n]);
-      }
-#pragma unroll
-      for (int n = 0; n < 4; ++n) {
-        const int cabs = cbase + 16 * n + (lane & 15);
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int row = 16 * wave + MF::row(lane, g);
-          if (row < rows && cabs < ce && cabs <= row0 + row) K[(int64_t)(row0 + row) * ld + cabs] = acc[n][g];
-        }
-      }
-      __syncthreads();  // Bs reused by the next piece
     }
   }
-  if (ok && region) {
-    // this chunk's diagonal block: every earlier block's strip is applied
-    // (chunk 0 reads it from K; the others left it in LDS, see above)
-    const int j0 = k0 + 64 * c;
-    const int bj = ce - j0 < 64 ? ce - j0 : 64;
-    if (c == 0)
-      diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb0, info, smem, smem + 64 * DS, smem + 2 * 64 * DS,
-                                         nullptr);
-    else
-      diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb0 + (int64_t)c * 64 * 64, info, smem, smem + 64 * DS,
-                                        smem + 2 * 64 * DS, nullptr);
-    if (!(inject && c == 0)) publish(&ctrl[OP_DIAG + c]);  // inject: tests of the timeout path only
-  }
-  // ---- completion: the last workgroup out zeroes the ctrl words
-  __syncthreads();
-  if (tid == 0) {
-    const unsigned prev = __hip_atomic_fetch_add(&ctrl[OP_DONE], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      for (int i = 0; i < OP_WORDS; ++i)
-        if (i != OP_ERR) __hip_atomic_store(&ctrl[i], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  pstamp_max(pidx, 6);
 }
 
+// ---------------------------------------------------------------------------
 template <typename T>
-static hipError_t outer_panel_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw, int* info,
-                                unsigned* ctrl, hipStream_t st) {
+static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw, int* info,
+                                 unsigned* area, unsigned* err, const T* Wprev, int kprev, int boprev, bool rows_prev,
+                                 hipStream_t st_chain, hipStream_t st_rows) {
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
-  const int nch = (N - k0 + 63) / 64;
-  hipLaunchKernelGGL(outer_panel_kernel<T>, dim3(nch), dim3(256), 0, st, K, ld, N, k0, k0 + bo, D, Lb0, Wp, ldw, info,
-                     ctrl, debug_inject_mask() & IPMZ_INJECT_PANEL);
+  const int ce = k0 + bo;
+  const int nb = (bo + 63) / 64;
+  // chain + nb - 1 helpers (+ one tile worker per region block below the
+  // diagonal block (0, 0) when the look-ahead update is applied here)
+  const int nwork = Wprev ? nb * (nb + 1) / 2 - 1 : 0;
+  hipLaunchKernelGGL(panel_chain_kernel<T>, dim3(nb + nwork), dim3(256), 0, st_chain, K, ld, N, k0, ce, D, Lb0, Wp, ldw, info,
+                     area, err, debug_inject_mask() & IPMZ_INJECT_PANEL, Wprev, kprev, boprev);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess || ce >= N) return e;
+  const int nch = (N - ce + 63) / 64;
+  hipLaunchKernelGGL(panel_rows_kernel<T>, dim3(nch), dim3(256), 0, st_rows, K, ld, N, k0, ce, (const T*)D,
+                     (const T*)Lb0, Wp, ldw, area, err, rows_prev ? Wprev : nullptr, ldw, kprev, boprev);
   return hipGetLastError();
 }
-hipError_t outer_panel(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
-                       int* info, unsigned* ctrl, hipStream_t st) {
-  return outer_panel_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, ctrl, st);
+hipError_t panel_stamps(unsigned long long* out, bool reset) {
+  if (reset) {
+    static unsigned long long init[128][8];
+    for (int p = 0; p < 128; ++p)
+      for (int i = 0; i < 8; ++i) init[p][i] = (i == 0 || i == 2 || i == 4) ? ~0ull : 0ull;
+    return hipMemcpyToSymbol(HIP_SYMBOL(g_pstamp), init, sizeof(init));
+  }
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamp), sizeof(unsigned long long) * 128 * 8);
 }
-hipError_t outer_panel(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
-                       int* info, unsigned* ctrl, hipStream_t st) {
-  return outer_panel_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, ctrl, st);
+hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                        int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows) {
+  return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, area, err, Wprev, kprev, boprev, rows_prev,
+                                st_chain, st_rows);
+}
+hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
+                        int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows) {
+  return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, area, err, Wprev, kprev, boprev, rows_prev,
+                               st_chain, st_rows);
 }
 
 }  // namespace ipmz

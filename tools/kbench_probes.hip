@@ -31,6 +31,11 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 14: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st);
     case 15: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st);  // the product's trailing tile
     case 23: return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st);
+    // persistent grids (OPT_PERSIST): 16-wave tile with 256 / 384 / 512 workgroups
+    case 30: g.persist = 256; return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st);
+    case 31: g.persist = 384; return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st);
+    case 32: g.persist = 512; return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st);
+    case 33: g.persist = 248; return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st);
     default: break;
   }
   g.lower = 1;  // strip (rectangle, upper tiles of the diagonal band skipped)
