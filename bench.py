@@ -241,13 +241,15 @@ def main():
                                        (", normal equations (Cholesky H, S)" if wl.get("normal") else
                                         ", augmented LDL^T")),
                        "parallelism": f"replicas x{world} (independent QPs, one per GPU)",
-                       "blocking": {"nbo": args.nbo or (384 if Nk >= 8192 and args.nbi == 64 else 256),
-                                    "nbi": args.nbi},
+                       "blocking": dict(zip(("nbo", "nbi"), ctx.blocking(Nk))),
                        "timing": "HIP-graph replay of the whole step (production path); phases from a second, "
                                  "instrumented pass",
                        "description": wl["desc"]},
             "restarts": s["restarts"],
         }
+        if mixed:  # refinement corrections of the last step's two solves
+            out["ir"] = {"iters_affine": s["ir_iters_aff"], "iters_corrector": s["ir_iters"],
+                         "ratio_affine": s["ir_ratio_aff"], "ratio_corrector": s["ir_ratio"]}
         if ph:
             k = args.steps
             factor_ms = ph["factor"] / k

@@ -111,6 +111,9 @@ int ipmz_debug_inject(int mask);
  * diagonal block nbi (64 or 128).  Defaults 0 / 64.  Workspace sizes depend
  * on it: query them after setting the blocking. */
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);
+/* The blocking an order-N factor uses with this context (nbo resolved when
+ * the context's is 0 = by matrix order). */
+int ipmz_ctx_get_blocking(ipmz_ctx* ctx, int N, int* nbo, int* nbi);
 
 /* ---- LinearSolvers on device memory ------------------------------------ */
 /* Workspace for factor + solve of order N (bytes). */

@@ -54,12 +54,12 @@ struct ipmz_ctx {
 };
 
 // outer panel width for an order-N factor: the context's, or by size --
-// 384 for N >= 8192 (C3: 59.7 -> 61.1 steps/s, C5: 31.3 -> 32.4), 256 below
-// (C2: 277 vs 260 at 384).  Every workspace layout and every factor / solve
+// 512 for N >= 8192 (kbench factor, N = 11264: 12.95 ms at 384, 12.34 at
+// 512; N = 16384: 32.1 -> 31.2 ms), 256 below (C2: 277 vs 260 steps/s at 384).  Every workspace layout and every factor / solve
 // of an order-N matrix uses this same value.
 static int nbo_for(const ipmz_ctx* ctx, int N) {
   if (ctx->nbo > 0) return ctx->nbo;
-  return N >= 8192 && ctx->nbi == 64 ? 384 : 256;
+  return N >= 8192 && ctx->nbi == 64 ? 512 : 256;
 }
 
 static int ensure_events(ipmz_ctx* ctx, size_t n) {
@@ -161,6 +161,13 @@ int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi) {
     return fail(IPMZ_ERR_INVALID, "blocking: nbi in {64,128}, nbo 0 (auto) or a multiple of nbi, <= 512");
   ctx->nbo = nbo;
   ctx->nbi = nbi;
+  return IPMZ_OK;
+}
+
+int ipmz_ctx_get_blocking(ipmz_ctx* ctx, int N, int* nbo, int* nbi) {
+  if (!ctx || N < 0 || !nbo || !nbi) return fail(IPMZ_ERR_INVALID, "ipmz_ctx_get_blocking: bad arguments");
+  *nbo = nbo_for(ctx, N);
+  *nbi = ctx->nbi;
   return IPMZ_OK;
 }
 

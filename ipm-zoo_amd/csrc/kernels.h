@@ -14,8 +14,6 @@ namespace ipmz {
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2 };
 int debug_inject_mask();
 void set_debug_inject_mask(int mask);
-void set_trail_persist(int wgs);  // EXPERIMENT (kbench A/B)
-hipError_t panel_stamps(unsigned long long* out, bool reset);  // DEBUG
 // error words the persistent kernels raise on a spin timeout (sync.h): the
 // panel kernel's ctrl[PANEL_ERR_WORD], the solve's ctrl[1]
 constexpr int PANEL_ERR_WORD = 2;

@@ -29,8 +29,6 @@
 namespace ipmz {
 
 static int g_inject = 0;
-static int g_trail_persist = 0;  // EXPERIMENT: persistent trailing GEMM grid (0 = off)
-void set_trail_persist(int wgs) { g_trail_persist = wgs; }
 
 int debug_inject_mask() { return g_inject; }
 void set_debug_inject_mask(int mask) { g_inject = mask; }
@@ -261,13 +259,8 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // steps/s; the fp32 factor (C5) keeps 2 x 4 (71 vs 67 TFLOP/s in situ)
   if (square_lower) {
     if (M <= IPMZ_TRAIL_SMALL_M) return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch);
-    if constexpr (std::is_same<T, double>::value) {
-      if (g_trail_persist > 0 && batch == 1) {
-        g.persist = g_trail_persist;
-        return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP | OPT_PERSIST>(g, st, batch);
-      }
+    if constexpr (std::is_same<T, double>::value)
       return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
-    }
     return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);
   }
   if (M <= 4096) return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st, batch);

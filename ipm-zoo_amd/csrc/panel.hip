@@ -19,11 +19,12 @@
 //       (c, c-1) and (c, c) carry every contribution but block c-1's, which
 //       the chain applies itself.
 //   panel_rows_kernel (one 256-thread workgroup per 64 rows below the region,
-//   66.5 KB): first the look-ahead update of its rows with the PREVIOUS
-//   panel (A[rows, panel] -= W_prev[rows] L_prev[panel rows]^T -- real work
-//   while the chain runs, instead of a separate strip launch), then for every
-//   j: TRSM with L_jj^{-1} (waits DIAG[j]), L = T / D, W = T, and the strip
-//   pieces A[rows, q] -= L W[q, j]^T (waits REG[j][q]).
+//   66.5 KB): optionally (rows_prev) first the look-ahead update of its rows
+//   with the PREVIOUS panel (A[rows, panel] -= W_prev[rows] L_prev[panel
+//   rows]^T; the fused factor runs that update as a strip GEMM on its own
+//   stream instead), then for every j: TRSM with L_jj^{-1} (waits DIAG[j]),
+//   L = T / D, W = T, and the strip pieces A[rows, q] -= L W[q, j]^T (waits
+//   REG[j][q]).
 //
 // Flags: one area of IPMZ_PANEL_CTRL_WORDS words per outer panel (zeroed by
 // one memset when the factorization starts); the sticky error word is shared.
@@ -38,17 +39,6 @@
 #include "sync.h"
 
 namespace ipmz {
-
-// DEBUG stamps (s_memrealtime, 100 MHz): per panel p, [0] chain start,
-// [1] chain end, [2] first helper start, [3] last helper end, [4] first rows
-// start, [5] last rows prologue end, [6] last rows end
-__device__ unsigned long long g_pstamp[128][8];
-__device__ __forceinline__ void pstamp_min(int p, int i) {
-  if (threadIdx.x == 0 && p < 128) atomicMin(&g_pstamp[p][i], __builtin_amdgcn_s_memrealtime());
-}
-__device__ __forceinline__ void pstamp_max(int p, int i) {
-  if (threadIdx.x == 0 && p < 128) atomicMax(&g_pstamp[p][i], __builtin_amdgcn_s_memrealtime());
-}
 
 namespace {
 enum { OP_TICKET = 0, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128 };
@@ -225,8 +215,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   const int t = (int)sh_ticket;
   const int ce = c1 < N ? c1 : N;
   const int nb = (ce - k0 + 63) / 64;
-  const int pidx = k0 / (c1 - k0 > 0 ? c1 - k0 : 1);
-  pstamp_min(pidx, t == 0 ? 0 : 2);
   double* M = smem;
   double* X = smem + 64 * DS;
   double* dsh = smem + 2 * 64 * DS;  // 64 doubles (diag64_body's pivots)
@@ -307,7 +295,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       }
       // (diag64_body's first barrier orders these stores before its reads)
     }
-    pstamp_max(pidx, 1);
     return;
   }
   if (t >= nb) {
@@ -387,7 +374,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     }
   }
   publish(&area[OP_READY + c]);
-  pstamp_max(pidx, 3);
 }
 
 // ---------------------------------------------------------------------------
@@ -410,8 +396,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
   T* Krow = K + (int64_t)row0 * ld;
-  const int pidx = k0 / (c1 - k0 > 0 ? c1 - k0 : 1);
-  pstamp_min(pidx, 4);
   // ---- look-ahead update with the previous panel (written by earlier launches)
   if (Wprev) {
     for (int q = 0; q < nb; ++q) {
@@ -428,7 +412,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
     }
   }
-  pstamp_max(pidx, 5);
   // ---- TRSMs and strips of this chunk's rows
   bool ok = true;
   for (int j = 0; j < nb && ok; ++j) {
@@ -470,7 +453,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       __syncthreads();
     }
   }
-  pstamp_max(pidx, 6);
 }
 
 // ---------------------------------------------------------------------------
@@ -492,15 +474,6 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   hipLaunchKernelGGL(panel_rows_kernel<T>, dim3(nch), dim3(256), 0, st_rows, K, ld, N, k0, ce, (const T*)D,
                      (const T*)Lb0, Wp, ldw, area, err, rows_prev ? Wprev : nullptr, ldw, kprev, boprev);
   return hipGetLastError();
-}
-hipError_t panel_stamps(unsigned long long* out, bool reset) {
-  if (reset) {
-    static unsigned long long init[128][8];
-    for (int p = 0; p < 128; ++p)
-      for (int i = 0; i < 8; ++i) init[p][i] = (i == 0 || i == 2 || i == 4) ? ~0ull : 0ull;
-    return hipMemcpyToSymbol(HIP_SYMBOL(g_pstamp), init, sizeof(init));
-  }
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamp), sizeof(unsigned long long) * 128 * 8);
 }
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
                         int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,

@@ -35,7 +35,7 @@ SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_
 
 EXPORTS = [
     "ipmz_ctx_create", "ipmz_ctx_destroy", "ipmz_ctx_set_stream", "ipmz_ctx_reset_stream", "ipmz_ctx_sync", "ipmz_last_error",
-    "ipmz_ctx_set_blocking", "ipmz_ldlt_workspace_bytes", "ipmz_ldlt_factor", "ipmz_ldlt_solve",
+    "ipmz_ctx_set_blocking", "ipmz_ctx_get_blocking", "ipmz_ldlt_workspace_bytes", "ipmz_ldlt_factor", "ipmz_ldlt_solve",
     "ipmz_ldlt_prepare_solve", "ipmz_ldlt_decomposition", "ipmz_overwriting_solve_ldlt", "ipmz_qp_create",
     "ipmz_qp_destroy", "ipmz_qp_load_host", "ipmz_qp_generate", "ipmz_qp_step", "ipmz_qp_scalars",
     "ipmz_qp_device_scalars", "ipmz_qp_copy_scalars", "ipmz_qp_solve", "ipmz_qp_state_len", "ipmz_qp_get_state", "ipmz_qp_set_state",
@@ -90,6 +90,7 @@ def _load():
         "ipmz_ctx_sync": ([_VP], _I),
         "ipmz_last_error": ([], ctypes.c_char_p),
         "ipmz_ctx_set_blocking": ([_VP, _I, _I], _I),
+        "ipmz_ctx_get_blocking": ([_VP, _I, ctypes.POINTER(_I), ctypes.POINTER(_I)], _I),
         "ipmz_ldlt_workspace_bytes": ([_VP, _I], _I64),
         "ipmz_ldlt_factor": ([_VP, _I, _VP, _I64, _VP, _VP, _I64], _I),
         "ipmz_ldlt_solve": ([_VP, _I, _VP, _I64, _VP, _VP, _VP], _I),
@@ -180,6 +181,12 @@ class Context:
 
     def set_blocking(self, nbo, nbi):
         _check(lib.ipmz_ctx_set_blocking(self.h, nbo, nbi), "ipmz_ctx_set_blocking")
+
+    def blocking(self, N):
+        """(nbo, nbi) an order-N factor uses with this context."""
+        nbo, nbi = _I(0), _I(0)
+        _check(lib.ipmz_ctx_get_blocking(self.h, N, ctypes.byref(nbo), ctypes.byref(nbi)), "ipmz_ctx_get_blocking")
+        return nbo.value, nbi.value
 
     def sync(self):
         """Synchronize; raises IpmzError when the last device-memory factor /

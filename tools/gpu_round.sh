@@ -30,9 +30,6 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmc_write) step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
-    kpersist) step kgvar 300 ipm-zoo_amd/build/kbench 11264 gvar 15 30 31 32 33; for P in 248 256 384; do KB_PERSIST=$P step kpersist$P 300 ipm-zoo_amd/build/kbench 11264 factor 384 256; done ;;
-    kstamps) KB_STAMPS=1 step kstamps 300 ipm-zoo_amd/build/kbench 11264 factor 384 ;;
-    kmask) for R in 8 16 32; do KB_RESERVE=$R step kmask$R 300 ipm-zoo_amd/build/kbench 11264 factor 384; KB_RESERVE=$R KB_MASK_A=1 step kmaskA$R 300 ipm-zoo_amd/build/kbench 11264 factor 384; done ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;
     counters) step counters 120 rocprofv3 -L ;;
     ktrace) step ktrace 300 rocprofv3 --kernel-trace -d "$OUT/ktrace" -o run --output-format csv -- ipm-zoo_amd/build/kbench 11264 factor 384 ;;

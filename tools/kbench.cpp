@@ -169,43 +169,20 @@ int main(int argc, char** argv) {
   }
   // factor: the look-ahead factor (panel path on a high-priority stream,
   // trailing updates on a low-priority one) and the persistent solve.
-  // (Measured and dropped: s_setprio on the panel / look-ahead strip waves,
-  // and CU masks reserving 16 / 32 CUs for the panel stream -- no gain.)
+  // (Measured and dropped: CU masks reserving 8 / 16 / 32 CUs for the panel
+  // streams, a persistent trailing-GEMM grid of 248-512 workgroups -- no gain.)
   std::vector<hipEvent_t> ev(3 * (N / 64 + 2) + 8);
   for (size_t i = 0; i < ev.size(); ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   int lo = 0, hi = 0;
   CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
   hipStream_t sA, sB, sC;
-  // KB_RESERVE=R: R CUs (every ncu/R-th) masked off the trailing (B) and rows
-  // (C) streams; KB_MASK_A=1 confines the chain stream (A) to them
-  const int reserve = std::getenv("KB_RESERVE") ? std::atoi(std::getenv("KB_RESERVE")) : 0;
-  const bool mask_a = std::getenv("KB_MASK_A") && std::atoi(std::getenv("KB_MASK_A"));
-  int ncu = 0;
-  CK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, 0));
-  std::vector<uint32_t> mRest((ncu + 31) / 32, 0u), mRes((ncu + 31) / 32, 0u);
-  for (int c = 0; c < ncu; ++c) {
-    const bool r = reserve && c % (ncu / reserve) == 0;
-    (r ? mRes : mRest)[c / 32] |= 1u << (c % 32);
-  }
-  if (reserve) {
-    if (mask_a) CK(hipExtStreamCreateWithCUMask(&sA, (uint32_t)mRes.size(), mRes.data()));
-    else CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
-    CK(hipExtStreamCreateWithCUMask(&sB, (uint32_t)mRest.size(), mRest.data()));
-    CK(hipExtStreamCreateWithCUMask(&sC, (uint32_t)mRest.size(), mRest.data()));
-    std::printf("CU reserve %d (mask A %d)\n", reserve, (int)mask_a);
-  } else {
-    CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
-    CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
-    CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
-  }
-  const int persist = std::getenv("KB_PERSIST") ? std::atoi(std::getenv("KB_PERSIST")) : 0;
-  ipmz::set_trail_persist(persist);
-  if (persist) std::printf("persistent trailing GEMM: %d workgroups\n", persist);
+  CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+  CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+  CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
   for (int a = 3; a < argc || a == 3; ++a) {
     const int nbo = argc > a ? std::atoi(argv[a]) : 384;
     float best = 1e30f;
     for (int rep = 0; rep < 3; ++rep) {
-      CK(ipmz::panel_stamps(nullptr, true));
       hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, sA, K, ld, N, 7ull);
       CK(hipMemsetAsync(pctrl, 0, ipmz::panel_ctrl_words(N, 64) * 4, sA));
       CK(hipStreamSynchronize(sA));
@@ -219,17 +196,6 @@ int main(int argc, char** argv) {
       if (rep) best = fms < best ? fms : best;
     }
     CK(hipStreamSynchronize(sB));
-    if (std::getenv("KB_STAMPS")) {  // per panel: chain / helpers / rows start-end (us from chain 0 start)
-      static unsigned long long stp[128][8];
-      CK(ipmz::panel_stamps(&stp[0][0], false));
-      const double t0 = (double)stp[0][0];
-      std::printf("panel  chain[start end]  helpers[start end]  rows[start prologue end]  (us)\n");
-      for (int p = 0; p * nbo < N && p < 128; ++p) {
-        auto us = [&](int i) { return (stp[p][i] == ~0ull || stp[p][i] == 0) ? -1.0 : ((double)stp[p][i] - t0) / 100.0; };
-        std::printf("%3d  %8.1f %8.1f   %8.1f %8.1f   %8.1f %8.1f %8.1f\n", p, us(0), us(1), us(2), us(3), us(4), us(5),
-                    us(6));
-      }
-    }
     unsigned hc[IPMZ_PANEL_CTRL_WORDS];
     CK(hipMemcpy(hc, pctrl, sizeof(hc), hipMemcpyDeviceToHost));
     std::printf("look-ahead factor N=%d nbo=%d: %.3f ms = %.2f TFLOP/s%s\n", N, nbo, best,
