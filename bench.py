@@ -19,7 +19,10 @@ Multi-GPU (torchrun, one process per GPU):
   * "batched" sub-object (C4, BASELINE.json configs[3]): the 1024-QP batch
     (n=256, m=64) sharded over the ranks, strong scaling, with ONE all-reduce
     (MAX) of the device-computed convergence summary per step -- the only
-    collective.
+    collective (SURVEY.md §8e);
+  * "configs" sub-object (default c3 run): C2 (normal equations, n=2048) and
+    C5 (n=16384, fp32 factor + fp64 refinement), replicas like the headline,
+    each with its own roofline and CPU baseline (--no-configs skips them).
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--workload c3|c2|c4|c5|...]
 """
@@ -36,6 +39,7 @@ sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
 FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix peak (BASELINE.md "Peaks")
 FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X f32-input MFMA peak (MI355X_MICROARCH.md, Matrix cores)
 
+HEADLINE_METRIC = "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X"  # BASELINE.json metric
 WORKLOADS = {
     "c3": dict(n=8192, m=2048, p=1024, sample_scale=2, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
                                           "(Regularization), augmented LDL^T, KKT N=11264"),
@@ -146,6 +150,106 @@ def run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch):
     return out
 
 
+def run_single(I, ctx, args, world, dist, torch, workload):
+    """One QP per rank (replicas): the timed HIP-graph pass, then the
+    instrumented pass for the phase split and the roofline."""
+    wl = WORKLOADS[workload]
+    n, m, p = wl["n"], wl["m"], wl["p"]
+    Nk = n + m + p
+    mixed = wl.get("mixed", False)
+    peak = FP32_MFMA_PEAK_TFLOPS if mixed else FP64_MFMA_PEAK_TFLOPS
+    rank = dist.get_rank() if world > 1 else 0
+    qp = I.Optimizer(n, m, p, ctx)
+    qp.generate(1234 + rank)
+    if mixed:
+        qp.set_mixed_precision(True, args.ir_tol, 20)
+    if wl.get("normal"):
+        qp.set_reduction(I.REDUCTION_NORMAL)
+    flags = I.STEP_RESTART_IF_CONVERGED | I.STEP_GRAPH
+    for _ in range(args.warmup):
+        qp.step(flags)
+    elapsed = timed(world, dist, torch, args.steps, lambda: qp.step(flags))
+    ph = None
+    if not args.no_instrumented:
+        qp.set_timing(True)  # resets the phase accumulators; eager launches with HIP events
+        t_ins = timed(world, dist, torch, args.steps, lambda: qp.step(I.STEP_RESTART_IF_CONVERGED))
+        ph = qp.phase_times()
+    s = qp.scalars()
+    out = {
+        "metric": (HEADLINE_METRIC if workload == "c3" else
+                   f"Newton steps/sec + factor TFLOP/s, {workload.upper()}: {wl['desc']}"),
+        "value": args.steps * world / elapsed,
+        "unit": "steps/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 factor + f64 refinement" if mixed else "f64",
+        "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; seed 1234+rank)",
+        "config": {"workload": workload, "n": n, "m": m, "p": p, "kkt_N": Nk,
+                   "formulation": ("SlackedSlacks box-only, fp32 LDL^T of S K S + fp64 iterative refinement "
+                                   f"(tol {args.ir_tol:g})") if mixed else
+                                  ("SlackedSlacks" + (" ineq" if m else " box-only") +
+                                   (" + Regularization eq (delta=1e-4)" if p else "") +
+                                   (", normal equations (Cholesky H, S)" if wl.get("normal") else
+                                    ", augmented LDL^T")),
+                   "parallelism": f"replicas x{world} (independent QPs, one per GPU)",
+                   "blocking": dict(zip(("nbo", "nbi"), ctx.blocking(Nk))),
+                   "timing": "HIP-graph replay of the whole step (production path); phases from a second, "
+                             "instrumented pass",
+                   "description": wl["desc"]},
+        "restarts": s["restarts"],
+    }
+    if mixed:  # refinement corrections of the last step's two solves
+        out["ir"] = {"iters_affine": s["ir_iters_aff"], "iters_corrector": s["ir_iters"],
+                     "ratio_affine": s["ir_ratio_aff"], "ratio_corrector": s["ir_ratio"]}
+    if ph:
+        k = args.steps
+        factor_ms = ph["factor"] / k
+        out["value_instrumented"] = k * world / t_ins
+        out["factor_tflops"] = (Nk ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
+        out["phase_ms_per_step"] = {kk: ph[kk] / k for kk in ("step", "assemble", "factor", "solve", "eval")}
+        if wl.get("normal"):
+            fl = n ** 3 / 3.0 + n * n * (m + p) + n * (m + p) ** 2 + (m + p) ** 3 / 3.0
+            what = "normal-equations factor phase: LDL^T(H) + TRSM + SYRK + LDL^T(S)"
+        else:
+            fl = Nk ** 3 / 3.0
+            what = ("blocked LDL^T factor phase (" + ("fp32 " if mixed else "fp64 ") +
+                    "MFMA; outer-panel and trailing/strip GEMM launches on two streams)")
+        ach = fl / (factor_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": what, "achieved": ach, "peak": peak, "unit": "TFLOP/s",
+                "frac": ach / peak, "traffic": None,
+                "note": "algorithmic flops (N^3/3 for LDL^T, SURVEY.md §8d) over the factor phase time "
+                        "(HIP events on the solver stream around the phase)"}
+        ftr = load_json(f"profiles/factor_traffic_{workload}.json")
+        if ftr:
+            roof["traffic"] = ftr.get("factor_traffic_bytes_per_step")
+            roof["traffic_source"] = ftr["source"]
+            roof["mfma"] = ftr.get("mfma")
+        tr_s = ph["trailing"] * 1e-3
+        launches = ph["trailing_launches"]
+        if launches:
+            trk = load_json("profiles/pmc_traffic.json") if workload == "c3" else None
+            tach = ph["trailing_flops"] / tr_s / 1e12
+            roof["trailing"] = {
+                "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB,"
+                           f"{'2,4' if mixed else '4,4'}> (trailing update A22 -= W21 L21^T)"),
+                "achieved": tach, "peak": peak, "unit": "TFLOP/s", "frac": tach / peak,
+                "traffic": trk.get("traffic_bytes_per_launch") if trk else None,
+                "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)",
+                "traffic_source": trk.get("source") if trk else None,
+                "algorithmic_bytes_per_launch": trk.get("algorithmic_bytes_per_launch") if trk else None,
+                "launches": launches, "avg_launch_ms": ph["trailing"] / launches,
+                "flops_per_launch": ph["trailing_flops"] / launches,
+            }
+        out["roofline"] = roof
+    qp.close()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -157,6 +261,7 @@ def main():
     ap.add_argument("--nbi", type=int, default=int(os.environ.get("IPMZ_NBI", 64)))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-batched", action="store_true", help="skip the C4 'batched' sub-object")
+    ap.add_argument("--no-configs", action="store_true", help="c3: skip the C2 / C5 'configs' sub-objects")
     ap.add_argument("--no-instrumented", action="store_true", help="skip the per-phase HIP-event pass")
     ap.add_argument("--ir-tol", type=float, default=1e-12, help="c5: refinement tolerance")
     ap.add_argument("--batch", type=int, default=0, help="c4: override the global batch (e.g. 128 = one rank's "
@@ -186,15 +291,11 @@ def main():
     import ipmz_amd as I
 
     wl = WORKLOADS[args.workload]
-    n, m, p = wl["n"], wl["m"], wl["p"]
-    Nk = n + m + p
     stream = torch.cuda.current_stream()
     ctx = I.Context(local_rank, stream=stream.cuda_stream, nbo=args.nbo, nbi=args.nbi)
     nbatch = wl.get("batch", 0)
     if nbatch and args.batch:
         nbatch = args.batch
-    mixed = wl.get("mixed", False)
-    peak = FP32_MFMA_PEAK_TFLOPS if mixed else FP64_MFMA_PEAK_TFLOPS
 
     if nbatch:  # C4 as the headline
         head = run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch)
@@ -204,100 +305,19 @@ def main():
         out["config"]["description"] = wl["desc"]
         out["config"]["formulation"] = "SlackedSlacks ineq, augmented LDL^T"
     else:
-        qp = I.Optimizer(n, m, p, ctx)
-        qp.generate(1234 + rank)
-        if mixed:
-            qp.set_mixed_precision(True, args.ir_tol, 20)
-        if wl.get("normal"):
-            qp.set_reduction(I.REDUCTION_NORMAL)
-        flags = I.STEP_RESTART_IF_CONVERGED | I.STEP_GRAPH
-        for _ in range(args.warmup):
-            qp.step(flags)
-        elapsed = timed(world, dist, torch, args.steps, lambda: qp.step(flags))
-        ph = None
-        if not args.no_instrumented:
-            qp.set_timing(True)  # resets the phase accumulators; eager launches with HIP events
-            t_ins = timed(world, dist, torch, args.steps, lambda: qp.step(I.STEP_RESTART_IF_CONVERGED))
-            ph = qp.phase_times()
-        s = qp.scalars()
-        out = {
-            "metric": "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X",
-            "value": args.steps * world / elapsed,
-            "unit": "steps/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": 1e3 * elapsed / args.steps,
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32 factor + f64 refinement" if mixed else "f64",
-            "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; seed 1234+rank)",
-            "config": {"workload": args.workload, "n": n, "m": m, "p": p, "kkt_N": Nk,
-                       "formulation": ("SlackedSlacks box-only, fp32 LDL^T of S K S + fp64 iterative refinement "
-                                       f"(tol {args.ir_tol:g})") if mixed else
-                                      ("SlackedSlacks" + (" ineq" if m else " box-only") +
-                                       (" + Regularization eq (delta=1e-4)" if p else "") +
-                                       (", normal equations (Cholesky H, S)" if wl.get("normal") else
-                                        ", augmented LDL^T")),
-                       "parallelism": f"replicas x{world} (independent QPs, one per GPU)",
-                       "blocking": dict(zip(("nbo", "nbi"), ctx.blocking(Nk))),
-                       "timing": "HIP-graph replay of the whole step (production path); phases from a second, "
-                                 "instrumented pass",
-                       "description": wl["desc"]},
-            "restarts": s["restarts"],
-        }
-        if mixed:  # refinement corrections of the last step's two solves
-            out["ir"] = {"iters_affine": s["ir_iters_aff"], "iters_corrector": s["ir_iters"],
-                         "ratio_affine": s["ir_ratio_aff"], "ratio_corrector": s["ir_ratio"]}
-        if ph:
-            k = args.steps
-            factor_ms = ph["factor"] / k
-            out["value_instrumented"] = k * world / t_ins
-            out["factor_tflops"] = (Nk ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
-            out["phase_ms_per_step"] = {kk: ph[kk] / k for kk in ("step", "assemble", "factor", "solve", "eval")}
-            if wl.get("normal"):
-                fl = n ** 3 / 3.0 + n * n * (m + p) + n * (m + p) ** 2 + (m + p) ** 3 / 3.0
-                what = "normal-equations factor phase: LDL^T(H) + TRSM + SYRK + LDL^T(S)"
-            else:
-                fl = Nk ** 3 / 3.0
-                what = ("blocked LDL^T factor phase (" + ("fp32 " if mixed else "fp64 ") +
-                        "MFMA; outer-panel and trailing/strip GEMM launches on two streams)")
-            ach = fl / (factor_ms * 1e-3) / 1e12
-            roof = {"bound": "mfma", "kernel": what, "achieved": ach, "peak": peak, "unit": "TFLOP/s",
-                    "frac": ach / peak, "traffic": None,
-                    "note": "algorithmic flops (N^3/3 for LDL^T, SURVEY.md §8d) over the factor phase time "
-                            "(HIP events on the solver stream around the phase)"}
-            ftr = load_json(f"profiles/factor_traffic_{args.workload}.json")
-            if ftr:
-                roof["traffic"] = ftr.get("factor_traffic_bytes_per_step")
-                roof["traffic_source"] = ftr["source"]
-                roof["mfma"] = ftr.get("mfma")
-            tr_s = ph["trailing"] * 1e-3
-            launches = ph["trailing_launches"]
-            if launches:
-                trk = load_json("profiles/pmc_traffic.json") if args.workload == "c3" else None
-                tach = ph["trailing_flops"] / tr_s / 1e12
-                roof["trailing"] = {
-                    "kernel": (f"gemm_nt_kernel<{'float' if mixed else 'double'},128,128,EPI_SUB,"
-                               f"{'2,4' if mixed else '4,4'}> (trailing update A22 -= W21 L21^T)"),
-                    "achieved": tach, "peak": peak, "unit": "TFLOP/s", "frac": tach / peak,
-                    "traffic": trk.get("traffic_bytes_per_launch") if trk else None,
-                    "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)",
-                    "traffic_source": trk.get("source") if trk else None,
-                    "algorithmic_bytes_per_launch": trk.get("algorithmic_bytes_per_launch") if trk else None,
-                    "launches": launches, "avg_launch_ms": ph["trailing"] / launches,
-                    "flops_per_launch": ph["trailing_flops"] / launches,
-                }
-            out["roofline"] = roof
-        qp.close()
+        out = run_single(I, ctx, args, world, dist, torch, args.workload)
         if not args.no_batched:
             out["batched"] = run_batched(I, ctx, args, world, rank, dist, torch, WORKLOADS["c4"], 1024)
+        if args.workload == "c3" and not args.no_configs:
+            # the other single-GPU configs of BASELINE.json, each its own line item
+            out["configs"] = {w: run_single(I, ctx, args, world, dist, torch, w) for w in ("c2", "c5")}
     if rank == 0:
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(wl)
             if "batched" in out:
                 out["batched"]["cpu_baseline"] = cpu_baseline(WORKLOADS["c4"])
+            for w, sub in out.get("configs", {}).items():
+                sub["cpu_baseline"] = cpu_baseline(WORKLOADS[w])
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -173,10 +173,10 @@ int ipmz_ctx_get_blocking(ipmz_ctx* ctx, int N, int* nbo, int* nbi) {
 
 // ---------------------------------------------------------------------------
 // Workspace: [info int (256 B)] [panel ctrl words] [side 2*nbi] [Linv nblk*nbi^2] [W 3*N*nbo]
-//            [ybuf N] [zbuf N] [ctrl: ticket, sticky error]
+//            [ybuf N] [zbuf N] [solve ctrl words] [solve prep (nbi 64): X, X^T, M, Q per 128-row block]
 namespace {
 struct WsLayout {
-  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, total;
+  int64_t info_off, pctrl_off, side_off, linv_off, w_off, y_off, z_off, ctrl_off, prep_off, total;
 };
 WsLayout ws_layout(int N, int nbo, int nbi) {
   WsLayout l;
@@ -189,7 +189,8 @@ WsLayout ws_layout(int N, int nbo, int nbi) {
   l.y_off = l.w_off + round_up(3 * (int64_t)N * nbo * 8, 256);  // W triple-buffered (look-ahead)
   l.z_off = l.y_off + round_up((int64_t)N * 8, 256);
   l.ctrl_off = l.z_off + round_up((int64_t)N * 8, 256);
-  l.total = l.ctrl_off + 256;
+  l.prep_off = l.ctrl_off + 256;
+  l.total = l.prep_off + (nbi == 64 ? round_up(solve_prep_elems(N) * 8, 256) : 0);
   return l;
 }
 // the solve: one persistent launch for nbi == 64 (trsv_persist.hip), else
@@ -200,9 +201,9 @@ hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const c
   char* w = const_cast<char*>(ws);
   const double* Linv = reinterpret_cast<const double*>(w + l.linv_off);
   if (nbi == 64)
-    return ldlt_solve_persistent(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.y_off),
-                                 reinterpret_cast<double*>(w + l.z_off), reinterpret_cast<unsigned*>(w + l.ctrl_off),
-                                 st);
+    return ldlt_solve_persistent(K, ld, N, D, reinterpret_cast<const double*>(w + l.prep_off), b,
+                                 reinterpret_cast<double*>(w + l.y_off), reinterpret_cast<double*>(w + l.z_off),
+                                 reinterpret_cast<unsigned*>(w + l.ctrl_off), st);
   return ldlt_solve(K, ld, N, D, Linv, nbi, b, reinterpret_cast<double*>(w + l.side_off), st);
 }
 // Sticky error words of a workspace (synchronizes): a spin that timed out in
@@ -235,12 +236,18 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
   HIP_OK(hipMemsetAsync(pctrl, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * sizeof(unsigned), ctx->stream));
-  HIP_OK(hipMemsetAsync(ws + l.ctrl_off, 0, 2 * sizeof(unsigned), ctx->stream));  // solve: ticket + sticky error
+  HIP_OK(hipMemsetAsync(ws + l.ctrl_off, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), ctx->stream));  // solve
   const int nbo = nbo_for(ctx, N);
   const int npan = (N + nbo - 1) / nbo;
+  // the persistent solve's per-block operators, built once from this factor
+  auto prep = [&]() -> hipError_t {
+    return ctx->nbi == 64 ? solve_prep(K, ld, N, Linv, reinterpret_cast<double*>(ws + l.prep_off), ctx->stream)
+                          : hipSuccess;
+  };
   if (npan < 3) {
     HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, nullptr, 0,
                        pctrl));
+    HIP_OK(prep());
     return IPMZ_OK;
   }
   const int nev = 3 * npan + 4;
@@ -257,6 +264,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   // join (A has already waited for B's tail)
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  HIP_OK(prep());
   return IPMZ_OK;
 }
 
@@ -301,10 +309,13 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
   const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
   HIP_OK(linv_from_l(L, ld, N, ctx->nbi, reinterpret_cast<double*>(static_cast<char*>(ws) + l.linv_off),
                      ctx->stream));
+  if (ctx->nbi == 64)
+    HIP_OK(solve_prep(L, ld, N, reinterpret_cast<const double*>(static_cast<char*>(ws) + l.linv_off),
+                      reinterpret_cast<double*>(static_cast<char*>(ws) + l.prep_off), ctx->stream));
   // no factorization ran in this workspace: clear its sticky error words
   HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * 4,
                         ctx->stream));
-  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.ctrl_off, 0, 8, ctx->stream));
+  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.ctrl_off, 0, IPMZ_SOLVE_CTRL_WORDS * 4, ctx->stream));
   return IPMZ_OK;
 }
 
@@ -316,6 +327,7 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
   const int npan = (w.N + w.nbo - 1) / w.nbo;
   if (npan < 3) {
     HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, nullptr, 0, timer));
+    HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
     return IPMZ_OK;
   }
   const int nev = 3 * npan + 4;
@@ -329,6 +341,7 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
   HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer));
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
   return IPMZ_OK;
 }
 

@@ -5,6 +5,8 @@
 
 #define IPMZ_NBO_MAX 512
 #define IPMZ_PANEL_CTRL_WORDS 256
+#define IPMZ_SOLVE_BLOCK 128     // rows per block of the persistent solve
+#define IPMZ_SOLVE_CTRL_WORDS 8  // its control words (error, tickets, sweep counters)
 
 namespace ipmz {
 
@@ -93,21 +95,27 @@ hipError_t ldlt_solve(const double* K, int64_t ld, int N, const double* D, const
 hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
                               double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st);
 
-// trsv_persist.hip: the same solve as ONE persistent launch (nbi == 64);
-// ybuf, zbuf: N doubles; ctrl: 2 unsigned (ticket counter zeroed inside,
-// ctrl[1] a sticky error word the caller clears).
-hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* Linv, int nbi,
-                                 double* b, double* ybuf, double* zbuf, unsigned* ctrl, hipStream_t st);
+// trsv_persist.hip: the same solve as ONE persistent launch on 128-row
+// blocks (nbi == 64 factors).  P: solve_prep_elems(N) elements written by
+// solve_prep from the factor's 64 x 64 inverses (once per factorization);
+// ybuf, xbuf: N elements; ctrl: IPMZ_SOLVE_CTRL_WORDS unsigned (counters
+// zeroed inside, ctrl[SOLVE_ERR_WORD] a sticky error word the caller clears).
+int64_t solve_prep_elems(int N);
+hipError_t solve_stamps(unsigned long long* out);  // DEBUG
+hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, double* P, hipStream_t st);
+hipError_t solve_prep(const float* K, int64_t ld, int N, const float* Linv, float* P, hipStream_t st);
+hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* P, double* b,
+                                 double* ybuf, double* xbuf, unsigned* ctrl, hipStream_t st);
 // fp32 variant; skip (device flag, may be null): return at once when set
-hipError_t ldlt_solve_persistent(const float* K, int64_t ld, int N, const float* D, const float* Linv, int nbi,
-                                 float* b, float* ybuf, float* zbuf, unsigned* ctrl, hipStream_t st,
+hipError_t ldlt_solve_persistent(const float* K, int64_t ld, int N, const float* D, const float* P, float* b,
+                                 float* ybuf, float* xbuf, unsigned* ctrl, hipStream_t st,
                                  const unsigned* skip = nullptr);
 
 // mixed.hip: fp32 factor of S K S + fp64 iterative refinement (config C5) ----
 struct MixedWs {
   int N = 0, nbo = 256;
   int64_t ld32 = 0;
-  float *K32 = nullptr, *D32 = nullptr, *Linv32 = nullptr, *W32 = nullptr;
+  float *K32 = nullptr, *D32 = nullptr, *Linv32 = nullptr, *W32 = nullptr, *P32 = nullptr;
   float *y32 = nullptr, *z32 = nullptr, *r32 = nullptr;
   unsigned *ctrl = nullptr, *state = nullptr, *pctrl = nullptr;
   int* info = nullptr;

@@ -211,7 +211,8 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   w.y32 = reinterpret_cast<float*>(take((int64_t)N * 4));
   w.z32 = reinterpret_cast<float*>(take((int64_t)N * 4));
   w.r32 = reinterpret_cast<float*>(take((int64_t)N * 4));
-  w.ctrl = reinterpret_cast<unsigned*>(take(2 * 4));
+  w.ctrl = reinterpret_cast<unsigned*>(take(IPMZ_SOLVE_CTRL_WORDS * 4));
+  w.P32 = reinterpret_cast<float*>(take(solve_prep_elems(N) * 4));
   w.state = reinterpret_cast<unsigned*>(take(64));
   w.info = reinterpret_cast<int*>(take(64));
   w.pctrl = reinterpret_cast<unsigned*>(take(panel_ctrl_words(N, nbo) * 4));
@@ -234,7 +235,7 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   hipError_t e = hipMemsetAsync(w.info, 0x7f, sizeof(int), st);
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(w.pctrl, 0, panel_ctrl_words(N, w.nbo) * sizeof(unsigned), st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(w.ctrl, 0, 2 * sizeof(unsigned), st)) != hipSuccess) return e;  // solve: counter + error
+  if ((e = hipMemsetAsync(w.ctrl, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), st)) != hipSuccess) return e;
   return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, st3, ev, nev,
                      w.pctrl);
 }
@@ -247,7 +248,7 @@ hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, doubl
   const dim3 gv((N + MNT - 1) / MNT), bt(MNT);
   hipLaunchKernelGGL(k_mx_begin, gv, bt, 0, st, N, b, w.s, w.x, w.r32, w.state);
   for (int it = 0; it <= max_refine; ++it) {
-    hipError_t e = ldlt_solve_persistent(w.K32, w.ld32, N, w.D32, w.Linv32, 64, w.r32, w.y32, w.z32, w.ctrl, st,
+    hipError_t e = ldlt_solve_persistent(w.K32, w.ld32, N, w.D32, w.P32, w.r32, w.y32, w.z32, w.ctrl, st,
                                          it ? w.state : nullptr);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_mx_accum, gv, bt, 0, st, N, w.s, w.r32, w.x, w.state);

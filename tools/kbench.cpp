@@ -202,10 +202,28 @@ int main(int argc, char** argv) {
                 (double)N * N * N / 3.0 / best / 1e9, hc[ipmz::PANEL_ERR_WORD] ? " PANEL ERROR" : "");
   }
   CK(hipMemsetAsync(b, 0, N * 8, st));
-  CK(ipmz::ldlt_solve_persistent(K, ld, N, D, Linv, 64, b, yb, xb, ctrl, st));
+  double* P;
+  CK(hipMalloc(&P, ipmz::solve_prep_elems(N) * 8));
+  CK(hipMemsetAsync(ctrl, 0, 256, st));
   t.start(st);
-  for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve_persistent(K, ld, N, D, Linv, 64, b, yb, xb, ctrl, st));
+  CK(ipmz::solve_prep(K, ld, N, Linv, P, st));
+  const float pms = t.stop(st);
+  CK(ipmz::ldlt_solve_persistent(K, ld, N, D, P, b, yb, xb, ctrl, st));
+  t.start(st);
+  for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve_persistent(K, ld, N, D, P, b, yb, xb, ctrl, st));
   const float sms = t.stop(st) / 5;
+  {
+    static unsigned long long stp[2][256][4];
+    CK(ipmz::solve_stamps(&stp[0][0][0]));
+    const double t0 = (double)stp[0][0][0];
+    std::printf("fwd block: start bulkdone critin stored (us from block 0 start)\n");
+    for (int j = 0; j < (N + 127) / 128 && j < 256; ++j)
+      std::printf("%3d %8.2f %8.2f %8.2f %8.2f\n", j, (stp[0][j][0] - t0) / 100.0, (stp[0][j][1] - t0) / 100.0,
+                  (stp[0][j][2] - t0) / 100.0, (stp[0][j][3] - t0) / 100.0);
+  }
+  unsigned hctrl[8];
+  CK(hipMemcpy(hctrl, ctrl, sizeof(hctrl), hipMemcpyDeviceToHost));
+  std::printf("solve prep N=%d: %.3f ms%s\n", N, pms, hctrl[ipmz::SOLVE_ERR_WORD] ? " SOLVE ERROR" : "");
   std::printf("persistent solve N=%d: %.3f ms (%.2f TB/s over the 2 x N^2/2 x 8 B of L)\n", N, sms,
               8.0 * N * (double)N / sms / 1e9);
   std::printf("done\n");
