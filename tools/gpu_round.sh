@@ -28,6 +28,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
     # HBM traffic: one counter group per pass (MI355X_MICROARCH.md, rocprofv3 PMC slots)
     pmc_fetch) step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_write) step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
+    # factor-phase counters of ONE bench step (tools/pmc_factor.py), one counter group per pass
+    pmcf_fetch) step pmcf_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_write) step pmcf_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcf_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_mfma) step pmcf_mfma 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES -d "$OUT/pmcf_mfma" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;

@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Per-step HBM traffic and MFMA counters of the factorization phase, from
+separate rocprofv3 --pmc passes of ONE bench step
+(`bench.py --steps 1 --warmup 0 --no-instrumented --no-batched --no-configs
+--no-cpu-baseline`, see tools/gpu_round.sh steps pmcf_*):
+
+    pass fetch : FETCH_SIZE
+    pass write : WRITE_SIZE
+    pass mfma  : SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES
+
+The factor phase = every launch of the factor's kernels (trailing / strip
+GEMMs, the panel chain and rows launches, the solve prep).  Corrections
+(MI355X_MICROARCH.md, HBM / PMC): FETCH_SIZE and WRITE_SIZE are KiB,
+FETCH_SIZE reports half the bytes of a 16-B/lane read on gfx950 (doubled);
+SQ_INSTS_VALU_MFMA_MOPS_F64 counts 512-flop units.
+
+    python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir> <label> <N> > profiles/factor_traffic_c3.json
+"""
+import csv
+import json
+import sys
+from collections import defaultdict
+
+FACTOR_KERNELS = ("gemm_nt_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel")
+
+
+def load(d):
+    per = defaultdict(lambda: defaultdict(float))  # kernel -> counter -> sum over launches
+    launches = defaultdict(set)
+    for r in csv.DictReader(open(f"{d}/run_counter_collection.csv")):
+        name = r["Kernel_Name"].split("(")[0]
+        if not any(k in name for k in FACTOR_KERNELS):
+            continue
+        per[name][r["Counter_Name"]] += float(r["Counter_Value"])
+        launches[name].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+    return per, {k: len(v) for k, v in launches.items()}
+
+
+def main():
+    fetch, nf = load(sys.argv[1])
+    write, _ = load(sys.argv[2])
+    mfma, _ = load(sys.argv[3])
+    label = sys.argv[4] if len(sys.argv) > 4 else ""
+    N = int(sys.argv[5]) if len(sys.argv) > 5 else 11264
+    kernels = sorted(set(fetch) | set(write) | set(mfma))
+    rows = {}
+    tot = defaultdict(float)
+    for k in kernels:
+        fb = 2.0 * fetch[k].get("FETCH_SIZE", 0.0) * 1024
+        wb = write[k].get("WRITE_SIZE", 0.0) * 1024
+        mops = mfma[k].get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)
+        row = {"launches": nf.get(k, 0), "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+               "f64_mfma_flops": 512.0 * mops,
+               "mfma_busy_cycles": mfma[k].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0),
+               "grbm_gui_active": mfma[k].get("GRBM_GUI_ACTIVE", 0.0),
+               "busy_cu_cycles": mfma[k].get("SQ_BUSY_CU_CYCLES", 0.0)}
+        rows[k] = row
+        for f in ("fetch_bytes", "write_bytes", "hbm_bytes", "f64_mfma_flops", "mfma_busy_cycles", "busy_cu_cycles"):
+            tot[f] += row[f]
+    alg_flops = N ** 3 / 3.0
+    out = {
+        "profile": label,
+        "N": N,
+        "factor_traffic_bytes_per_step": tot["hbm_bytes"],
+        "mfma": {
+            "f64_mfma_flops_per_step": tot["f64_mfma_flops"],
+            "algorithmic_flops_per_step": alg_flops,
+            "executed_over_algorithmic": tot["f64_mfma_flops"] / alg_flops if alg_flops else None,
+            "mfma_busy_cycles": tot["mfma_busy_cycles"],
+            "busy_cu_cycles": tot["busy_cu_cycles"],
+            "mfma_busy_over_busy_cu": (tot["mfma_busy_cycles"] / tot["busy_cu_cycles"]
+                                       if tot["busy_cu_cycles"] else None),
+        },
+        "per_kernel": rows,
+        "note": "one bench step (one factorization), separate --pmc passes, counters summed over the factor's "
+                "launches; FETCH_SIZE x2 + WRITE_SIZE (KiB -> B); MFMA flops = 512 x SQ_INSTS_VALU_MFMA_MOPS_F64 "
+                "(executed, incl. the masked upper halves of diagonal tiles); mfma_busy_over_busy_cu = "
+                "SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CU_CYCLES as reported (both summed over the chip)",
+    }
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
