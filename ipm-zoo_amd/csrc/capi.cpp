@@ -236,7 +236,8 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
   HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
   HIP_OK(hipMemsetAsync(pctrl, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * sizeof(unsigned), ctx->stream));
-  HIP_OK(hipMemsetAsync(ws + l.ctrl_off, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), ctx->stream));  // solve
+  HIP_OK(solve_reset(ws + l.y_off, ws + l.z_off, sizeof(double), N, reinterpret_cast<unsigned*>(ws + l.ctrl_off),
+                     ctx->stream));  // the persistent solve's state for this factor
   const int nbo = nbo_for(ctx, N);
   const int npan = (N + nbo - 1) / nbo;
   // the persistent solve's per-block operators, built once from this factor
@@ -315,7 +316,8 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
   // no factorization ran in this workspace: clear its sticky error words
   HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * 4,
                         ctx->stream));
-  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.ctrl_off, 0, IPMZ_SOLVE_CTRL_WORDS * 4, ctx->stream));
+  HIP_OK(solve_reset(static_cast<char*>(ws) + l.y_off, static_cast<char*>(ws) + l.z_off, sizeof(double), N,
+                     reinterpret_cast<unsigned*>(static_cast<char*>(ws) + l.ctrl_off), ctx->stream));
   return IPMZ_OK;
 }
 

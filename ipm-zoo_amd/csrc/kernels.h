@@ -98,9 +98,13 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
 // trsv_persist.hip: the same solve as ONE persistent launch on 128-row
 // blocks (nbi == 64 factors).  P: solve_prep_elems(N) elements written by
 // solve_prep from the factor's 64 x 64 inverses (once per factorization);
-// ybuf, xbuf: N elements; ctrl: IPMZ_SOLVE_CTRL_WORDS unsigned (counters
-// zeroed inside, ctrl[SOLVE_ERR_WORD] a sticky error word the caller clears).
+// ybuf, xbuf: N elements; ctrl: IPMZ_SOLVE_CTRL_WORDS unsigned, all set up
+// by solve_reset once per factorization (ctrl[SOLVE_ERR_WORD] is sticky).
 int64_t solve_prep_elems(int N);
+// the persistent solve's state after a factorization: control words zero,
+// y / x buffers (N elements of size elem) all-ones sentinels; the solve
+// launches keep it so for the next solve
+hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st);
 hipError_t solve_stamps(unsigned long long* out);  // DEBUG
 hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, double* P, hipStream_t st);
 hipError_t solve_prep(const float* K, int64_t ld, int N, const float* Linv, float* P, hipStream_t st);

@@ -65,7 +65,7 @@ __global__ __launch_bounds__(NB* NB / 16) void ldlt_diag_kernel(T* __restrict__ 
   __shared__ T dsh[NB];
   const int tid = threadIdx.x;
   const int tr = tid % TG, tc = tid / TG;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int wave = tid >> 6;
   for (int idx = tid; idx < NB * NB; idx += NT) {
     const int r = idx / NB, c = idx % NB;
     M[r][c] = (r < b && c <= r) ? K[(int64_t)(k0 + r) * ld + k0 + c] : (r == c ? T(1) : T(0));

@@ -67,6 +67,11 @@ template <>
 __device__ __forceinline__ bool is_sentinel<float>(float v) {
   return __float_as_int(v) == -1;
 }
+template <typename T>
+__device__ __forceinline__ T sentinel() {
+  if constexpr (sizeof(T) == 8) return __longlong_as_double(-1ll);
+  else return __int_as_float(-1);
+}
 
 // Workgroup barrier for LDS hand-offs only: unlike __syncthreads() it does not
 // wait for the wave's outstanding global loads (the tile prefetches stay in
@@ -331,12 +336,16 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
     lds_sync();
     const int ticket = (int)sh_ticket;
     if (ticket >= nb) return;
+    // the other sweep's ticket counter, for the next launch of that sweep
+    // (the previous one has completed: stream order)
+    if (ticket == 0 && tid == 0) st_sc1(&ctrl[BWD ? SC_TICKET : SC_TICKET_B], 0u);
 
     if constexpr (!BWD) {
       // ============================================================ forward
       const int J = ticket, J0 = J * SB;
       const int R = N - J0 < SB ? N - J0 : SB;
       SSTAMP(J, 0);
+      if (tid < R) st_sc1(&xbuf[J0 + tid], sentinel<T>());  // for this solve's backward launch
       // rows past N read row J0 (finite data): their sums are never used
       const T* Lrow = K + (int64_t)J0 * ld;
       const int64_t ldr = ld;
@@ -429,6 +438,7 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
       }
       load_rows(ta, XT + (int64_t)J * SB * SB);
       if (tid < SB) bj[tid] = tid < R ? ybuf[J0 + tid] / D[J0 + tid] : T(0);
+      if (tid < R) st_sc1(&ybuf[J0 + tid], sentinel<T>());  // only this block reads y_J: reset for the next solve
       put_xs(ta);
       auto load_tile = [&](Tile& t, int Kb) {
         const int R0 = Kb * SB + CP_ROWS * crg;
@@ -538,11 +548,10 @@ static hipError_t solve_persistent_t(const T* K, int64_t ld, int N, const T* D, 
   if (ld % 2) return hipErrorInvalidValue;  // 2-element vector loads of the tiles
   const int nb = (N + SB - 1) / SB;
   const int64_t q = (int64_t)nb * SB * SB;
-  // the two ticket counters; ctrl[SOLVE_ERR_WORD] stays sticky
-  hipError_t e = hipMemsetAsync(ctrl + SC_TICKET, 0, 2 * sizeof(unsigned), st);
-  if (e != hipSuccess) return e;
-  if ((e = hipMemsetAsync(ybuf, 0xff, (size_t)N * sizeof(T), st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(xbuf, 0xff, (size_t)N * sizeof(T), st)) != hipSuccess) return e;
+  // no per-solve memsets: each launch leaves the state the next one needs
+  // (the forward resets x and the backward ticket, the backward resets y and
+  // the forward ticket); solve_reset establishes it after a factorization
+  hipError_t e = hipSuccess;
   // the two sweeps as two launches (each its own register allocation);
   // resident grids: one workgroup per CU
   const int grid = nb < 256 ? nb : 256;
@@ -553,6 +562,13 @@ static hipError_t solve_persistent_t(const T* K, int64_t ld, int N, const T* D, 
   hipLaunchKernelGGL((trsv128_kernel<T, true>), dim3(grid), dim3(SNT), 0, st, K, ld, N, D, P, P + q, P + 2 * q,
                      P + 3 * q, b, ybuf, xbuf, ctrl, nb, skip, inject);
   return hipGetLastError();
+}
+
+hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st) {
+  hipError_t e = hipMemsetAsync(ctrl, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), st);  // tickets + sticky error
+  if (e == hipSuccess) e = hipMemsetAsync(ybuf, 0xff, (size_t)N * elem, st);
+  if (e == hipSuccess) e = hipMemsetAsync(xbuf, 0xff, (size_t)N * elem, st);
+  return e;
 }
 
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* P, double* b,

@@ -163,6 +163,34 @@ static void dump_system(std::ostream& os, const SO::NewtonSystem& ns) {
   for (auto& [v, d] : ns.delta_definitions) os << "    " << to_s(v) << " := " << to_s(d) << "\n";
 }
 
+static SO::Bounds bounds_from(const std::string& b) {
+  if (b == "None") return SO::Bounds::None;
+  if (b == "Lower") return SO::Bounds::Lower;
+  if (b == "Upper") return SO::Bounds::Upper;
+  return SO::Bounds::Both;
+}
+
+// one Settings' formulation to stdout (exploration; fixtures use mode_formulation)
+static int mode_formulation_one(const std::string& ineq, const std::string& ineq_bounds,
+                                const std::string& var_bounds) {
+  SO::Settings s = settings_from(ineq, "none", ineq_bounds != "None");
+  s.inequalities = bounds_from(ineq_bounds);
+  s.variable_bounds = bounds_from(var_bounds);
+  const SO::VariableNames names;
+  const auto ns = SO::get_newton_system(s, names);
+  std::cout << "-- newton system\n";
+  dump_system(std::cout, ns);
+  const auto sh = SO::get_shorthand_rhs(ns);
+  std::cout << "-- shorthand definitions\n";
+  for (auto& [v, d] : sh.vector_definitions) std::cout << "    " << to_s(v) << " := " << to_s(d) << "\n";
+  auto ns2 = ns;
+  ns2.rhs = sh.shorthand_rhs;
+  const auto aug = SO::get_augmented_system(ns2);
+  std::cout << "-- augmented system\n";
+  dump_system(std::cout, aug);
+  return 0;
+}
+
 static int mode_formulation(const std::string& dir) {
   std::ofstream os(dir + "/formulations.txt");
   const SO::VariableNames names;
@@ -390,7 +418,9 @@ static IterRecord reference_iteration(NO::Optimizer& opt) {
   return r;
 }
 
-static int mode_newton(const std::string& dir, size_t n, size_t m, uint64_t seed, int iters, const std::string& tag) {
+static int mode_newton(const std::string& dir, size_t n, size_t m, uint64_t seed, int iters, const std::string& tag,
+                       const std::string& ineq = "SlackedSlacks", const std::string& ineq_bounds = "",
+                       const std::string& var_bounds = "Both") {
   const QP q = make_qp(n, m, 0, seed);
   NO::Data data;
   data.Q = q.Q;
@@ -401,7 +431,9 @@ static int mode_newton(const std::string& dir, size_t n, size_t m, uint64_t seed
   data.l_x = q.lx;
   data.u_x = q.ux;
   const SO::VariableNames names;
-  SO::Settings s = settings_from("SlackedSlacks", "none", m > 0);
+  SO::Settings s = settings_from(ineq, "none", m > 0);
+  if (!ineq_bounds.empty()) s.inequalities = bounds_from(ineq_bounds);
+  s.variable_bounds = bounds_from(var_bounds);
   const auto oe = SO::get_optimization_expressions(names);
   auto env = NO::build_environment(names, data);
   const auto ns = SO::get_newton_system(s, names);
@@ -508,6 +540,7 @@ int main(int argc, char** argv) {
   const std::string mode = argv[1], dir = argv[2];
   try {
     if (mode == "formulation") return mode_formulation(dir);
+    if (mode == "formulation_one" && argc == 5) return mode_formulation_one(argv[2], argv[3], argv[4]);
     if (mode == "ldlt" && argc == 6) return mode_ldlt(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk" && argc == 6) return mode_bk(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk_zeros_at" && argc == 7)
@@ -517,6 +550,9 @@ int main(int argc, char** argv) {
     if (mode == "newton" && argc == 8)
       return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
                          argv[7]);
+    if (mode == "newton" && argc == 11)  // + <ineq handling> <inequality bounds> <variable bounds>
+      return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
+                         argv[7], argv[8], argv[9], argv[10]);
     if (mode == "component_eq" && argc == 8)
       return mode_component_eq(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoul(argv[5]),
                                std::stoull(argv[6]), argv[7]);

@@ -204,7 +204,7 @@ int main(int argc, char** argv) {
   CK(hipMemsetAsync(b, 0, N * 8, st));
   double* P;
   CK(hipMalloc(&P, ipmz::solve_prep_elems(N) * 8));
-  CK(hipMemsetAsync(ctrl, 0, 256, st));
+  CK(ipmz::solve_reset(yb, xb, 8, N, ctrl, st));
   t.start(st);
   CK(ipmz::solve_prep(K, ld, N, Linv, P, st));
   const float pms = t.stop(st);
