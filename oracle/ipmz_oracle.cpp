@@ -70,14 +70,31 @@ struct QP {
   // reference's evaluator asserts on the scalar block (Evaluation.cpp:57-60);
   // here it is mu * I (§8f row f4)
   bool eq_pen = false;
+  // Settings (SymbolicOptimization.h:28-64, formulations.txt): InequalityHandling
+  // ::Slacks -- no nonnegative slacks g, h, y, z; the complementarity rows are
+  // ((X - L_x) lambda_y - mu e), ((U_x - X) lambda_z - mu e), ((S - L_A)
+  // lambda_g - mu e), ((U_A - S) lambda_h - mu e) -- and one-sided / absent
+  // bounds: vlo / vup = Settings::variable_bounds has Lower / Upper, alo / aup
+  // = Settings::inequalities has Lower / Upper (one of them when m > 0).
+  // Defaults: SlackedSlacks, Bounds::Both.
+  bool slacks = false;
+  bool vlo = true, vup = true, alo = true, aup = true;
   Vec Q, c, A, lA, uA, C, d, lx, ux;
   Vec v[NSLOT];       // iterate
   Vec daff[NSLOT], dir[NSLOT];
   double mu;          // EnvironmentBuilder.cpp:49
   int64_t size(int s) const {
     switch (s) {
-      case X: case LY: case LZ: case Y: case Z: return n;
-      case LA: case S: case LG: case LH: case G: case H: return m;
+      case X: return n;
+      case LY: return vlo ? n : 0;
+      case LZ: return vup ? n : 0;
+      case Y: return vlo && !slacks ? n : 0;
+      case Z: return vup && !slacks ? n : 0;
+      case LA: case S: return m;
+      case LG: return alo ? m : 0;
+      case LH: return aup ? m : 0;
+      case G: return alo && !slacks ? m : 0;
+      case H: return aup && !slacks ? m : 0;
       case P: return (eq_none || eq_pen) ? 0 : p;
       default: return p;
     }
@@ -121,24 +138,45 @@ void residuals(const QP& q, double mu, Residuals& R) {
   if (m) { matvec_t(q.A, m, n, v[LA].data(), ATl.data()); matvec(q.A, m, n, v[X].data(), Ax.data()); }
   if (p) { matvec_t(q.C, p, n, v[LC].data(), CTl.data()); matvec(q.C, p, n, v[X].data(), Cx.data()); }
   for (int64_t i = 0; i < n; ++i) {
-    // r_x := (c + lambda_z + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] - lambda_y)
-    double t = q.c[i] + v[LZ][i];
+    // r_x := (c [+ lambda_z] + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] [- lambda_y])
+    double t = q.c[i];
+    if (q.vup) t = t + v[LZ][i];
     t = t + Qx[i];
     if (m) t = t + ATl[i];
     if (p) t = t + CTl[i];
-    R.r[X][i] = t + (-v[LY][i]);
-    R.r[LY][i] = (q.lx[i] + v[Y][i]) + (-v[X][i]);     // (l_x + y - x)
-    R.r[LZ][i] = (v[X][i] + v[Z][i]) + (-q.ux[i]);     // (x + z - u_x)
-    R.r[Y][i] = v[Y][i] * v[LY][i] + (-(mu * 1.0));    // ((Y*lambda_y) - (mu*e_x))
-    R.r[Z][i] = v[Z][i] * v[LZ][i] + (-(mu * 1.0));
+    R.r[X][i] = q.vlo ? t + (-v[LY][i]) : t;
+    if (q.slacks) {
+      if (q.vlo) R.r[LY][i] = ((v[X][i] + (-q.lx[i])) * v[LY][i]) + (-(mu * 1.0));  // (((X - L_x)*lambda_y) - (mu*e_x))
+      if (q.vup) R.r[LZ][i] = ((q.ux[i] + (-v[X][i])) * v[LZ][i]) + (-(mu * 1.0));  // (((U_x - X)*lambda_z) - (mu*e_x))
+    } else {
+      if (q.vlo) {
+        R.r[LY][i] = (q.lx[i] + v[Y][i]) + (-v[X][i]);  // (l_x + y - x)
+        R.r[Y][i] = v[Y][i] * v[LY][i] + (-(mu * 1.0));  // ((Y*lambda_y) - (mu*e_x))
+      }
+      if (q.vup) {
+        R.r[LZ][i] = (v[X][i] + v[Z][i]) + (-q.ux[i]);  // (x + z - u_x)
+        R.r[Z][i] = v[Z][i] * v[LZ][i] + (-(mu * 1.0));
+      }
+    }
   }
   for (int64_t i = 0; i < m; ++i) {
-    R.r[LA][i] = Ax[i] + (-v[S][i]);                               // ((A*x) - s)
-    R.r[S][i] = -((v[LA][i] + v[LG][i]) + (-v[LH][i]));           // -(lambda_A + lambda_g - lambda_h)
-    R.r[LG][i] = (q.lA[i] + v[G][i]) + (-v[S][i]);                 // (l_A + g - s)
-    R.r[LH][i] = (v[H][i] + v[S][i]) + (-q.uA[i]);                 // (h + s - u_A)
-    R.r[G][i] = v[G][i] * v[LG][i] + (-(mu * 1.0));
-    R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
+    R.r[LA][i] = Ax[i] + (-v[S][i]);  // ((A*x) - s)
+    if (q.alo && q.aup) R.r[S][i] = -((v[LA][i] + v[LG][i]) + (-v[LH][i]));  // -(lambda_A + lambda_g - lambda_h)
+    else if (q.alo) R.r[S][i] = -(v[LA][i] + v[LG][i]);                      // -(lambda_A + lambda_g)
+    else R.r[S][i] = v[LH][i] + (-v[LA][i]);                                 // (lambda_h - lambda_A)
+    if (q.slacks) {
+      R.r[LG][i] = ((v[S][i] + (-q.lA[i])) * v[LG][i]) + (-(mu * 1.0));  // (((S - L_A)*lambda_g) - (mu*e_A))
+      R.r[LH][i] = ((q.uA[i] + (-v[S][i])) * v[LH][i]) + (-(mu * 1.0));  // (((U_A - S)*lambda_h) - (mu*e_A))
+    } else {
+      if (q.alo) {
+        R.r[LG][i] = (q.lA[i] + v[G][i]) + (-v[S][i]);  // (l_A + g - s)
+        R.r[G][i] = v[G][i] * v[LG][i] + (-(mu * 1.0));
+      }
+      if (q.aup) {
+        R.r[LH][i] = (v[H][i] + v[S][i]) + (-q.uA[i]);  // (h + s - u_A)
+        R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
+      }
+    }
   }
   for (int64_t i = 0; i < p && q.eq_none; ++i) R.r[LC][i] = Cx[i] + (-q.d[i]);  // ((C*x) - d)
   for (int64_t i = 0; i < p && q.eq_pen; ++i)                                    // -(d + (mu*lambda_C) - (C*x))
@@ -147,6 +185,14 @@ void residuals(const QP& q, double mu, Residuals& R) {
     R.r[LC][i] = (Cx[i] + q.delta * v[P][i]) + (-q.d[i]);          // ((C*x) + (delta*p) - d)
     R.r[P][i] = v[P][i] + q.delta * v[LC][i];                      // (p + (delta*lambda_C))
   }
+}
+
+// The rows that carry e and mu (get_mu_'s filter, Optimizer.cpp:250-268), in
+// Newton order: g, h, y, z (SlackedSlacks) or lambda_g, lambda_h, lambda_y,
+// lambda_z (Slacks).
+inline void comp_rows(const QP& q, int out[4]) {
+  const int ss[4] = {G, H, Y, Z}, sl[4] = {LG, LH, LY, LZ};
+  for (int k = 0; k < 4; ++k) out[k] = q.slacks ? sl[k] : ss[k];
 }
 
 // Newton-variable order of the reference (absent blocks dropped).
@@ -173,17 +219,29 @@ double residual_norm(const QP& q) {
 
 // get_mu_ (Optimizer.cpp:249-268): mean |complementarity| at mu=0 over the
 // rows containing e and mu, in Newton order (g, h, y, z).
+// A complementarity row at mu (the residuals() expressions of those rows).
+inline double comp_value(const QP& q, int slot, int64_t i, double mu) {
+  const Vec* v = q.v;
+  switch (slot) {
+    case G: return v[G][i] * v[LG][i] + (-(mu * 1.0));
+    case H: return v[H][i] * v[LH][i] + (-(mu * 1.0));
+    case Y: return v[Y][i] * v[LY][i] + (-(mu * 1.0));
+    case Z: return v[Z][i] * v[LZ][i] + (-(mu * 1.0));
+    case LG: return ((v[S][i] + (-q.lA[i])) * v[LG][i]) + (-(mu * 1.0));
+    case LH: return ((q.uA[i] + (-v[S][i])) * v[LH][i]) + (-(mu * 1.0));
+    case LY: return ((v[X][i] + (-q.lx[i])) * v[LY][i]) + (-(mu * 1.0));
+    default: return ((q.ux[i] + (-v[X][i])) * v[LZ][i]) + (-(mu * 1.0));  // LZ
+  }
+}
+
 double mu_of(const QP& q) {
+  int comp[4];
+  comp_rows(q, comp);
   double s = 0.0;
   int64_t cnt = 0;
-  const int comp[4] = {G, H, Y, Z};
-  const int dual[4] = {LG, LH, LY, LZ};
   for (int k = 0; k < 4; ++k) {
     const int64_t len = q.size(comp[k]);
-    for (int64_t i = 0; i < len; ++i) {
-      const double r = -(q.v[comp[k]][i] * q.v[dual[k]][i] + (-(0.0 * 1.0)));
-      s = s + std::abs(r);
-    }
+    for (int64_t i = 0; i < len; ++i) s = s + std::abs(-comp_value(q, comp[k], i, 0.0));
     cnt += len;
   }
   return cnt == 0 ? 0.0 : s / (double)cnt;
@@ -206,6 +264,30 @@ double objective(const QP& q) {
 inline double ds_inv(const QP& q, int64_t i) {
   return inv(inv(q.v[G][i]) * q.v[LG][i] + inv(q.v[H][i]) * q.v[LH][i]);
 }
+// Slacks: (((U_A - S)^{-1}*Lambda_h) + ((S - L_A)^{-1}*Lambda_g))^{-1}
+inline double ds_inv_sl(const QP& q, int64_t i) {
+  return inv(inv(q.uA[i] + (-q.v[S][i])) * q.v[LH][i] + inv(q.v[S][i] + (-q.lA[i])) * q.v[LG][i]);
+}
+// the (x, x) diagonal term added to Q_ii and the (lambda_A, lambda_A) diagonal
+inline double kkt_xx(const QP& q, int64_t i, double qii) {
+  const Vec* v = q.v;
+  if (q.slacks) {  // (Q + ((U_x - X)^{-1}*Lambda_z) + ((X - L_x)^{-1}*Lambda_y))
+    double h = qii;
+    if (q.vup) h = h + inv(q.ux[i] + (-v[X][i])) * v[LZ][i];
+    if (q.vlo) h = h + inv(v[X][i] + (-q.lx[i])) * v[LY][i];
+    return h;
+  }
+  double h = qii;  // (Q [+ (Y^{-1}*Lambda_y)] [+ (Z^{-1}*Lambda_z)])
+  if (q.vlo) h = h + inv(v[Y][i]) * v[LY][i];
+  if (q.vup) h = h + inv(v[Z][i]) * v[LZ][i];
+  return h;
+}
+inline double kkt_aa(const QP& q, int64_t i) {
+  if (q.slacks) return -ds_inv_sl(q, i);
+  if (q.alo && q.aup) return -ds_inv(q, i);                   // -((G^{-1}*Lambda_g) + (H^{-1}*Lambda_h))^{-1}
+  if (q.alo) return -(inv(q.v[LG][i]) * q.v[G][i]);           // -(Lambda_g^{-1}*G)
+  return -(inv(q.v[LH][i]) * q.v[H][i]);                      // -(Lambda_h^{-1}*H)
+}
 
 // Augmented KKT (get_as_matrix_, Optimizer.cpp:387-391 / 441-501), dense
 // row-major N x N, both triangles.
@@ -214,16 +296,14 @@ void assemble(const QP& q, double* K) {
   std::memset(K, 0, sizeof(double) * (size_t)(N * N));
   for (int64_t i = 0; i < n; ++i) {
     for (int64_t j = 0; j < n; ++j) K[i * N + j] = q.Q[i * n + j];
-    // (Q + (Y^{-1}*Lambda_y) + (Z^{-1}*Lambda_z)): elementwise_diag_mat_op
-    double h = q.Q[i * n + i] + inv(q.v[Y][i]) * q.v[LY][i];
-    K[i * N + i] = h + inv(q.v[Z][i]) * q.v[LZ][i];
+    K[i * N + i] = kkt_xx(q, i, q.Q[i * n + i]);  // elementwise_diag_mat_op
   }
   for (int64_t r = 0; r < m; ++r) {
     for (int64_t j = 0; j < n; ++j) {
       K[(n + r) * N + j] = q.A[r * n + j];
       K[j * N + n + r] = q.A[r * n + j];
     }
-    K[(n + r) * N + n + r] = -ds_inv(q, r);
+    K[(n + r) * N + n + r] = kkt_aa(q, r);
   }
   for (int64_t r = 0; r < p; ++r) {
     for (int64_t j = 0; j < n; ++j) {
@@ -239,14 +319,34 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
   const int64_t n = q.n, m = q.m, p = q.p;
   const Vec* v = q.v;
   for (int64_t i = 0; i < n; ++i) {
-    const double tz = inv(v[Z][i]) * (R.r[Z][i] + (-(v[LZ][i] * R.r[LZ][i])));
-    const double ty = inv(v[Y][i]) * (R.r[Y][i] + (-(v[LY][i] * R.r[LY][i])));
-    b[i] = (tz + (-R.r[X][i])) + (-ty);
+    const double rx = R.r[X][i];
+    if (q.slacks) {  // (((U_x - X)^{-1}*r_lz) - r_x - ((X - L_x)^{-1}*r_ly)), absent terms dropped
+      double t = q.vup ? inv(q.ux[i] + (-v[X][i])) * R.r[LZ][i] + (-rx) : -rx;
+      if (q.vlo) t = t + (-(inv(v[X][i] + (-q.lx[i])) * R.r[LY][i]));
+      b[i] = t;
+      continue;
+    }
+    const double tz = q.vup ? inv(v[Z][i]) * (R.r[Z][i] + (-(v[LZ][i] * R.r[LZ][i]))) : 0.0;
+    const double ty = q.vlo ? inv(v[Y][i]) * (R.r[Y][i] + (-(v[LY][i] * R.r[LY][i]))) : 0.0;
+    if (q.vlo && q.vup) b[i] = (tz + (-rx)) + (-ty);  // ((Z^{-1}*(r_z - (L_z*r_lz))) - r_x - (Y^{-1}*(...)))
+    else if (q.vup) b[i] = tz + (-rx);               // ((Z^{-1}*(r_z - (L_z*r_lz))) - r_x)
+    else if (q.vlo) b[i] = -(rx + ty);               // -(r_x + (Y^{-1}*(r_y - (L_y*r_ly))))
+    else b[i] = -rx;                                 // -r_x
   }
   for (int64_t i = 0; i < m; ++i) {
-    const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
-    const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
-    b[n + i] = ds_inv(q, i) * ((th + (-R.r[S][i])) + (-tg)) + (-R.r[LA][i]);
+    const double rla = R.r[LA][i], rs = R.r[S][i];
+    if (q.slacks) {
+      const double a = inv(q.uA[i] + (-v[S][i])) * R.r[LH][i], c = inv(v[S][i] + (-q.lA[i])) * R.r[LG][i];
+      b[n + i] = ds_inv_sl(q, i) * ((a + (-rs)) + (-c)) + (-rla);
+    } else if (q.alo && q.aup) {
+      const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
+      const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
+      b[n + i] = ds_inv(q, i) * ((th + (-rs)) + (-tg)) + (-rla);
+    } else if (q.alo) {  // -(r_lA + (L_g^{-1}*(r_g + (G*r_s))) - r_lg)
+      b[n + i] = -((rla + inv(v[LG][i]) * (R.r[G][i] + v[G][i] * rs)) + (-R.r[LG][i]));
+    } else {  // ((L_h^{-1}*(r_h - (H*r_s))) - r_lA - r_lh)
+      b[n + i] = ((inv(v[LH][i]) * (R.r[H][i] + (-(v[H][i] * rs)))) + (-rla)) + (-R.r[LH][i]);
+    }
   }
   for (int64_t i = 0; i < p; ++i)  // None: -r_lambda_C ; Regularization: (delta*r_p) - r_lambda_C
     b[n + m + i] = (q.eq_none || q.eq_pen) ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
@@ -258,22 +358,53 @@ void back_substitute(const QP& q, const Residuals& R, Vec* D) {
   const int64_t n = q.n, m = q.m, p = q.p;
   const Vec* v = q.v;
   for (int64_t i = 0; i < m; ++i) {
-    const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
-    const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
-    const double ds = ds_inv(q, i) * ((((D[LA][i] + th) + (-R.r[S][i])) + (-tg)));
+    const double dla = D[LA][i], rs = R.r[S][i];
+    if (q.slacks) {
+      const double a = inv(q.uA[i] + (-v[S][i])) * R.r[LH][i], c = inv(v[S][i] + (-q.lA[i])) * R.r[LG][i];
+      const double ds = ds_inv_sl(q, i) * (((dla + a) + (-rs)) + (-c));
+      D[S][i] = ds;
+      D[LG][i] = -(inv(v[S][i] + (-q.lA[i])) * (R.r[LG][i] + v[LG][i] * ds));  // -((S - L_A)^{-1}*(r_lg + (L_g*ds)))
+      D[LH][i] = inv(q.uA[i] + (-v[S][i])) * (v[LH][i] * ds + (-R.r[LH][i]));  // ((U_A - S)^{-1}*((L_h*ds) - r_lh))
+      continue;
+    }
+    double ds;
+    if (q.alo && q.aup) {
+      const double th = inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])));
+      const double tg = inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i])));
+      ds = ds_inv(q, i) * ((((dla + th) + (-rs)) + (-tg)));
+    } else if (q.alo) {  // (L_g^{-1}*G*(dla - r_s - (G^{-1}*(r_g - (L_g*r_lg)))))
+      ds = (inv(v[LG][i]) * v[G][i]) *
+           ((dla + (-rs)) + (-(inv(v[G][i]) * (R.r[G][i] + (-(v[LG][i] * R.r[LG][i]))))));
+    } else {  // (L_h^{-1}*H*(dla + (H^{-1}*(r_h - (L_h*r_lh))) - r_s))
+      ds = (inv(v[LH][i]) * v[H][i]) *
+           ((dla + inv(v[H][i]) * (R.r[H][i] + (-(v[LH][i] * R.r[LH][i])))) + (-rs));
+    }
     D[S][i] = ds;
-    D[LG][i] = -((inv(v[G][i]) * v[LG][i]) * ((ds + inv(v[LG][i]) * R.r[G][i]) + (-R.r[LG][i])));
-    D[LH][i] = -((inv(v[H][i]) * v[LH][i]) * ((inv(v[LH][i]) * R.r[H][i] + (-R.r[LH][i])) + (-ds)));
-    D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));
-    D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
+    if (q.alo) {
+      D[LG][i] = -((inv(v[G][i]) * v[LG][i]) * ((ds + inv(v[LG][i]) * R.r[G][i]) + (-R.r[LG][i])));
+      D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));
+    }
+    if (q.aup) {
+      D[LH][i] = -((inv(v[H][i]) * v[LH][i]) * ((inv(v[LH][i]) * R.r[H][i] + (-R.r[LH][i])) + (-ds)));
+      D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
+    }
   }
   for (int64_t i = 0; i < p && !q.eq_none && !q.eq_pen; ++i) D[P][i] = -(R.r[P][i] + q.delta * D[LC][i]);
   for (int64_t i = 0; i < n; ++i) {
     const double dx = D[X][i];
-    D[LY][i] = -((inv(v[Y][i]) * v[LY][i]) * ((dx + inv(v[LY][i]) * R.r[Y][i]) + (-R.r[LY][i])));
-    D[LZ][i] = -((inv(v[Z][i]) * v[LZ][i]) * ((inv(v[LZ][i]) * R.r[Z][i] + (-R.r[LZ][i])) + (-dx)));
-    D[Y][i] = -(inv(v[LY][i]) * (R.r[Y][i] + v[Y][i] * D[LY][i]));
-    D[Z][i] = -(inv(v[LZ][i]) * (R.r[Z][i] + v[Z][i] * D[LZ][i]));
+    if (q.slacks) {
+      if (q.vlo) D[LY][i] = -(inv(v[X][i] + (-q.lx[i])) * (R.r[LY][i] + v[LY][i] * dx));  // -((X - L_x)^{-1}*(r_ly + (L_y*dx)))
+      if (q.vup) D[LZ][i] = inv(q.ux[i] + (-v[X][i])) * (v[LZ][i] * dx + (-R.r[LZ][i]));  // ((U_x - X)^{-1}*((L_z*dx) - r_lz))
+      continue;
+    }
+    if (q.vlo) {
+      D[LY][i] = -((inv(v[Y][i]) * v[LY][i]) * ((dx + inv(v[LY][i]) * R.r[Y][i]) + (-R.r[LY][i])));
+      D[Y][i] = -(inv(v[LY][i]) * (R.r[Y][i] + v[Y][i] * D[LY][i]));
+    }
+    if (q.vup) {
+      D[LZ][i] = -((inv(v[Z][i]) * v[LZ][i]) * ((inv(v[LZ][i]) * R.r[Z][i] + (-R.r[LZ][i])) + (-dx)));
+      D[Z][i] = -(inv(v[LZ][i]) * (R.r[Z][i] + v[Z][i] * D[LZ][i]));
+    }
   }
 }
 
@@ -380,7 +511,10 @@ void solve_ldlt(int64_t n, const double* L, int64_t ldl, const double* D, double
   }
 }
 
-// get_max_step_ (Optimizer.cpp:270-342).
+// get_max_step_ (Optimizer.cpp:270-342): the non-negative Newton variables,
+// and -- when neither g nor h is a Newton variable (box-only, or Slacks) --
+// explicit bounds on x (l_x, u_x) and s (l_A, u_A); the environment always
+// holds both bounds of each, whatever Settings::*_bounds say.
 double max_step(const QP& q, const Vec* D) {
   double a = 1.0;
   const int nonneg[8] = {LG, LH, LY, LZ, G, H, Y, Z};
@@ -393,11 +527,16 @@ double max_step(const QP& q, const Vec* D) {
       if (dij < 0.0) a = std::min(a, -vij / dij);
     }
   }
-  if (q.m == 0) {  // neither g nor h is a Newton variable: explicit x bounds
+  if (q.size(G) == 0 && q.size(H) == 0) {
     for (int64_t j = 0; j < q.n; ++j) {
       const double dij = D[X][j], vij = q.v[X][j];
       if (dij < 0.0) a = std::min(a, (q.lx[j] - vij) / dij);
       if (dij > 0.0) a = std::min(a, (q.ux[j] - vij) / dij);
+    }
+    for (int64_t j = 0; j < q.m; ++j) {
+      const double dij = D[S][j], vij = q.v[S][j];
+      if (dij < 0.0) a = std::min(a, (q.lA[j] - vij) / dij);
+      if (dij > 0.0) a = std::min(a, (q.uA[j] - vij) / dij);
     }
   }
   return a;
@@ -484,12 +623,28 @@ int iterate(QP& q, double* rec, double* phase_s) {
   const double sigma = mu > 0.0 ? std::pow(mu_aff / mu, 3) : 0.0;
   const double mu_new = mu * sigma;
   residuals(q, mu_new, R);
-  // Corrector (Optimizer.cpp:183-209): r_v += (dV_aff * dlambda_aff) - (0*e)
-  const int comp[4] = {G, H, Y, Z};
-  const int dual[4] = {LG, LH, LY, LZ};
-  for (int k = 0; k < 4; ++k)
-    for (int64_t i = 0; i < q.size(comp[k]); ++i)
-      R.r[comp[k]][i] = R.r[comp[k]][i] + (q.daff[comp[k]][i] * q.daff[dual[k]][i] + (-(0.0 * 1.0)));
+  // Corrector (Optimizer.cpp:183-209): every VARIABLE of a complementarity row
+  // replaced by its affine direction, mu by 0, added to the row at mu_new:
+  // SlackedSlacks r_g += (dG_aff*dlambda_g_aff) - (0*e); Slacks r_lambda_y +=
+  // ((dX_aff - L_x)*dlambda_y_aff) - (0*e) -- the bound constant leaks in
+  // (the reference's Slacks defect, reproduced)
+  {
+    const Vec* dv = q.daff;
+    for (int64_t i = 0; i < q.size(G); ++i) R.r[G][i] = R.r[G][i] + (dv[G][i] * dv[LG][i] + (-(0.0 * 1.0)));
+    for (int64_t i = 0; i < q.size(H); ++i) R.r[H][i] = R.r[H][i] + (dv[H][i] * dv[LH][i] + (-(0.0 * 1.0)));
+    for (int64_t i = 0; i < q.size(Y); ++i) R.r[Y][i] = R.r[Y][i] + (dv[Y][i] * dv[LY][i] + (-(0.0 * 1.0)));
+    for (int64_t i = 0; i < q.size(Z); ++i) R.r[Z][i] = R.r[Z][i] + (dv[Z][i] * dv[LZ][i] + (-(0.0 * 1.0)));
+    if (q.slacks) {
+      for (int64_t i = 0; i < q.size(LG); ++i)
+        R.r[LG][i] = R.r[LG][i] + ((dv[S][i] + (-q.lA[i])) * dv[LG][i] + (-(0.0 * 1.0)));
+      for (int64_t i = 0; i < q.size(LH); ++i)
+        R.r[LH][i] = R.r[LH][i] + ((q.uA[i] + (-dv[S][i])) * dv[LH][i] + (-(0.0 * 1.0)));
+      for (int64_t i = 0; i < q.size(LY); ++i)
+        R.r[LY][i] = R.r[LY][i] + ((dv[X][i] + (-q.lx[i])) * dv[LY][i] + (-(0.0 * 1.0)));
+      for (int64_t i = 0; i < q.size(LZ); ++i)
+        R.r[LZ][i] = R.r[LZ][i] + ((q.ux[i] + (-dv[X][i])) * dv[LZ][i] + (-(0.0 * 1.0)));
+    }
+  }
   search_direction(q, R, F, q.dir);
   const double alpha = max_step(q, q.dir);
   axpy_all(q, 0.995 * alpha, q.dir);
@@ -743,6 +898,29 @@ void ipmzo_set_equality_none(void* h) {
   q.v[P].clear();
   q.daff[P].clear();
   q.dir[P].clear();
+}
+
+// Settings (call right after ipmzo_create): inequality handling (0
+// SlackedSlacks, 1 Slacks) and the bounds (IPMZ_BOUNDS_*: 0 None, 1 Lower,
+// 2 Upper, 3 Both) of the inequalities and of the variables.  Resizes the
+// slots and restores build_environment's initial iterate.
+int ipmzo_set_formulation(void* h, int slacks, int ineq_bounds, int var_bounds) {
+  QP& q = *static_cast<QP*>(h);
+  if (q.m > 0 && ineq_bounds == 0) return -1;  // the reference then drops A entirely: not modelled
+  q.slacks = slacks != 0;
+  q.alo = (ineq_bounds & 1) != 0;
+  q.aup = (ineq_bounds & 2) != 0;
+  q.vlo = (var_bounds & 1) != 0;
+  q.vup = (var_bounds & 2) != 0;
+  if (q.slacks && (!q.alo || !q.aup || !q.vlo || !q.vup)) return -1;  // Slacks: Bounds::Both only (pinned)
+  for (int s = 0; s < NSLOT; ++s) {
+    q.v[s].assign(q.size(s), 1.0);
+    q.daff[s].assign(q.size(s), 0.0);
+    q.dir[s].assign(q.size(s), 0.0);
+  }
+  for (int64_t i = 0; i < q.n; ++i) q.v[X][i] = 0.5 * (q.lx[i] + q.ux[i]);
+  for (int64_t i = 0; i < q.m; ++i) q.v[S][i] = 0.5 * (q.lA[i] + q.uA[i]);
+  return 0;
 }
 
 int64_t ipmzo_kkt_dim(void* h) { return static_cast<QP*>(h)->N(); }

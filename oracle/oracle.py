@@ -22,20 +22,39 @@ SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_
 NONNEG = {"lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"}
 
 
-def slot_size(name, n, m, p, eq_none=False):
+# Settings (SymbolicOptimization.h:28-64): Bounds as bit masks (ipmz.h IPMZ_BOUNDS_*)
+BOUNDS = {"None": 0, "Lower": 1, "Upper": 2, "Both": 3}
+
+
+class Form:
+    """Formulation: inequality handling (slacks=True: InequalityHandling::Slacks)
+    and the bounds of the inequalities / variables (BOUNDS values)."""
+
+    def __init__(self, slacks=False, ineq_bounds=3, var_bounds=3):
+        self.slacks = bool(slacks)
+        self.ineq_bounds = ineq_bounds
+        self.var_bounds = var_bounds
+
+
+def slot_size(name, n, m, p, eq_none=False, form=None):
     """eq_none: any equality handling without the slack p (None, PenaltyFunction)."""
-    if name in ("x", "lambda_y", "lambda_z", "y", "z"):
-        return n
-    if name in ("lambda_A", "s", "lambda_g", "lambda_h", "g", "h"):
-        return m
+    f = form or Form()
+    vlo, vup = bool(f.var_bounds & 1), bool(f.var_bounds & 2)
+    alo, aup = bool(f.ineq_bounds & 1), bool(f.ineq_bounds & 2)
+    sizes = {"x": n, "lambda_y": n if vlo else 0, "lambda_z": n if vup else 0,
+             "y": n if vlo and not f.slacks else 0, "z": n if vup and not f.slacks else 0,
+             "lambda_A": m, "s": m, "lambda_g": m if alo else 0, "lambda_h": m if aup else 0,
+             "g": m if alo and not f.slacks else 0, "h": m if aup and not f.slacks else 0}
+    if name in sizes:
+        return sizes[name]
     if name == "p" and eq_none:
         return 0
     return p
 
 
-def newton_order(n, m, p, eq_none=False):
+def newton_order(n, m, p, eq_none=False, form=None):
     """Reference Newton-variable order with absent blocks dropped."""
-    return [s for s in SLOTS if slot_size(s, n, m, p, eq_none) > 0]
+    return [s for s in SLOTS if slot_size(s, n, m, p, eq_none, form) > 0]
 
 
 def _dp(a):
@@ -51,6 +70,8 @@ def _load():
     lib.ipmzo_destroy.argtypes = [ctypes.c_void_p]
     lib.ipmzo_set_equality_none.argtypes = [ctypes.c_void_p]
     lib.ipmzo_set_equality_penalty.argtypes = [ctypes.c_void_p]
+    lib.ipmzo_set_formulation.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.ipmzo_set_formulation.restype = ctypes.c_int
     lib.ipmzo_iterate.argtypes = [ctypes.c_void_p, _P]
     lib.ipmzo_iterate.restype = ctypes.c_int
     lib.ipmzo_iterate_timed.argtypes = [ctypes.c_void_p, _P, _P]
@@ -164,9 +185,10 @@ class OracleQP:
     equalities -- or, eq_none=True, EqualityHandling::None with the
     Bunch-Kaufman factor) from build_environment's initial iterate."""
 
-    def __init__(self, qp, eq_none=False, eq_penalty=False):
+    def __init__(self, qp, eq_none=False, eq_penalty=False, form=None):
         self.qp = qp
         self.eq_none = bool(eq_none) or bool(eq_penalty)  # no p block
+        self.form = form or Form()
         n, m, p = qp["n"], qp["m"], qp["p"]
         self._keep = [np.ascontiguousarray(qp[k], dtype=np.float64).reshape(-1) if np.size(qp[k]) else np.zeros(1)
                       for k in ("Q", "c", "A", "lA", "uA", "C", "d", "lx", "ux")]
@@ -175,9 +197,13 @@ class OracleQP:
             lib().ipmzo_set_equality_penalty(self.h)
         elif eq_none:
             lib().ipmzo_set_equality_none(self.h)
+        if form is not None:
+            ib = form.ineq_bounds if m else 3
+            if lib().ipmzo_set_formulation(self.h, int(form.slacks), ib, form.var_bounds) != 0:
+                raise ValueError("unsupported formulation")
         self.N = lib().ipmzo_kkt_dim(self.h)
         self.L = lib().ipmzo_state_len(self.h)
-        self.order = newton_order(n, m, p, self.eq_none)
+        self.order = newton_order(n, m, p, self.eq_none, self.form)
 
     def __del__(self):
         if getattr(self, "h", None) and _lib is not None:
@@ -238,7 +264,7 @@ class OracleQP:
         n, m, p = self.qp["n"], self.qp["m"], self.qp["p"]
         out, off = {}, 0
         for s in self.order:
-            k = slot_size(s, n, m, p, self.eq_none)
+            k = slot_size(s, n, m, p, self.eq_none, self.form)
             out[s] = flat[off:off + k]
             off += k
         return out

@@ -194,16 +194,23 @@ static int mode_formulation_one(const std::string& ineq, const std::string& ineq
 static int mode_formulation(const std::string& dir) {
   std::ofstream os(dir + "/formulations.txt");
   const SO::VariableNames names;
-  struct Case { const char* ineq; const char* eq; bool has_ineq; };
+  struct Case { const char* ineq; const char* eq; bool has_ineq; const char* ib; const char* vb; };
   const Case cases[] = {
-      {"SlackedSlacks", "none", false}, {"SlackedSlacks", "none", true},
-      {"SlackedSlacks", "Regularization", true}, {"Slacks", "none", true},
-      {"SlackedSlacks", "None", true}, {"SlackedSlacks", "PenaltyFunction", true},
+      {"SlackedSlacks", "none", false, "None", "Both"}, {"SlackedSlacks", "none", true, "Both", "Both"},
+      {"SlackedSlacks", "Regularization", true, "Both", "Both"}, {"Slacks", "none", true, "Both", "Both"},
+      {"SlackedSlacks", "None", true, "Both", "Both"}, {"SlackedSlacks", "PenaltyFunction", true, "Both", "Both"},
+      // one-sided / absent bounds (Settings::inequalities, Settings::variable_bounds) and box-only Slacks
+      {"SlackedSlacks", "none", true, "Both", "Lower"}, {"SlackedSlacks", "none", true, "Both", "Upper"},
+      {"SlackedSlacks", "none", true, "Both", "None"}, {"SlackedSlacks", "none", true, "Lower", "Both"},
+      {"SlackedSlacks", "none", true, "Upper", "Both"}, {"Slacks", "none", false, "None", "Both"},
   };
   for (const auto& c : cases) {
-    const auto s = settings_from(c.ineq, c.eq, c.has_ineq);
-    os << "=== inequality_handling=" << c.ineq << " equalities=" << c.eq
-       << " inequalities=" << (c.has_ineq ? "Both" : "None") << "\n";
+    auto s = settings_from(c.ineq, c.eq, c.has_ineq);
+    s.inequalities = bounds_from(c.ib);
+    s.variable_bounds = bounds_from(c.vb);
+    os << "=== inequality_handling=" << c.ineq << " equalities=" << c.eq << " inequalities=" << c.ib;
+    if (std::string(c.vb) != "Both") os << " variable_bounds=" << c.vb;
+    os << "\n";
     const auto ns = SO::get_newton_system(s, names);
     os << "-- newton system\n";
     dump_system(os, ns);

@@ -48,6 +48,17 @@ CASES = [
     ("newton", 48, 16, 7, 100, "s1"),
     # C3 structure, component level (Regularization equalities)
     ("component_eq", 64, 16, 8, 1234, "eq64"),
+    # other Settings (newton <n> <m> <seed> <iters> <inequality handling> <inequality bounds> <variable bounds>):
+    # one-sided / absent bounds -- every one converges in the reference
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Lower", "vlo"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Upper", "vup"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "None", "vnone"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Lower", "Both", "alo"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Upper", "Both", "aup"),
+    ("newton", 48, 0, 7, 100, "SlackedSlacks", "None", "Lower", "vlo0"),
+    # InequalityHandling::Slacks: runs but stagnates (SURVEY.md App. C.1 corrector defect); 12 iterations
+    ("newton", 48, 16, 7, 12, "Slacks", "Both", "Both", "sl"),
+    ("newton", 48, 0, 7, 12, "Slacks", "None", "Both", "slbox"),
 ]
 
 
@@ -57,7 +68,10 @@ def main():
     subprocess.run([HARNESS, "formulation", HERE], check=True)
     for case in CASES:
         mode, tag = case[0], case[-1]
-        args = [HARNESS, mode, HERE] + [str(a) for a in case[1:-1]] + [tag]
+        if mode == "newton" and len(case) == 9:  # harness order: ... <iters> <tag> <ineq> <ineq bounds> <var bounds>
+            args = [HARNESS, mode, HERE] + [str(a) for a in case[1:5]] + [tag] + list(case[5:8])
+        else:
+            args = [HARNESS, mode, HERE] + [str(a) for a in case[1:-1]] + [tag]
         subprocess.run(args, check=True)
     manifest = {
         "generator": "tests/golden/make_golden.py via oracle/ref_harness.cpp",
