@@ -189,12 +189,28 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
                                     Bunch-Kaufman (LinearSolvers.cpp:76-318); N <= 4096 */
 #define IPMZ_EQ_PENALTY 2        /* PenaltyFunction: -mu (lambda_C, lambda_C) block (mu I,
                                     mu = the iterate's environment mu), no p: LDL^T */
+/* Settings::InequalityHandling (SymbolicOptimization.h:28-64) */
+#define IPMZ_INEQ_SLACKED_SLACKS 0 /* s with slacks g = s - l_A, h = u_A - s (and y, z
+                                      for x): the reference default                  */
+#define IPMZ_INEQ_SLACKS 1         /* no g/h/y/z: complementarity on (s - l_A) lambda_g
+                                      etc.; the reference's corrector substitutes
+                                      dX_aff for X in (X - L_x),
+                                      reproduced.  Bounds must be IPMZ_BOUNDS_BOTH
+                                      (inequality bounds: when m > 0). */
+/* Settings::Bounds for inequality_bounds / variable_bounds */
+#define IPMZ_BOUNDS_BOTH 0
+#define IPMZ_BOUNDS_LOWER 1
+#define IPMZ_BOUNDS_UPPER 2
+#define IPMZ_BOUNDS_NONE 3 /* variable bounds only; inequalities need a bound when m > 0 */
 typedef struct ipmz_qp_config {
   int n;         /* primal dimension                                  */
-  int m;         /* inequality rows  l_A <= A x <= u_A (SlackedSlacks) */
+  int m;         /* inequality rows  l_A <= A x <= u_A                 */
   int p;         /* equality rows C x = d                              */
   double delta;  /* regularization (EnvironmentBuilder.cpp:48: 1e-4)  */
-  int equality_handling; /* IPMZ_EQ_* (0 = Regularization)            */
+  int equality_handling;   /* IPMZ_EQ_* (0 = Regularization)          */
+  int inequality_handling; /* IPMZ_INEQ_* (0 = SlackedSlacks)         */
+  int inequality_bounds;   /* IPMZ_BOUNDS_* (0 = Both)                */
+  int variable_bounds;     /* IPMZ_BOUNDS_* (0 = Both)                */
 } ipmz_qp_config;
 
 int ipmz_qp_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, ipmz_qp** out);

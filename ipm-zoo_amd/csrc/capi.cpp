@@ -672,6 +672,9 @@ struct ipmz_qp {
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
+  // InequalityHandling / Bounds (which Newton slots exist)
+  bool slacks = false;
+  bool vlo = true, vup = true, alo = true, aup = true;
   int* ipiv = nullptr;
   int64_t sP = 0;
   char* nws = nullptr;
@@ -689,10 +692,20 @@ struct ipmz_qp {
 };
 
 namespace {
+// Newton variables present per formulation (SymbolicOptimization.cpp
+// get_variables_: absent blocks are dropped from the Newton order)
 int64_t slot_len(const ipmz_qp* s, int slot) {
   switch (slot) {
-    case X: case LY: case LZ: case Y: case Z: return s->n;
-    case LA: case S: case LG: case LH: case G: case H: return s->m;
+    case X: return s->n;
+    case LY: return s->vlo ? s->n : 0;
+    case LZ: return s->vup ? s->n : 0;
+    case Y: return (s->vlo && !s->slacks) ? s->n : 0;
+    case Z: return (s->vup && !s->slacks) ? s->n : 0;
+    case LA: case S: return s->m;
+    case LG: return s->alo ? s->m : 0;
+    case LH: return s->aup ? s->m : 0;
+    case G: return (s->alo && !s->slacks) ? s->m : 0;
+    case H: return (s->aup && !s->slacks) ? s->m : 0;
     case P: return (s->eqnone || s->eqpen) ? 0 : s->p;
     default: return s->p;
   }
@@ -838,6 +851,15 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + cfg->m + cfg->p > IPMZ_BK_NMAX)
     return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
                                   "N <= " + std::to_string(IPMZ_BK_NMAX));
+  const int ih = cfg->inequality_handling, ib = cfg->inequality_bounds, vb = cfg->variable_bounds;
+  if (ih != IPMZ_INEQ_SLACKED_SLACKS && ih != IPMZ_INEQ_SLACKS) return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
+  if (ib < IPMZ_BOUNDS_BOTH || ib > IPMZ_BOUNDS_NONE || vb < IPMZ_BOUNDS_BOTH || vb > IPMZ_BOUNDS_NONE)
+    return fail(IPMZ_ERR_INVALID, "unknown bounds setting");
+  if (cfg->m > 0 && ib == IPMZ_BOUNDS_NONE)
+    return fail(IPMZ_ERR_INVALID, "inequality rows need a lower or an upper bound (inequality_bounds != NONE)");
+  if (ih == IPMZ_INEQ_SLACKS && ((cfg->m > 0 && ib != IPMZ_BOUNDS_BOTH) || vb != IPMZ_BOUNDS_BOTH))
+    return fail(IPMZ_ERR_INVALID, "InequalityHandling::Slacks is built on both bounds (the reference's Slacks "
+                                  "formulation drops one-sided bounds inconsistently)");
   HIP_OK(hipSetDevice(ctx->device));
   auto* s = new ipmz_qp();
   s->ctx = ctx;
@@ -849,9 +871,15 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
   s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY;
+  s->slacks = ih == IPMZ_INEQ_SLACKS;
+  s->vlo = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_LOWER;
+  s->vup = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_UPPER;
+  s->alo = ib == IPMZ_BOUNDS_BOTH || ib == IPMZ_BOUNDS_LOWER;
+  s->aup = ib == IPMZ_BOUNDS_BOTH || ib == IPMZ_BOUNDS_UPPER;
   s->ldn = round_up(s->n, 8);
   s->ldk = round_up(s->N, 64);
-  s->state_len = 5 * (int64_t)s->n + 6 * (int64_t)s->m + ((s->eqnone || s->eqpen) ? 1 : 2) * (int64_t)s->p;
+  s->state_len = 0;
+  for (int k = 0; k < NSLOT; ++k) s->state_len += slot_len(s, k);
   const int n = s->n, m = s->m, p = s->p, N = s->N;
   int64_t sQ, sA, sC, sn, sm, sp, sS, sNb, sScal, sPart, sT;
   double* Q = dev_array(s, (int64_t)n * s->ldn, &sQ);
@@ -929,6 +957,11 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.delta = s->delta;
     q.eqnone = s->eqnone ? 1 : 0;
     q.eqpen = s->eqpen ? 1 : 0;
+    q.slacks = s->slacks ? 1 : 0;
+    q.vlo = s->vlo ? 1 : 0;
+    q.vup = s->vup ? 1 : 0;
+    q.alo = s->alo ? 1 : 0;
+    q.aup = s->aup ? 1 : 0;
     q.Q = Q + i * sQ;
     q.A = A + i * sA;
     q.C = C + i * sC;

@@ -183,6 +183,9 @@ struct QPDev {
   double delta;
   int eqnone;  // EqualityHandling::None: no p, zero (lambda_C, lambda_C) block
   int eqpen;   // EqualityHandling::PenaltyFunction: no p, -mu (lambda_C, lambda_C) block
+  // Settings (oracle/ipmz_oracle.cpp QP): InequalityHandling::Slacks, and the
+  // Lower / Upper halves of Settings::variable_bounds and ::inequalities
+  int slacks, vlo, vup, alo, aup;
   // problem data (row-major, ld = ldn)
   const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;
   double* v[NSLOT];

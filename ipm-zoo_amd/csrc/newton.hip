@@ -3,9 +3,11 @@
 // KKT assembly, augmented rhs, eliminated-variable back-substitution, ratio
 // tests, mu / sigma, corrector residuals and the iterate update.
 //
-// Formulation: InequalityHandling::SlackedSlacks, variable bounds Both,
-// optional EqualityHandling::Regularization (tests/golden/formulations.txt
-// is the reference's own symbolic output these formulas restate).  The
+// Formulations (tests/golden/formulations.txt is the reference's own
+// symbolic output these formulas restate): InequalityHandling::SlackedSlacks
+// (default) or ::Slacks, one-sided / absent inequality and variable bounds,
+// EqualityHandling Regularization / None / PenaltyFunction.  The flags are
+// per QP and uniform inside a launch.  The
 // element-wise formulas keep the reference evaluator's operand order
 // (Evaluation.cpp:102-176) and the library is built with -ffp-contract=off,
 // so they round exactly like oracle/ipmz_oracle.cpp; only the reductions
@@ -126,18 +128,18 @@ __global__ void k_init_iterate(const QPDev* __restrict__ qs) {
   const int t = blockIdx.x * NT + threadIdx.x;
   if (t < q.n) {
     q.v[X][t] = 0.5 * (q.lx[t] + q.ux[t]);
-    q.v[LY][t] = 1.0;
-    q.v[LZ][t] = 1.0;
-    q.v[Y][t] = 1.0;
-    q.v[Z][t] = 1.0;
+    if (q.vlo) q.v[LY][t] = 1.0;
+    if (q.vup) q.v[LZ][t] = 1.0;
+    if (q.vlo && !q.slacks) q.v[Y][t] = 1.0;
+    if (q.vup && !q.slacks) q.v[Z][t] = 1.0;
   }
   if (t < q.m) {
     q.v[S][t] = 0.5 * (q.lA[t] + q.uA[t]);
     q.v[LA][t] = 1.0;
-    q.v[LG][t] = 1.0;
-    q.v[LH][t] = 1.0;
-    q.v[G][t] = 1.0;
-    q.v[H][t] = 1.0;
+    if (q.alo) q.v[LG][t] = 1.0;
+    if (q.aup) q.v[LH][t] = 1.0;
+    if (q.alo && !q.slacks) q.v[G][t] = 1.0;
+    if (q.aup && !q.slacks) q.v[H][t] = 1.0;
   }
   if (t < q.p) {
     q.v[LC][t] = 1.0;
@@ -221,6 +223,9 @@ static void matvec_t(const QPBatch& qb, hipStream_t st) {
   hipLaunchKernelGGL((k_sum_chunks<MV>), grid2((h.n + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
 }
 
+// number of complementarity rows (get_mu_'s divisor, Optimizer.cpp:250-268)
+__device__ __forceinline__ int comp_count(const QPDev& q) { return (q.vlo + q.vup) * q.n + (q.alo + q.aup) * q.m; }
+
 // ---------------------------------------------------------------------------
 // Shorthand residuals r_v := -rhs_v at mu (SymbolicOptimization.cpp:480-492),
 // plus per-block partials of ||rhs||^2, sum |complementarity|, and the two
@@ -234,40 +239,83 @@ __global__ __launch_bounds__(NT) void k_residuals(const QPDev* __restrict__ qs, 
   for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
     if (t < n) {
       const int i = t;
-      double s = q.c[i] + q.v[LZ][i];
+      // r_x := (c [+ lambda_z] + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] [- lambda_y])
+      double s = q.c[i];
+      if (q.vup) s = s + q.v[LZ][i];
       s = s + q.Qx[i];
       if (m) s = s + q.ATl[i];
       if (p) s = s + q.CTl[i];
-      const double rx = s + (-q.v[LY][i]);
-      const double rly = (q.lx[i] + q.v[Y][i]) + (-q.v[X][i]);
-      const double rlz = (q.v[X][i] + q.v[Z][i]) + (-q.ux[i]);
-      const double ry = q.v[Y][i] * q.v[LY][i] + (-(mu * 1.0));
-      const double rz = q.v[Z][i] * q.v[LZ][i] + (-(mu * 1.0));
+      const double rx = q.vlo ? s + (-q.v[LY][i]) : s;
       q.r[X][i] = rx;
-      q.r[LY][i] = rly;
-      q.r[LZ][i] = rlz;
-      q.r[Y][i] = ry;
-      q.r[Z][i] = rz;
-      res2 += rx * rx + rly * rly + rlz * rlz + ry * ry + rz * rz;
-      comp += fabs(ry) + fabs(rz);
+      res2 += rx * rx;
+      if (q.slacks) {  // (((X - L_x)*lambda_y) - (mu*e_x)), (((U_x - X)*lambda_z) - (mu*e_x))
+        if (q.vlo) {
+          const double r = ((q.v[X][i] + (-q.lx[i])) * q.v[LY][i]) + (-(mu * 1.0));
+          q.r[LY][i] = r;
+          res2 += r * r;
+          comp += fabs(r);
+        }
+        if (q.vup) {
+          const double r = ((q.ux[i] + (-q.v[X][i])) * q.v[LZ][i]) + (-(mu * 1.0));
+          q.r[LZ][i] = r;
+          res2 += r * r;
+          comp += fabs(r);
+        }
+      } else {
+        if (q.vlo) {
+          const double rly = (q.lx[i] + q.v[Y][i]) + (-q.v[X][i]);     // (l_x + y - x)
+          const double ry = q.v[Y][i] * q.v[LY][i] + (-(mu * 1.0));  // ((Y*lambda_y) - (mu*e_x))
+          q.r[LY][i] = rly;
+          q.r[Y][i] = ry;
+          res2 += rly * rly + ry * ry;
+          comp += fabs(ry);
+        }
+        if (q.vup) {
+          const double rlz = (q.v[X][i] + q.v[Z][i]) + (-q.ux[i]);   // (x + z - u_x)
+          const double rz = q.v[Z][i] * q.v[LZ][i] + (-(mu * 1.0));
+          q.r[LZ][i] = rlz;
+          q.r[Z][i] = rz;
+          res2 += rlz * rlz + rz * rz;
+          comp += fabs(rz);
+        }
+      }
       fa += (0.5 * q.v[X][i]) * q.Qx[i];
       fb += q.c[i] * q.v[X][i];
     } else if (t < n + m) {
       const int i = t - n;
-      const double rla = q.Ax[i] + (-q.v[S][i]);
-      const double rs = -((q.v[LA][i] + q.v[LG][i]) + (-q.v[LH][i]));
-      const double rlg = (q.lA[i] + q.v[G][i]) + (-q.v[S][i]);
-      const double rlh = (q.v[H][i] + q.v[S][i]) + (-q.uA[i]);
-      const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));
-      const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
+      const double rla = q.Ax[i] + (-q.v[S][i]);  // ((A*x) - s)
+      double rs;
+      if (q.alo && q.aup) rs = -((q.v[LA][i] + q.v[LG][i]) + (-q.v[LH][i]));  // -(lambda_A + lambda_g - lambda_h)
+      else if (q.alo) rs = -(q.v[LA][i] + q.v[LG][i]);                        // -(lambda_A + lambda_g)
+      else rs = q.v[LH][i] + (-q.v[LA][i]);                                   // (lambda_h - lambda_A)
       q.r[LA][i] = rla;
       q.r[S][i] = rs;
-      q.r[LG][i] = rlg;
-      q.r[LH][i] = rlh;
-      q.r[G][i] = rg;
-      q.r[H][i] = rh;
-      res2 += rla * rla + rs * rs + rlg * rlg + rlh * rlh + rg * rg + rh * rh;
-      comp += fabs(rg) + fabs(rh);
+      res2 += rla * rla + rs * rs;
+      if (q.slacks) {  // (((S - L_A)*lambda_g) - (mu*e_A)), (((U_A - S)*lambda_h) - (mu*e_A))
+        const double rlg = ((q.v[S][i] + (-q.lA[i])) * q.v[LG][i]) + (-(mu * 1.0));
+        const double rlh = ((q.uA[i] + (-q.v[S][i])) * q.v[LH][i]) + (-(mu * 1.0));
+        q.r[LG][i] = rlg;
+        q.r[LH][i] = rlh;
+        res2 += rlg * rlg + rlh * rlh;
+        comp += fabs(rlg) + fabs(rlh);
+      } else {
+        if (q.alo) {
+          const double rlg = (q.lA[i] + q.v[G][i]) + (-q.v[S][i]);  // (l_A + g - s)
+          const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));
+          q.r[LG][i] = rlg;
+          q.r[G][i] = rg;
+          res2 += rlg * rlg + rg * rg;
+          comp += fabs(rg);
+        }
+        if (q.aup) {
+          const double rlh = (q.v[H][i] + q.v[S][i]) + (-q.uA[i]);  // (h + s - u_A)
+          const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
+          q.r[LH][i] = rlh;
+          q.r[H][i] = rh;
+          res2 += rlh * rlh + rh * rh;
+          comp += fabs(rh);
+        }
+      }
     } else {
       const int i = t - n - m;
       if (q.eqnone) {  // ((C*x) - d)
@@ -311,7 +359,7 @@ __global__ void k_stats_final(const QPDev* __restrict__ qs, int nblocks) {
     for (int i = 0; i < NT; ++i)
       for (int k = 0; k < 4; ++k) t[k] += sh[k][i];
     const double res = sqrt(t[0]);
-    const int cnt = 2 * q.n + 2 * q.m;
+    const int cnt = comp_count(q);
     const double mu = cnt == 0 ? 0.0 : t[1] / (double)cnt;
     q.scal[SC_F] = t[2] + t[3];
     q.scal[SC_RES] = res;
@@ -348,6 +396,28 @@ hipError_t qp_evaluate(const QPBatch& qb, hipStream_t st) {
 __device__ __forceinline__ double ds_inv(const QPDev& q, int i) {
   return ipmz_inv(ipmz_inv(q.v[G][i]) * q.v[LG][i] + ipmz_inv(q.v[H][i]) * q.v[LH][i]);
 }
+// Slacks: (((U_A - S)^{-1}*Lambda_h) + ((S - L_A)^{-1}*Lambda_g))^{-1}
+__device__ __forceinline__ double ds_inv_sl(const QPDev& q, int i) {
+  return ipmz_inv(ipmz_inv(q.uA[i] + (-q.v[S][i])) * q.v[LH][i] + ipmz_inv(q.v[S][i] + (-q.lA[i])) * q.v[LG][i]);
+}
+// (x, x) diagonal: Q_ii + the bound terms; (lambda_A, lambda_A) diagonal
+__device__ __forceinline__ double kkt_xx(const QPDev& q, int i, double qii) {
+  double h = qii;
+  if (q.slacks) {  // (Q + ((U_x - X)^{-1}*Lambda_z) + ((X - L_x)^{-1}*Lambda_y))
+    if (q.vup) h = h + ipmz_inv(q.ux[i] + (-q.v[X][i])) * q.v[LZ][i];
+    if (q.vlo) h = h + ipmz_inv(q.v[X][i] + (-q.lx[i])) * q.v[LY][i];
+  } else {  // (Q [+ (Y^{-1}*Lambda_y)] [+ (Z^{-1}*Lambda_z)])
+    if (q.vlo) h = h + ipmz_inv(q.v[Y][i]) * q.v[LY][i];
+    if (q.vup) h = h + ipmz_inv(q.v[Z][i]) * q.v[LZ][i];
+  }
+  return h;
+}
+__device__ __forceinline__ double kkt_aa(const QPDev& q, int i) {
+  if (q.slacks) return -ds_inv_sl(q, i);
+  if (q.alo && q.aup) return -ds_inv(q, i);            // -((G^{-1}*Lambda_g) + (H^{-1}*Lambda_h))^{-1}
+  if (q.alo) return -(ipmz_inv(q.v[LG][i]) * q.v[G][i]);  // -(Lambda_g^{-1}*G)
+  return -(ipmz_inv(q.v[LH][i]) * q.v[H][i]);             // -(Lambda_h^{-1}*H)
+}
 
 __global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
@@ -359,16 +429,13 @@ __global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
   if (i < n) {
     const double* Qr = q.Q + (int64_t)i * q.ldn;
     for (int j = threadIdx.x; j < i; j += NT) Kr[j] = Qr[j];
-    if (threadIdx.x == 0) {
-      const double h = Qr[i] + ipmz_inv(q.v[Y][i]) * q.v[LY][i];
-      Kr[i] = h + ipmz_inv(q.v[Z][i]) * q.v[LZ][i];
-    }
+    if (threadIdx.x == 0) Kr[i] = kkt_xx(q, i, Qr[i]);
   } else if (i < n + m) {
     const int r = i - n;
     const double* Ar = q.A + (int64_t)r * q.ldn;
     for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Ar[j];
     for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
-    if (threadIdx.x == 0) Kr[i] = -ds_inv(q, r);
+    if (threadIdx.x == 0) Kr[i] = kkt_aa(q, r);
   } else {
     const int r = i - n - m;
     const double* Cr = q.C + (int64_t)r * q.ldn;
@@ -391,14 +458,35 @@ __global__ void k_rhs(const QPDev* __restrict__ qs) {
   const int n = q.n, m = q.m;
   if (t < n) {
     const int i = t;
-    const double tz = ipmz_inv(q.v[Z][i]) * (q.r[Z][i] + (-(q.v[LZ][i] * q.r[LZ][i])));
-    const double ty = ipmz_inv(q.v[Y][i]) * (q.r[Y][i] + (-(q.v[LY][i] * q.r[LY][i])));
-    q.b[i] = (tz + (-q.r[X][i])) + (-ty);
+    const double rx = q.r[X][i];
+    if (q.slacks) {  // (((U_x - X)^{-1}*r_lz) - r_x - ((X - L_x)^{-1}*r_ly)), absent terms dropped
+      double b = q.vup ? ipmz_inv(q.ux[i] + (-q.v[X][i])) * q.r[LZ][i] + (-rx) : -rx;
+      if (q.vlo) b = b + (-(ipmz_inv(q.v[X][i] + (-q.lx[i])) * q.r[LY][i]));
+      q.b[i] = b;
+      return;
+    }
+    const double tz = q.vup ? ipmz_inv(q.v[Z][i]) * (q.r[Z][i] + (-(q.v[LZ][i] * q.r[LZ][i]))) : 0.0;
+    const double ty = q.vlo ? ipmz_inv(q.v[Y][i]) * (q.r[Y][i] + (-(q.v[LY][i] * q.r[LY][i]))) : 0.0;
+    if (q.vlo && q.vup) q.b[i] = (tz + (-rx)) + (-ty);
+    else if (q.vup) q.b[i] = tz + (-rx);  // ((Z^{-1}*(r_z - (L_z*r_lz))) - r_x)
+    else if (q.vlo) q.b[i] = -(rx + ty);  // -(r_x + (Y^{-1}*(r_y - (L_y*r_ly))))
+    else q.b[i] = -rx;
   } else if (t < n + m) {
     const int i = t - n;
-    const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
-    const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
-    q.b[t] = ds_inv(q, i) * ((th + (-q.r[S][i])) + (-tg)) + (-q.r[LA][i]);
+    const double rla = q.r[LA][i], rs = q.r[S][i];
+    if (q.slacks) {
+      const double a = ipmz_inv(q.uA[i] + (-q.v[S][i])) * q.r[LH][i];
+      const double c = ipmz_inv(q.v[S][i] + (-q.lA[i])) * q.r[LG][i];
+      q.b[t] = ds_inv_sl(q, i) * ((a + (-rs)) + (-c)) + (-rla);
+    } else if (q.alo && q.aup) {
+      const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
+      const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
+      q.b[t] = ds_inv(q, i) * ((th + (-rs)) + (-tg)) + (-rla);
+    } else if (q.alo) {  // -(r_lA + (L_g^{-1}*(r_g + (G*r_s))) - r_lg)
+      q.b[t] = -((rla + ipmz_inv(q.v[LG][i]) * (q.r[G][i] + q.v[G][i] * rs)) + (-q.r[LG][i]));
+    } else {  // ((L_h^{-1}*(r_h - (H*r_s))) - r_lA - r_lh)
+      q.b[t] = ((ipmz_inv(q.v[LH][i]) * (q.r[H][i] + (-(q.v[H][i] * rs)))) + (-rla)) + (-q.r[LH][i]);
+    }
   } else if (t < q.N) {
     const int i = t - n - m;
     q.b[t] = (q.eqnone || q.eqpen) ? -q.r[LC][i] : q.delta * q.r[P][i] + (-q.r[LC][i]);
@@ -426,28 +514,61 @@ __global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
     const int i = t;
     const double dx = q.b[i];
     D.d[X][i] = dx;
-    D.d[LY][i] = -((ipmz_inv(q.v[Y][i]) * q.v[LY][i]) *
-                   ((dx + ipmz_inv(q.v[LY][i]) * q.r[Y][i]) + (-q.r[LY][i])));
-    D.d[LZ][i] = -((ipmz_inv(q.v[Z][i]) * q.v[LZ][i]) *
-                   ((ipmz_inv(q.v[LZ][i]) * q.r[Z][i] + (-q.r[LZ][i])) + (-dx)));
-    D.d[Y][i] = -(ipmz_inv(q.v[LY][i]) * (q.r[Y][i] + q.v[Y][i] * D.d[LY][i]));
-    D.d[Z][i] = -(ipmz_inv(q.v[LZ][i]) * (q.r[Z][i] + q.v[Z][i] * D.d[LZ][i]));
+    if (q.slacks) {
+      if (q.vlo)  // -((X - L_x)^{-1}*(r_ly + (L_y*dx)))
+        D.d[LY][i] = -(ipmz_inv(q.v[X][i] + (-q.lx[i])) * (q.r[LY][i] + q.v[LY][i] * dx));
+      if (q.vup)  // ((U_x - X)^{-1}*((L_z*dx) - r_lz))
+        D.d[LZ][i] = ipmz_inv(q.ux[i] + (-q.v[X][i])) * (q.v[LZ][i] * dx + (-q.r[LZ][i]));
+      return;
+    }
+    if (q.vlo) {
+      D.d[LY][i] = -((ipmz_inv(q.v[Y][i]) * q.v[LY][i]) *
+                     ((dx + ipmz_inv(q.v[LY][i]) * q.r[Y][i]) + (-q.r[LY][i])));
+      D.d[Y][i] = -(ipmz_inv(q.v[LY][i]) * (q.r[Y][i] + q.v[Y][i] * D.d[LY][i]));
+    }
+    if (q.vup) {
+      D.d[LZ][i] = -((ipmz_inv(q.v[Z][i]) * q.v[LZ][i]) *
+                     ((ipmz_inv(q.v[LZ][i]) * q.r[Z][i] + (-q.r[LZ][i])) + (-dx)));
+      D.d[Z][i] = -(ipmz_inv(q.v[LZ][i]) * (q.r[Z][i] + q.v[Z][i] * D.d[LZ][i]));
+    }
   } else if (t < n + m) {
     const int i = t - n;
-    const double dla = q.b[t];
+    const double dla = q.b[t], rs = q.r[S][i];
     D.d[LA][i] = dla;
-    const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
-    const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
-    const double ds = ds_inv(q, i) * (((dla + th) + (-q.r[S][i])) + (-tg));
+    if (q.slacks) {
+      const double a = ipmz_inv(q.uA[i] + (-q.v[S][i])) * q.r[LH][i];
+      const double c = ipmz_inv(q.v[S][i] + (-q.lA[i])) * q.r[LG][i];
+      const double ds = ds_inv_sl(q, i) * (((dla + a) + (-rs)) + (-c));
+      D.d[S][i] = ds;
+      D.d[LG][i] = -(ipmz_inv(q.v[S][i] + (-q.lA[i])) * (q.r[LG][i] + q.v[LG][i] * ds));
+      D.d[LH][i] = ipmz_inv(q.uA[i] + (-q.v[S][i])) * (q.v[LH][i] * ds + (-q.r[LH][i]));
+      return;
+    }
+    double ds;
+    if (q.alo && q.aup) {
+      const double th = ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])));
+      const double tg = ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i])));
+      ds = ds_inv(q, i) * (((dla + th) + (-rs)) + (-tg));
+    } else if (q.alo) {  // (L_g^{-1}*G*(dla - r_s - (G^{-1}*(r_g - (L_g*r_lg)))))
+      ds = (ipmz_inv(q.v[LG][i]) * q.v[G][i]) *
+           ((dla + (-rs)) + (-(ipmz_inv(q.v[G][i]) * (q.r[G][i] + (-(q.v[LG][i] * q.r[LG][i]))))));
+    } else {  // (L_h^{-1}*H*(dla + (H^{-1}*(r_h - (L_h*r_lh))) - r_s))
+      ds = (ipmz_inv(q.v[LH][i]) * q.v[H][i]) *
+           ((dla + ipmz_inv(q.v[H][i]) * (q.r[H][i] + (-(q.v[LH][i] * q.r[LH][i])))) + (-rs));
+    }
     D.d[S][i] = ds;
-    const double dlg =
-        -((ipmz_inv(q.v[G][i]) * q.v[LG][i]) * ((ds + ipmz_inv(q.v[LG][i]) * q.r[G][i]) + (-q.r[LG][i])));
-    const double dlh =
-        -((ipmz_inv(q.v[H][i]) * q.v[LH][i]) * ((ipmz_inv(q.v[LH][i]) * q.r[H][i] + (-q.r[LH][i])) + (-ds)));
-    D.d[LG][i] = dlg;
-    D.d[LH][i] = dlh;
-    D.d[G][i] = -(ipmz_inv(q.v[LG][i]) * (q.r[G][i] + q.v[G][i] * dlg));
-    D.d[H][i] = -(ipmz_inv(q.v[LH][i]) * (q.r[H][i] + q.v[H][i] * dlh));
+    if (q.alo) {
+      const double dlg =
+          -((ipmz_inv(q.v[G][i]) * q.v[LG][i]) * ((ds + ipmz_inv(q.v[LG][i]) * q.r[G][i]) + (-q.r[LG][i])));
+      D.d[LG][i] = dlg;
+      D.d[G][i] = -(ipmz_inv(q.v[LG][i]) * (q.r[G][i] + q.v[G][i] * dlg));
+    }
+    if (q.aup) {
+      const double dlh =
+          -((ipmz_inv(q.v[H][i]) * q.v[LH][i]) * ((ipmz_inv(q.v[LH][i]) * q.r[H][i] + (-q.r[LH][i])) + (-ds)));
+      D.d[LH][i] = dlh;
+      D.d[H][i] = -(ipmz_inv(q.v[LH][i]) * (q.r[H][i] + q.v[H][i] * dlh));
+    }
   } else if (t < q.N) {
     const int i = t - n - m;
     const double dlc = q.b[t];
@@ -463,8 +584,9 @@ hipError_t qp_backsub(const QPBatch& qb, int which, hipStream_t st) {
 
 // ---------------------------------------------------------------------------
 // get_max_step_ (Optimizer.cpp:270-342): fraction-to-boundary over the
-// non-negative Newton variables, plus explicit x bounds when neither g nor h
-// is a Newton variable (m == 0).
+// non-negative Newton variables, plus -- when neither g nor h is a Newton
+// variable (box-only SlackedSlacks, or Slacks) -- explicit bounds on x
+// (l_x, u_x) and s (l_A, u_A), both always (the environment holds both).
 __global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs, int which) {
   const QPDev& q = qs[blockIdx.y];
   const DSel D = dsel(q, which);
@@ -472,28 +594,34 @@ __global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs,
   double a = 1.0;
   const int n = q.n, m = q.m;
   const int total = n + m;
+  const bool explicit_bounds = q.slacks || m == 0;
+  auto nonneg = [&](int slot, int i) {
+    const double d = D.d[slot][i];
+    if (d < 0.0) a = fmin(a, -q.v[slot][i] / d);
+  };
+  auto bounded = [&](double v, double d, double lo, double up) {
+    if (d < 0.0) a = fmin(a, (lo - v) / d);
+    if (d > 0.0) a = fmin(a, (up - v) / d);
+  };
   for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
     if (t < n) {
       const int i = t;
-      const int sl[4] = {LY, LZ, Y, Z};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double d = D.d[sl[k]][i];
-        if (d < 0.0) a = fmin(a, -q.v[sl[k]][i] / d);
+      if (q.vlo) nonneg(LY, i);
+      if (q.vup) nonneg(LZ, i);
+      if (!q.slacks) {
+        if (q.vlo) nonneg(Y, i);
+        if (q.vup) nonneg(Z, i);
       }
-      if (m == 0) {
-        const double d = D.d[X][i], v = q.v[X][i];
-        if (d < 0.0) a = fmin(a, (q.lx[i] - v) / d);
-        if (d > 0.0) a = fmin(a, (q.ux[i] - v) / d);
-      }
+      if (explicit_bounds) bounded(q.v[X][i], D.d[X][i], q.lx[i], q.ux[i]);
     } else {
       const int i = t - n;
-      const int sl[4] = {LG, LH, G, H};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const double d = D.d[sl[k]][i];
-        if (d < 0.0) a = fmin(a, -q.v[sl[k]][i] / d);
+      if (q.alo) nonneg(LG, i);
+      if (q.aup) nonneg(LH, i);
+      if (!q.slacks) {
+        if (q.alo) nonneg(G, i);
+        if (q.aup) nonneg(H, i);
       }
+      if (explicit_bounds) bounded(q.v[S][i], D.d[S][i], q.lA[i], q.uA[i]);
     }
   }
   a = block_min(a, sh);
@@ -515,25 +643,36 @@ hipError_t qp_ratio(const QPBatch& qb, int which, int out_index, hipStream_t st)
   return hipGetLastError();
 }
 
-// mu at the affine trial point v + alpha_aff * daff (Optimizer.cpp:167-180).
+// mu at the affine trial point v + alpha_aff * daff (Optimizer.cpp:167-180):
+// |complementarity| of every row that carries e and mu, at the trial point.
 __global__ __launch_bounds__(NT) void k_mu_aff_part(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   const double al = q.scal[SC_ALPHA_AFF];
   double s = 0.0;
   const int n = q.n, m = q.m;
+  auto tv = [&](int slot, int i) { return q.v[slot][i] + al * q.daff[slot][i]; };
+  auto term = [&](double a, double b) { return fabs(-(a * b + (-(0.0 * 1.0)))); };
   for (int t = blockIdx.x * NT + threadIdx.x; t < n + m; t += gridDim.x * NT) {
-    int c0, d0, c1, d1, i;
     if (t < n) {
-      i = t;
-      c0 = Y; d0 = LY; c1 = Z; d1 = LZ;
+      const int i = t;
+      if (q.slacks) {
+        if (q.vlo) s += term(tv(X, i) + (-q.lx[i]), tv(LY, i));  // ((X - L_x)*lambda_y)
+        if (q.vup) s += term(q.ux[i] + (-tv(X, i)), tv(LZ, i));  // ((U_x - X)*lambda_z)
+      } else {
+        if (q.vlo) s += term(tv(Y, i), tv(LY, i));
+        if (q.vup) s += term(tv(Z, i), tv(LZ, i));
+      }
     } else {
-      i = t - n;
-      c0 = G; d0 = LG; c1 = H; d1 = LH;
+      const int i = t - n;
+      if (q.slacks) {
+        s += term(tv(S, i) + (-q.lA[i]), tv(LG, i));  // ((S - L_A)*lambda_g)
+        s += term(q.uA[i] + (-tv(S, i)), tv(LH, i));  // ((U_A - S)*lambda_h)
+      } else {
+        if (q.alo) s += term(tv(G, i), tv(LG, i));
+        if (q.aup) s += term(tv(H, i), tv(LH, i));
+      }
     }
-    const double a0 = q.v[c0][i] + al * q.daff[c0][i], b0 = q.v[d0][i] + al * q.daff[d0][i];
-    const double a1 = q.v[c1][i] + al * q.daff[c1][i], b1 = q.v[d1][i] + al * q.daff[d1][i];
-    s += fabs(-(a0 * b0 + (-(0.0 * 1.0)))) + fabs(-(a1 * b1 + (-(0.0 * 1.0))));
   }
   s = block_sum(s, sh);
   if (threadIdx.x == 0) q.part[blockIdx.x] = s;
@@ -545,7 +684,7 @@ __global__ void k_mu_aff_final(const QPDev* __restrict__ qs, int nblocks) {
   for (int b = threadIdx.x; b < nblocks; b += NT) s += q.part[b];
   s = block_sum(s, sh);
   if (threadIdx.x == 0) {
-    const int cnt = 2 * q.n + 2 * q.m;
+    const int cnt = comp_count(q);
     const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
     const double mu = q.scal[SC_MU];
     const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
@@ -562,27 +701,51 @@ hipError_t qp_mu_aff(const QPBatch& qb, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Corrector (Optimizer.cpp:183-209): r_v = (V lambda - mu_new e) + dV_aff dlambda_aff.
+// Corrector (Optimizer.cpp:183-209): every complementarity row at mu_new plus
+// the same row with mu -> 0 and every VARIABLE replaced by its affine
+// direction: SlackedSlacks r_y = (Y lambda_y - mu_new e) + (dY_aff
+// dlambda_y_aff - 0 e); Slacks r_lambda_y = ((X - L_x) lambda_y - mu_new e) +
+// ((dX_aff - L_x) dlambda_y_aff - 0 e) -- the bound constant leaks into the
+// correction (the reference's Slacks defect, SURVEY.md App. C.1, reproduced).
 __global__ void k_corrector(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
   const int t = blockIdx.x * NT + threadIdx.x;
   const double mu = q.scal[SC_MU_NEW];
   const int n = q.n, m = q.m;
-  int c0, d0, c1, d1, i;
+  const double* const* v = q.v;
+  const double* const* da = q.daff;
+  auto ss = [&](int c, int d, int i) {  // SlackedSlacks pair (c = slack, d = its dual)
+    q.r[c][i] = (v[c][i] * v[d][i] + (-(mu * 1.0))) + (da[c][i] * da[d][i] + (-(0.0 * 1.0)));
+  };
   if (t < n) {
-    i = t;
-    c0 = Y; d0 = LY; c1 = Z; d1 = LZ;
+    const int i = t;
+    if (q.slacks) {
+      if (q.vlo)
+        q.r[LY][i] = (((v[X][i] + (-q.lx[i])) * v[LY][i]) + (-(mu * 1.0))) +
+                     ((da[X][i] + (-q.lx[i])) * da[LY][i] + (-(0.0 * 1.0)));
+      if (q.vup)
+        q.r[LZ][i] = (((q.ux[i] + (-v[X][i])) * v[LZ][i]) + (-(mu * 1.0))) +
+                     ((q.ux[i] + (-da[X][i])) * da[LZ][i] + (-(0.0 * 1.0)));
+    } else {
+      if (q.vlo) ss(Y, LY, i);
+      if (q.vup) ss(Z, LZ, i);
+    }
   } else if (t < n + m) {
-    i = t - n;
-    c0 = G; d0 = LG; c1 = H; d1 = LH;
+    const int i = t - n;
+    if (q.slacks) {
+      q.r[LG][i] = (((v[S][i] + (-q.lA[i])) * v[LG][i]) + (-(mu * 1.0))) +
+                   ((da[S][i] + (-q.lA[i])) * da[LG][i] + (-(0.0 * 1.0)));
+      q.r[LH][i] = (((q.uA[i] + (-v[S][i])) * v[LH][i]) + (-(mu * 1.0))) +
+                   ((q.uA[i] + (-da[S][i])) * da[LH][i] + (-(0.0 * 1.0)));
+    } else {
+      if (q.alo) ss(G, LG, i);
+      if (q.aup) ss(H, LH, i);
+    }
   } else {
     // PenaltyFunction: r_lambda_C carries mu (no e, so no affine correction)
-    i = t - n - m;
-    if (q.eqpen && i < q.p) q.r[LC][i] = -((q.d[i] + mu * q.v[LC][i]) + (-q.Cx[i]));
-    return;
+    const int i = t - n - m;
+    if (q.eqpen && i < q.p) q.r[LC][i] = -((q.d[i] + mu * v[LC][i]) + (-q.Cx[i]));
   }
-  q.r[c0][i] = (q.v[c0][i] * q.v[d0][i] + (-(mu * 1.0))) + (q.daff[c0][i] * q.daff[d0][i] + (-(0.0 * 1.0)));
-  q.r[c1][i] = (q.v[c1][i] * q.v[d1][i] + (-(mu * 1.0))) + (q.daff[c1][i] * q.daff[d1][i] + (-(0.0 * 1.0)));
 }
 
 hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st) {
@@ -600,19 +763,25 @@ __global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
   const int t = blockIdx.x * NT + threadIdx.x;
   const double s = 0.995 * q.scal[SC_ALPHA];
   const int n = q.n, m = q.m, p = q.p;
+  auto up = [&](int slot, int i) { q.v[slot][i] = q.v[slot][i] + s * q.dir[slot][i]; };
   if (t < n) {
-    const int sl[5] = {X, LY, LZ, Y, Z};
-#pragma unroll
-    for (int k = 0; k < 5; ++k) q.v[sl[k]][t] = q.v[sl[k]][t] + s * q.dir[sl[k]][t];
+    up(X, t);
+    if (q.vlo) up(LY, t);
+    if (q.vup) up(LZ, t);
+    if (q.vlo && !q.slacks) up(Y, t);
+    if (q.vup && !q.slacks) up(Z, t);
   }
   if (t < m) {
-    const int sl[6] = {LA, S, LG, LH, G, H};
-#pragma unroll
-    for (int k = 0; k < 6; ++k) q.v[sl[k]][t] = q.v[sl[k]][t] + s * q.dir[sl[k]][t];
+    up(LA, t);
+    up(S, t);
+    if (q.alo) up(LG, t);
+    if (q.aup) up(LH, t);
+    if (q.alo && !q.slacks) up(G, t);
+    if (q.aup && !q.slacks) up(H, t);
   }
   if (t < p) {
-    q.v[LC][t] = q.v[LC][t] + s * q.dir[LC][t];
-    if (!q.eqnone && !q.eqpen) q.v[P][t] = q.v[P][t] + s * q.dir[P][t];
+    up(LC, t);
+    if (!q.eqnone && !q.eqpen) up(P, t);
   }
 }
 

@@ -9,10 +9,9 @@
 // Same names, argument meaning and error behaviour: value-returning factor
 // (fresh L and D), in-place solve, and failures thrown as AssertionError,
 // a std::logic_error (Utils::AssertionError, Assert.h:7-12).  Formulation:
-// InequalityHandling::SlackedSlacks, Bounds::Both, and
-// EqualityHandling::Regularization when equality rows are present; the other
-// Settings the reference's numeric path cannot run are
-// rejected with AssertionError.
+// Settings below (default SlackedSlacks, Bounds::Both, Regularization when
+// equality rows are present); Settings the numeric path cannot run (SURVEY.md
+// §0.3) are rejected with AssertionError.
 #pragma once
 #include <cstdint>
 #include <stdexcept>
@@ -115,15 +114,40 @@ enum class EqualityHandling {
   PenaltyFunction = IPMZ_EQ_PENALTY
 };
 
+// Settings::Bounds and Settings::InequalityHandling (SymbolicOptimization.h:
+// 28-39): the numeric path runs SlackedSlacks and Slacks (Slacks with Both
+// bounds only); NaiveSlacks is rejected.
+enum class Bounds { None = IPMZ_BOUNDS_NONE, Lower = IPMZ_BOUNDS_LOWER, Upper = IPMZ_BOUNDS_UPPER, Both = IPMZ_BOUNDS_BOTH };
+enum class InequalityHandling { Slacks = IPMZ_INEQ_SLACKS, SlackedSlacks = IPMZ_INEQ_SLACKED_SLACKS };
+
+// The subset of Settings (SymbolicOptimization.h:58-64) that selects the
+// Newton system; defaults are this library's (Regularization when equality
+// rows exist), not the reference's EqualityHandling::None.
+struct Settings {
+  Bounds inequalities = Bounds::Both;
+  Bounds variable_bounds = Bounds::Both;
+  EqualityHandling equality_handling = EqualityHandling::Regularization;
+  InequalityHandling inequality_handling = InequalityHandling::SlackedSlacks;
+};
+
 // build_environment + Optimizer: the iterate lives in device memory; solve()
 // runs Optimizer.cpp:124-219 (tolerance 1e-8, at most 100 iterations).
 class Optimizer {
  public:
   explicit Optimizer(const Data& d, Context& ctx = Context::instance(),
-                     EqualityHandling eq = EqualityHandling::Regularization) {
+                     EqualityHandling eq = EqualityHandling::Regularization)
+      : Optimizer(d, Settings{Bounds::Both, Bounds::Both, eq, InequalityHandling::SlackedSlacks}, ctx) {}
+  Optimizer(const Data& d, const Settings& st, Context& ctx = Context::instance()) {
     const int n = (int)d.Q.size(), m = (int)d.A_ineq.size(), p = (int)d.A_eq.size();
     n_ = n;
-    ipmz_qp_config cfg{n, m, p, 1e-4, static_cast<int>(eq)};
+    ipmz_qp_config cfg{n,
+                       m,
+                       p,
+                       1e-4,
+                       static_cast<int>(st.equality_handling),
+                       static_cast<int>(st.inequality_handling),
+                       static_cast<int>(st.inequalities),
+                       static_cast<int>(st.variable_bounds)};
     check(ipmz_qp_create(ctx.get(), &cfg, &h_), "ipmz_qp_create");
     auto flat = [](const Matrix& M, size_t cols) {
       std::vector<double> f;

@@ -62,11 +62,18 @@ class IpmzError(AssertionError):
 EQ_REGULARIZATION = 0  # Settings::EqualityHandling::Regularization (include/ipmz.h IPMZ_EQ_*)
 EQ_NONE = 1            # zero (lambda_C, lambda_C) block, Bunch-Kaufman factor
 EQ_PENALTY = 2         # PenaltyFunction: -mu (lambda_C, lambda_C) block, LDL^T
+INEQ_SLACKED_SLACKS = 0  # Settings::InequalityHandling (include/ipmz.h IPMZ_INEQ_*)
+INEQ_SLACKS = 1          # no g/h/y/z slacks (the reference's corrector defect reproduced)
+BOUNDS_BOTH = 0          # Settings::Bounds (include/ipmz.h IPMZ_BOUNDS_*)
+BOUNDS_LOWER = 1
+BOUNDS_UPPER = 2
+BOUNDS_NONE = 3
 
 
 class _QPConfig(ctypes.Structure):
     _fields_ = [("n", ctypes.c_int), ("m", ctypes.c_int), ("p", ctypes.c_int), ("delta", ctypes.c_double),
-                ("equality_handling", ctypes.c_int)]
+                ("equality_handling", ctypes.c_int), ("inequality_handling", ctypes.c_int),
+                ("inequality_bounds", ctypes.c_int), ("variable_bounds", ctypes.c_int)]
 
 
 def _load():
@@ -349,17 +356,23 @@ class Data:
 class Optimizer:
     """The Newton-step solver: build_environment + Optimizer (Optimizer.h:15-20).
 
-    Formulation: InequalityHandling::SlackedSlacks with Bounds::Both, and
-    EqualityHandling::Regularization (delta = 1e-4) when equalities exist --
-    or equality_handling=EQ_NONE: the zero (lambda_C, lambda_C) block the
+    Formulation (Settings, SymbolicOptimization.h:28-64): by default
+    InequalityHandling::SlackedSlacks with Bounds::Both, and
+    EqualityHandling::Regularization (delta = 1e-4) when equalities exist.
+    equality_handling=EQ_NONE: the zero (lambda_C, lambda_C) block the
     reference routes to solve_indefinite_ (Optimizer.cpp:63-75), factored
-    with Bunch-Kaufman (N <= 4096).
+    with Bunch-Kaufman (N <= 4096); EQ_PENALTY: PenaltyFunction.
+    inequality_handling=INEQ_SLACKS, inequality_bounds / variable_bounds =
+    BOUNDS_LOWER / UPPER / NONE select the other Newton systems (absent
+    blocks dropped from the Newton order, as the reference does).
     """
 
-    def __init__(self, n, m=0, p=0, ctx=None, delta=1e-4, equality_handling=0):
+    def __init__(self, n, m=0, p=0, ctx=None, delta=1e-4, equality_handling=0, inequality_handling=0,
+                 inequality_bounds=0, variable_bounds=0):
         self.ctx = ctx or default_context()
-        cfg = _QPConfig(n, m, p, delta, equality_handling)
+        cfg = _QPConfig(n, m, p, delta, equality_handling, inequality_handling, inequality_bounds, variable_bounds)
         self.equality_handling = equality_handling
+        self.form = (inequality_handling, inequality_bounds, variable_bounds)
         h = _VP()
         _check(lib.ipmz_qp_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)), "ipmz_qp_create")
         self.h = h
@@ -368,9 +381,9 @@ class Optimizer:
         self.state_len = lib.ipmz_qp_state_len(h)
 
     @classmethod
-    def from_data(cls, data, ctx=None):
+    def from_data(cls, data, ctx=None, **form):
         n, m, p = data.Q.shape[0], data.A_ineq.shape[0], data.A_eq.shape[0]
-        o = cls(n, m, p, ctx)
+        o = cls(n, m, p, ctx, **form)
         o.load(data)
         return o
 
@@ -471,10 +484,12 @@ class Batch(Optimizer):
     kernel launch serves the whole batch.  QP i of generate(seed) uses
     seed + i."""
 
-    def __init__(self, n, m=0, p=0, batch=1, ctx=None, delta=1e-4, equality_handling=0):
+    def __init__(self, n, m=0, p=0, batch=1, ctx=None, delta=1e-4, equality_handling=0, inequality_handling=0,
+                 inequality_bounds=0, variable_bounds=0):
         self.ctx = ctx or default_context()
-        cfg = _QPConfig(n, m, p, delta, equality_handling)
+        cfg = _QPConfig(n, m, p, delta, equality_handling, inequality_handling, inequality_bounds, variable_bounds)
         self.equality_handling = equality_handling
+        self.form = (inequality_handling, inequality_bounds, variable_bounds)
         h = _VP()
         _check(lib.ipmz_batch_create(self.ctx.h, ctypes.byref(cfg), batch, ctypes.byref(h)), "ipmz_batch_create")
         self.h = h

@@ -22,7 +22,8 @@ SLOTS = ["x", "lambda_A", "lambda_C", "s", "p", "lambda_g", "lambda_h", "lambda_
 NONNEG = {"lambda_g", "lambda_h", "lambda_y", "lambda_z", "g", "h", "y", "z"}
 
 
-# Settings (SymbolicOptimization.h:28-64): Bounds as bit masks (ipmz.h IPMZ_BOUNDS_*)
+# Settings (SymbolicOptimization.h:28-64): Bounds as bit masks 1 = Lower, 2 = Upper
+# (the C ABI encodes them as IPMZ_BOUNDS_*, Both = 0; tests map between the two)
 BOUNDS = {"None": 0, "Lower": 1, "Upper": 2, "Both": 3}
 
 

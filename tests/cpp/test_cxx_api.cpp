@@ -60,6 +60,27 @@ int main() {
   // optimum: x1 + x2 <= 1.2 active, x2 at 0 -> x = (1.2, 0)
   EXPECT(std::fabs(x[0] - 1.2) < 1e-6 && std::fabs(x[1]) < 1e-6);
 
+  // the same optimum with only the active sides of the bounds (Settings,
+  // SymbolicOptimization.h:58-64): x1 + x2 <= 1.2 and x >= 0
+  Settings st;
+  st.inequalities = Bounds::Upper;
+  st.variable_bounds = Bounds::Lower;
+  Optimizer one_sided(d, st);
+  auto trace1 = one_sided.solve();
+  auto x1 = one_sided.x();
+  EXPECT(!trace1.empty() && trace1.size() < 100);
+  EXPECT(std::fabs(x1[0] - 1.2) < 1e-6 && std::fabs(x1[1]) < 1e-6);
+  EXPECT(one_sided.variables().size() == 2 + 2 * 2 + 4 * 1);  // x, lambda_y, y; lambda_A, s, lambda_h, h
+  // Slacks is built on both bounds: one-sided settings are rejected
+  st.inequality_handling = InequalityHandling::Slacks;
+  threw = false;
+  try {
+    Optimizer o3(d, st);
+  } catch (const ipmz::AssertionError&) {
+    threw = true;
+  }
+  EXPECT(threw);
+
   // build_environment validation: l_x < u_x (EnvironmentBuilder.cpp:12-14)
   Data bad = d;
   bad.u_x = {0.0, 10.0};

@@ -1,0 +1,134 @@
+"""The other Newton systems on the GPU (Settings, SymbolicOptimization.h:
+28-64): one-sided / absent variable and inequality bounds and
+InequalityHandling::Slacks (with the reference's corrector defect), through
+the C ABI, against the reference's own Newton traces (tests/golden/
+{vlo,vup,vnone,alo,aup,vlo0,sl,slbox}_*, made by tests/golden/make_golden.py)
+and against the oracle at blocked-factor sizes.
+
+Tolerances as tests/test_gpu_parity.py: element-wise formulas (initial
+iterate, KKT assembly) bit-identical; directions 1e-9 relative per block and
+||dx_gpu - dx_ref||_inf < 1e-10 (BASELINE.json north_star)."""
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import load, sym_from_lower, trace
+
+pytestmark = pytest.mark.gpu
+
+I = pytest.importorskip("ipmz_amd")
+
+DX_TOL = 1e-10
+ABI_BOUNDS = {3: I.BOUNDS_BOTH, 1: I.BOUNDS_LOWER, 2: I.BOUNDS_UPPER, 0: I.BOUNDS_NONE}
+
+# (tag, n, m, oracle.Form(slacks, inequality bounds mask, variable bounds mask)),
+# as tests/test_oracle_golden.py FORMS
+FORMS = [
+    ("vlo", 48, 16, oracle.Form(False, 3, 1)), ("vup", 48, 16, oracle.Form(False, 3, 2)),
+    ("vnone", 48, 16, oracle.Form(False, 3, 0)), ("alo", 48, 16, oracle.Form(False, 1, 3)),
+    ("aup", 48, 16, oracle.Form(False, 2, 3)), ("vlo0", 48, 0, oracle.Form(False, 0, 1)),
+    ("sl", 48, 16, oracle.Form(True, 3, 3)), ("slbox", 48, 0, oracle.Form(True, 0, 3)),
+]
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return I.Context(0)
+
+
+def _abi(form):
+    return dict(inequality_handling=I.INEQ_SLACKS if form.slacks else I.INEQ_SLACKED_SLACKS,
+                inequality_bounds=ABI_BOUNDS[form.ineq_bounds], variable_bounds=ABI_BOUNDS[form.var_bounds])
+
+
+def _close(got, ref, label):
+    scale = max(1.0, np.abs(ref).max())
+    assert np.abs(got - ref).max() < 1e-9 * scale, label
+
+
+@pytest.mark.parametrize("tag,n,m,form", FORMS, ids=[f[0] for f in FORMS])
+def test_formulation_golden_trace(ctx, tag, n, m, form):
+    names, rows, conv = trace(tag)
+    g = I.Optimizer(n, m, 0, ctx, **_abi(form))
+    g.generate(7)
+    assert g.state_len == len(load(f"{tag}_it0_vars.bin"))
+    # initial iterate and KKT assembly: element-wise, bit for bit
+    assert np.array_equal(g.vars(), load(f"{tag}_it0_vars.bin"))
+    assert np.array_equal(g.kkt(), np.tril(sym_from_lower(load(f"{tag}_it0_kkt.bin"), n + m)))
+    o = oracle.OracleQP(oracle.gen_qp(n, m, 0, 7), form=form)
+    for it, ref in enumerate(rows):
+        g.set_vars(load(f"{tag}_it{it}_vars.bin"))
+        s0 = g.scalars()
+        for k in ("f", "res", "mu"):
+            assert abs(s0[k] - ref[k]) <= 1e-12 * max(1.0, abs(ref[k])), (tag, it, k, s0[k], ref[k])
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - ref[k]) <= 1e-9 * max(1.0, abs(ref[k])), (tag, it, k, s1[k], ref[k])
+        for got, which in ((g.daff(), "daff"), (g.dir(), "d")):
+            want = load(f"{tag}_it{it}_{which}.bin")
+            so, sg = o.split(want), o.split(got)
+            for s in o.order:
+                _close(sg[s], so[s], (tag, it, which, s))
+            assert np.abs(sg["x"] - so["x"]).max() < DX_TOL, (tag, it, which)
+        if it + 1 < len(rows):  # the update: v + 0.995 alpha d, element-wise
+            _close(g.vars(), load(f"{tag}_it{it + 1}_vars.bin"), (tag, it, "update"))
+
+
+@pytest.mark.parametrize("tag,form", [(f[0], f[3]) for f in FORMS], ids=[f[0] for f in FORMS])
+def test_formulation_blocked_vs_oracle(ctx, tag, form):
+    # past one diagonal block (nbi = 64) and with equality rows (Regularization)
+    n, m, p, seed = 300, (0 if tag in ("vlo0", "slbox") else 70), 30, 3
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), form=form)
+    g = I.Optimizer(n, m, p, ctx, **_abi(form))
+    g.generate(seed)
+    assert np.array_equal(g.vars(), o.vars())
+    assert np.array_equal(g.kkt(), np.tril(o.kkt()))
+    for it in range(4):
+        s0 = g.scalars()
+        done, rec = o.iterate()
+        for k in ("f", "res", "mu"):
+            assert abs(s0[k] - rec[k]) <= 1e-12 * max(1.0, abs(rec[k])), (tag, it, k)
+        if done:
+            break
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (tag, it, k, s1[k], rec[k])
+        for which, (a, b) in enumerate(((g.daff(), o.daff()), (g.dir(), o.dir()))):
+            sa, sb = o.split(a), o.split(b)
+            for s in o.order:
+                _close(sa[s], sb[s], (tag, it, which, s))
+            assert np.abs(sa["x"] - sb["x"]).max() < DX_TOL, (tag, it, which)
+        g.set_vars(o.vars())
+
+
+def test_formulation_batch_matches_single(ctx):
+    n, m, B = 96, 24, 3
+    form = dict(inequality_handling=I.INEQ_SLACKED_SLACKS, inequality_bounds=I.BOUNDS_LOWER,
+                variable_bounds=I.BOUNDS_UPPER)
+    bt = I.Batch(n, m, 0, B, ctx, **form)
+    bt.generate(11)
+    bt.step()
+    g = I.Optimizer(n, m, 0, ctx, **form)
+    g.generate(12)  # QP 1 of the batch uses seed + 1
+    g.step()
+    sc = g.scalars()
+    import torch
+    dst = torch.zeros(B * I.SC_COUNT, dtype=torch.float64, device="cuda")
+    bt.copy_batch_scalars(dst.data_ptr())
+    torch.cuda.synchronize()
+    ref = dst.cpu().numpy().reshape(B, I.SC_COUNT)
+    for k in ("alpha_aff", "alpha", "mu_aff"):
+        assert abs(ref[1, I.SC[k]] - sc[k]) <= 1e-12 * max(1.0, abs(sc[k])), k
+
+
+@pytest.mark.parametrize("kw,msg", [
+    (dict(inequality_bounds=3), "m > 0 with no inequality bound"),
+    (dict(inequality_handling=1, variable_bounds=1), "Slacks with one-sided bounds"),
+    (dict(inequality_handling=2), "NaiveSlacks"),
+    (dict(variable_bounds=4), "unknown bounds"),
+])
+def test_formulation_rejected(ctx, kw, msg):
+    with pytest.raises(I.IpmzError):
+        I.Optimizer(16, 4, 0, ctx, **kw)
