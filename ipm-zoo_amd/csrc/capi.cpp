@@ -751,7 +751,8 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
   return IPMZ_OK;
 }
 
-int factor_batch(ipmz_qp* s, TrailTimer* tt) {
+// info_reset: the caller already reset the batched factor's info word
+int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   if (s->eqnone) {  // zero diagonal block: symmetric_indefinite_factorization (reference kp behaviour)
     HIP_OK(bk_factor(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->B, s->sK, s->sP, s->ctx->stream));
     return IPMZ_OK;
@@ -767,11 +768,15 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt) {
   bs.sD = s->sD;
   bs.sL = s->sL;
   bs.sW = s->sW;
-  HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
+  if (!info_reset) HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
   HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
                              s->ctx->stream, bs));
   return IPMZ_OK;
 }
+
+// batches of small systems: the O(N) / O(n^2) phases as three per-QP
+// workgroup kernels (newton.hip k_fused_*)
+bool fused_phases(const ipmz_qp* s) { return s->B > 1 && s->N <= IPMZ_FUSED_NMAX; }
 
 int run_step(ipmz_qp* s, int flags) {
   hipStream_t st = s->ctx->stream;
@@ -780,36 +785,57 @@ int run_step(ipmz_qp* s, int flags) {
   auto mark = [&](int i) {
     if (t) hipEventRecord(s->ev[i], st);
   };
-  if (flags & IPMZ_STEP_RESTART_IF_CONVERGED) HIP_OK(qp_restart_if_converged(qb, st));
-  const int freeze = (flags & IPMZ_STEP_RESTART_IF_CONVERGED) ? 0 : 1;
-  mark(0);
-  HIP_OK(qp_assemble(qb, st));
-  mark(1);
+  const bool restart = flags & IPMZ_STEP_RESTART_IF_CONVERGED;
+  const int freeze = restart ? 0 : 1;
+  const bool fused = fused_phases(s);
   TrailTimer tt;
   tt.pairs = s->tr_pairs;
   tt.cap = t ? s->tr_cap : 0;
-  int rc = factor_batch(s, t ? &tt : nullptr);
-  if (rc) return rc;
-  mark(2);
-  // predictor (affine scaling) direction
-  HIP_OK(qp_rhs(qb, st));
-  if ((rc = solve_batch(s, st, 0))) return rc;
-  mark(3);
-  HIP_OK(qp_backsub(qb, 0, st));
-  HIP_OK(qp_ratio(qb, 0, SC_ALPHA_AFF, st));
-  HIP_OK(qp_mu_aff(qb, st));
-  // centering-corrector direction
-  HIP_OK(qp_corrector_residuals(qb, st));
-  HIP_OK(qp_rhs(qb, st));
-  mark(4);
-  if ((rc = solve_batch(s, st, 1))) return rc;
-  mark(5);
-  HIP_OK(qp_backsub(qb, 1, st));
-  HIP_OK(qp_ratio(qb, 1, SC_ALPHA, st));
-  HIP_OK(qp_update(qb, freeze, st));
-  mark(6);
-  HIP_OK(qp_evaluate(qb, st));
-  mark(7);
+  int rc;
+  if (fused) {
+    // phases: assemble = pre (restart, assembly, affine rhs); factor;
+    // solve = the two solves; eval = mid + post
+    mark(0);
+    HIP_OK(qp_fused_pre(qb, restart ? 1 : 0, s->eqnone ? nullptr : s->binfo, st));
+    mark(1);
+    if ((rc = factor_batch(s, nullptr, true))) return rc;
+    mark(2);
+    if ((rc = solve_batch(s, st, 0))) return rc;
+    mark(3);
+    HIP_OK(qp_fused_mid(qb, st));
+    mark(4);
+    if ((rc = solve_batch(s, st, 1))) return rc;
+    mark(5);
+    HIP_OK(qp_fused_post(qb, freeze, st));
+    mark(6);
+    mark(7);
+  } else {
+    if (restart) HIP_OK(qp_restart_if_converged(qb, st));
+    mark(0);
+    HIP_OK(qp_assemble(qb, st));
+    mark(1);
+    if ((rc = factor_batch(s, t ? &tt : nullptr, false))) return rc;
+    mark(2);
+    // predictor (affine scaling) direction
+    HIP_OK(qp_rhs(qb, st));
+    if ((rc = solve_batch(s, st, 0))) return rc;
+    mark(3);
+    HIP_OK(qp_backsub(qb, 0, st));
+    HIP_OK(qp_ratio(qb, 0, SC_ALPHA_AFF, st));
+    HIP_OK(qp_mu_aff(qb, st));
+    // centering-corrector direction
+    HIP_OK(qp_corrector_residuals(qb, st));
+    HIP_OK(qp_rhs(qb, st));
+    mark(4);
+    if ((rc = solve_batch(s, st, 1))) return rc;
+    mark(5);
+    HIP_OK(qp_backsub(qb, 1, st));
+    HIP_OK(qp_ratio(qb, 1, SC_ALPHA, st));
+    HIP_OK(qp_update(qb, freeze, st));
+    mark(6);
+    HIP_OK(qp_evaluate(qb, st));
+    mark(7);
+  }
   if (t) {
     HIP_OK(hipStreamSynchronize(st));
     float ms = 0.f;
@@ -821,7 +847,7 @@ int run_step(ipmz_qp* s, int flags) {
     s->ph_ms[IPMZ_PH_ASSEMBLE] += el(0, 1);
     s->ph_ms[IPMZ_PH_FACTOR] += el(1, 2);
     s->ph_ms[IPMZ_PH_SOLVE] += el(2, 3) + el(4, 5);
-    s->ph_ms[IPMZ_PH_EVAL] += el(6, 7);
+    s->ph_ms[IPMZ_PH_EVAL] += fused ? el(3, 4) + el(5, 6) : el(6, 7);
     for (int i = 0; i < tt.used; ++i) {
       hipEventElapsedTime(&ms, s->tr_pairs[i][0], s->tr_pairs[i][1]);
       s->ph_ms[IPMZ_PH_TRAILING] += ms;
@@ -907,11 +933,14 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   double* scal0 = dev_array(s, SC_COUNT);
   double* part = dev_array(s, 4 * 1024, &sPart);
   double* tpart = dev_array(s, (int64_t)((m > p ? m : p) + 127) / 128 * n + 8, &sT);
+  int64_t sDone;
+  double* done = dev_array(s, 1, &sDone);
   s->K = dev_array(s, (int64_t)N * s->ldk, &s->sK);
   s->D = dev_array(s, N, &s->sD);
   s->sb = sNb;
   bool ok = Q && A && C && c && lx && ux && Qx && ATl && CTl && lA && uA && Ax && d && Cx && v && r && da && di &&
-            v0 && r0 && bvec && scal && scal0 && part && tpart && s->K && s->D;
+            v0 && r0 && bvec && scal && scal0 && part && tpart && done && s->K && s->D &&
+            hipMemset(done, 0, (size_t)(sDone * B) * sizeof(double)) == hipSuccess;
   if (ok && B == 1) {
     s->ws_bytes = ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
     void* w = nullptr;
@@ -988,6 +1017,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.part = part + i * sPart;
     q.tpart = tpart + i * sT;
     q.K = s->K + i * s->sK;
+    q.done = reinterpret_cast<unsigned*>(done + i * sDone);
   }
   void* dqp = nullptr;
   if (hipMalloc(&dqp, sizeof(QPDev) * B) != hipSuccess) {

@@ -199,6 +199,7 @@ struct QPDev {
   double* tpart;  // transposed-GEMV partials
   double* K;      // KKT / factor (N x ldk)
   double *v0, *r0, *scal0;  // initial iterate snapshot (benchmark restarts)
+  unsigned* done;           // fused evaluation: arrival counter of the QP's workgroups (0 between launches)
 };
 
 // A batch of QPs with identical (n, m, p): d = device array of B
@@ -226,5 +227,13 @@ hipError_t qp_restart_if_converged(const QPBatch& qb, hipStream_t st);
 hipError_t qp_save_initial(const QPBatch& qb, hipStream_t st);
 // out (device, 3 doubles) = {max res, max mu, unconverged count} over the batch
 hipError_t qp_batch_summary(const QPBatch& qb, double* out, hipStream_t st);
+// Fused per-QP phases for batches of small systems (one workgroup per QP):
+// pre = restart-if-converged + assembly + affine rhs (+ info word reset),
+// mid = predictor back-substitution .. corrector rhs, post = corrector
+// back-substitution + update + evaluation.  N <= IPMZ_FUSED_NMAX.
+#define IPMZ_FUSED_NMAX 1024
+hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st);
+hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st);
+hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st);  // (+ the evaluation)
 
 }  // namespace ipmz

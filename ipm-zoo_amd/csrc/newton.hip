@@ -16,6 +16,7 @@
 // Everything here is HBM-bound O(n^2) (matvecs, assembly) or O(N) work.
 #include "common.h"
 #include "kernels.h"
+#include "sync.h"
 
 namespace ipmz {
 
@@ -44,6 +45,29 @@ __device__ __forceinline__ double block_min(double v, double* sh) {
   double t = 1.0;
   if (threadIdx.x == 0)
     for (int w = 0; w < NT / 64; ++w) t = fmin(t, sh[w]);
+  return t;
+}
+// every thread gets the result (fused per-QP kernels); deterministic order
+template <int NTH>
+__device__ __forceinline__ double block_allsum(double v, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_sum(v);
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < NTH / 64; ++w) t += sh[w];
+  __syncthreads();  // sh reusable
+  return t;
+}
+template <int NTH>
+__device__ __forceinline__ double block_allmin(double v, double* sh) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_min(v);
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  double t = 1.0;
+  for (int w = 0; w < NTH / 64; ++w) t = fmin(t, sh[w]);
+  __syncthreads();
   return t;
 }
 }  // namespace
@@ -159,6 +183,20 @@ hipError_t qp_init_iterate(const QPBatch& qb, hipStream_t st) {
 // :126-140).  MV selects Q x -> Qx, A x -> Ax, C x -> Cx; one wave per row,
 // 16-byte loads; blockIdx.y = QP of the batch.
 enum { MV_Q = 0, MV_A = 1, MV_C = 2 };
+// one wave: sum_j r[j] x[j] (16-byte loads, two lane partials, DPP sum)
+__device__ __forceinline__ double row_dot(const double* __restrict__ r, const double* __restrict__ x, int cols,
+                                          int lane) {
+  double s0 = 0.0, s1 = 0.0;
+  int j = lane * 2;
+  for (; j + 1 < cols; j += 128) {
+    const double2 a = *reinterpret_cast<const double2*>(r + j);
+    const double2 b = *reinterpret_cast<const double2*>(x + j);
+    s0 += a.x * b.x;
+    s1 += a.y * b.y;
+  }
+  if (j < cols) s0 += r[j] * x[j];
+  return wave_sum(s0 + s1);
+}
 template <int MV>
 __global__ __launch_bounds__(NT) void k_matvec_rows(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
@@ -170,17 +208,7 @@ __global__ __launch_bounds__(NT) void k_matvec_rows(const QPDev* __restrict__ qs
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * (NT / 64) + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const double* r = M + (int64_t)row * q.ldn;
-  double s0 = 0.0, s1 = 0.0;
-  int j = lane * 2;
-  for (; j + 1 < cols; j += 128) {
-    const double2 a = *reinterpret_cast<const double2*>(r + j);
-    const double2 b = *reinterpret_cast<const double2*>(x + j);
-    s0 += a.x * b.x;
-    s1 += a.y * b.y;
-  }
-  if (j < cols) s0 += r[j] * x[j];
-  const double s = wave_sum(s0 + s1);
+  const double s = row_dot(M + (int64_t)row * q.ldn, x, cols, lane);
   if (lane == 0) out[row] = s;
 }
 
@@ -230,111 +258,120 @@ __device__ __forceinline__ int comp_count(const QPDev& q) { return (q.vlo + q.vu
 // Shorthand residuals r_v := -rhs_v at mu (SymbolicOptimization.cpp:480-492),
 // plus per-block partials of ||rhs||^2, sum |complementarity|, and the two
 // objective sums (Optimizer.cpp:128-130).
+// one element t of the residual pass (t < n + m + p).  SC: the matvec
+// results (Qx, A^T lambda_A, ...) were stored write-through by other
+// workgroups of the same launch -- read them with agent-scope loads.
+template <bool SC = false>
+__device__ __forceinline__ void residual_elem(const QPDev& q, int t, double mu, double& res2, double& comp,
+                                              double& fa, double& fb) {
+  const int n = q.n, m = q.m, p = q.p;
+  auto mv = [](const double* a) { return SC ? ld_sc1(a) : *a; };
+  if (t < n) {
+    const int i = t;
+    // r_x := (c [+ lambda_z] + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] [- lambda_y])
+    double s = q.c[i];
+    if (q.vup) s = s + q.v[LZ][i];
+    s = s + mv(&q.Qx[i]);
+    if (m) s = s + mv(&q.ATl[i]);
+    if (p) s = s + mv(&q.CTl[i]);
+    const double rx = q.vlo ? s + (-q.v[LY][i]) : s;
+    q.r[X][i] = rx;
+    res2 += rx * rx;
+    if (q.slacks) {  // (((X - L_x)*lambda_y) - (mu*e_x)), (((U_x - X)*lambda_z) - (mu*e_x))
+      if (q.vlo) {
+        const double r = ((q.v[X][i] + (-q.lx[i])) * q.v[LY][i]) + (-(mu * 1.0));
+        q.r[LY][i] = r;
+        res2 += r * r;
+        comp += fabs(r);
+      }
+      if (q.vup) {
+        const double r = ((q.ux[i] + (-q.v[X][i])) * q.v[LZ][i]) + (-(mu * 1.0));
+        q.r[LZ][i] = r;
+        res2 += r * r;
+        comp += fabs(r);
+      }
+    } else {
+      if (q.vlo) {
+        const double rly = (q.lx[i] + q.v[Y][i]) + (-q.v[X][i]);     // (l_x + y - x)
+        const double ry = q.v[Y][i] * q.v[LY][i] + (-(mu * 1.0));  // ((Y*lambda_y) - (mu*e_x))
+        q.r[LY][i] = rly;
+        q.r[Y][i] = ry;
+        res2 += rly * rly + ry * ry;
+        comp += fabs(ry);
+      }
+      if (q.vup) {
+        const double rlz = (q.v[X][i] + q.v[Z][i]) + (-q.ux[i]);   // (x + z - u_x)
+        const double rz = q.v[Z][i] * q.v[LZ][i] + (-(mu * 1.0));
+        q.r[LZ][i] = rlz;
+        q.r[Z][i] = rz;
+        res2 += rlz * rlz + rz * rz;
+        comp += fabs(rz);
+      }
+    }
+    fa += (0.5 * q.v[X][i]) * mv(&q.Qx[i]);
+    fb += q.c[i] * q.v[X][i];
+  } else if (t < n + m) {
+    const int i = t - n;
+    const double rla = mv(&q.Ax[i]) + (-q.v[S][i]);  // ((A*x) - s)
+    double rs;
+    if (q.alo && q.aup) rs = -((q.v[LA][i] + q.v[LG][i]) + (-q.v[LH][i]));  // -(lambda_A + lambda_g - lambda_h)
+    else if (q.alo) rs = -(q.v[LA][i] + q.v[LG][i]);                        // -(lambda_A + lambda_g)
+    else rs = q.v[LH][i] + (-q.v[LA][i]);                                   // (lambda_h - lambda_A)
+    q.r[LA][i] = rla;
+    q.r[S][i] = rs;
+    res2 += rla * rla + rs * rs;
+    if (q.slacks) {  // (((S - L_A)*lambda_g) - (mu*e_A)), (((U_A - S)*lambda_h) - (mu*e_A))
+      const double rlg = ((q.v[S][i] + (-q.lA[i])) * q.v[LG][i]) + (-(mu * 1.0));
+      const double rlh = ((q.uA[i] + (-q.v[S][i])) * q.v[LH][i]) + (-(mu * 1.0));
+      q.r[LG][i] = rlg;
+      q.r[LH][i] = rlh;
+      res2 += rlg * rlg + rlh * rlh;
+      comp += fabs(rlg) + fabs(rlh);
+    } else {
+      if (q.alo) {
+        const double rlg = (q.lA[i] + q.v[G][i]) + (-q.v[S][i]);  // (l_A + g - s)
+        const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));
+        q.r[LG][i] = rlg;
+        q.r[G][i] = rg;
+        res2 += rlg * rlg + rg * rg;
+        comp += fabs(rg);
+      }
+      if (q.aup) {
+        const double rlh = (q.v[H][i] + q.v[S][i]) + (-q.uA[i]);  // (h + s - u_A)
+        const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
+        q.r[LH][i] = rlh;
+        q.r[H][i] = rh;
+        res2 += rlh * rlh + rh * rh;
+        comp += fabs(rh);
+      }
+    }
+  } else {
+    const int i = t - n - m;
+    if (q.eqnone) {  // ((C*x) - d)
+      const double rlc = mv(&q.Cx[i]) + (-q.d[i]);
+      q.r[LC][i] = rlc;
+      res2 += rlc * rlc;
+    } else if (q.eqpen) {  // -(d + (mu*lambda_C) - (C*x))
+      const double rlc = -((q.d[i] + mu * q.v[LC][i]) + (-mv(&q.Cx[i])));
+      q.r[LC][i] = rlc;
+      res2 += rlc * rlc;
+    } else {  // ((C*x) + (delta*p) - d), (p + (delta*lambda_C))
+      const double rlc = (mv(&q.Cx[i]) + q.delta * q.v[P][i]) + (-q.d[i]);
+      const double rp = q.v[P][i] + q.delta * q.v[LC][i];
+      q.r[LC][i] = rlc;
+      q.r[P][i] = rp;
+      res2 += rlc * rlc + rp * rp;
+    }
+  }
+}
+
 __global__ __launch_bounds__(NT) void k_residuals(const QPDev* __restrict__ qs, double mu, int with_stats) {
   const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   double res2 = 0.0, comp = 0.0, fa = 0.0, fb = 0.0;
-  const int n = q.n, m = q.m, p = q.p;
-  const int total = n + m + p;
-  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
-    if (t < n) {
-      const int i = t;
-      // r_x := (c [+ lambda_z] + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] [- lambda_y])
-      double s = q.c[i];
-      if (q.vup) s = s + q.v[LZ][i];
-      s = s + q.Qx[i];
-      if (m) s = s + q.ATl[i];
-      if (p) s = s + q.CTl[i];
-      const double rx = q.vlo ? s + (-q.v[LY][i]) : s;
-      q.r[X][i] = rx;
-      res2 += rx * rx;
-      if (q.slacks) {  // (((X - L_x)*lambda_y) - (mu*e_x)), (((U_x - X)*lambda_z) - (mu*e_x))
-        if (q.vlo) {
-          const double r = ((q.v[X][i] + (-q.lx[i])) * q.v[LY][i]) + (-(mu * 1.0));
-          q.r[LY][i] = r;
-          res2 += r * r;
-          comp += fabs(r);
-        }
-        if (q.vup) {
-          const double r = ((q.ux[i] + (-q.v[X][i])) * q.v[LZ][i]) + (-(mu * 1.0));
-          q.r[LZ][i] = r;
-          res2 += r * r;
-          comp += fabs(r);
-        }
-      } else {
-        if (q.vlo) {
-          const double rly = (q.lx[i] + q.v[Y][i]) + (-q.v[X][i]);     // (l_x + y - x)
-          const double ry = q.v[Y][i] * q.v[LY][i] + (-(mu * 1.0));  // ((Y*lambda_y) - (mu*e_x))
-          q.r[LY][i] = rly;
-          q.r[Y][i] = ry;
-          res2 += rly * rly + ry * ry;
-          comp += fabs(ry);
-        }
-        if (q.vup) {
-          const double rlz = (q.v[X][i] + q.v[Z][i]) + (-q.ux[i]);   // (x + z - u_x)
-          const double rz = q.v[Z][i] * q.v[LZ][i] + (-(mu * 1.0));
-          q.r[LZ][i] = rlz;
-          q.r[Z][i] = rz;
-          res2 += rlz * rlz + rz * rz;
-          comp += fabs(rz);
-        }
-      }
-      fa += (0.5 * q.v[X][i]) * q.Qx[i];
-      fb += q.c[i] * q.v[X][i];
-    } else if (t < n + m) {
-      const int i = t - n;
-      const double rla = q.Ax[i] + (-q.v[S][i]);  // ((A*x) - s)
-      double rs;
-      if (q.alo && q.aup) rs = -((q.v[LA][i] + q.v[LG][i]) + (-q.v[LH][i]));  // -(lambda_A + lambda_g - lambda_h)
-      else if (q.alo) rs = -(q.v[LA][i] + q.v[LG][i]);                        // -(lambda_A + lambda_g)
-      else rs = q.v[LH][i] + (-q.v[LA][i]);                                   // (lambda_h - lambda_A)
-      q.r[LA][i] = rla;
-      q.r[S][i] = rs;
-      res2 += rla * rla + rs * rs;
-      if (q.slacks) {  // (((S - L_A)*lambda_g) - (mu*e_A)), (((U_A - S)*lambda_h) - (mu*e_A))
-        const double rlg = ((q.v[S][i] + (-q.lA[i])) * q.v[LG][i]) + (-(mu * 1.0));
-        const double rlh = ((q.uA[i] + (-q.v[S][i])) * q.v[LH][i]) + (-(mu * 1.0));
-        q.r[LG][i] = rlg;
-        q.r[LH][i] = rlh;
-        res2 += rlg * rlg + rlh * rlh;
-        comp += fabs(rlg) + fabs(rlh);
-      } else {
-        if (q.alo) {
-          const double rlg = (q.lA[i] + q.v[G][i]) + (-q.v[S][i]);  // (l_A + g - s)
-          const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));
-          q.r[LG][i] = rlg;
-          q.r[G][i] = rg;
-          res2 += rlg * rlg + rg * rg;
-          comp += fabs(rg);
-        }
-        if (q.aup) {
-          const double rlh = (q.v[H][i] + q.v[S][i]) + (-q.uA[i]);  // (h + s - u_A)
-          const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
-          q.r[LH][i] = rlh;
-          q.r[H][i] = rh;
-          res2 += rlh * rlh + rh * rh;
-          comp += fabs(rh);
-        }
-      }
-    } else {
-      const int i = t - n - m;
-      if (q.eqnone) {  // ((C*x) - d)
-        const double rlc = q.Cx[i] + (-q.d[i]);
-        q.r[LC][i] = rlc;
-        res2 += rlc * rlc;
-      } else if (q.eqpen) {  // -(d + (mu*lambda_C) - (C*x))
-        const double rlc = -((q.d[i] + mu * q.v[LC][i]) + (-q.Cx[i]));
-        q.r[LC][i] = rlc;
-        res2 += rlc * rlc;
-      } else {  // ((C*x) + (delta*p) - d), (p + (delta*lambda_C))
-        const double rlc = (q.Cx[i] + q.delta * q.v[P][i]) + (-q.d[i]);
-        const double rp = q.v[P][i] + q.delta * q.v[LC][i];
-        q.r[LC][i] = rlc;
-        q.r[P][i] = rp;
-        res2 += rlc * rlc + rp * rp;
-      }
-    }
-  }
+  const int total = q.n + q.m + q.p;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT)
+    residual_elem(q, t, mu, res2, comp, fa, fb);
   if (!with_stats) return;
   double a = block_sum(res2, sh);
   if (threadIdx.x == 0) q.part[4 * blockIdx.x + 0] = a;
@@ -419,30 +456,33 @@ __device__ __forceinline__ double kkt_aa(const QPDev& q, int i) {
   return -(ipmz_inv(q.v[LH][i]) * q.v[H][i]);             // -(Lambda_h^{-1}*H)
 }
 
-__global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
-  const QPDev& q = qs[blockIdx.y];
+// row i of the lower triangle, columns split over nth threads (tid)
+__device__ __forceinline__ void assemble_row(const QPDev& q, int i, int tid, int nth) {
   double* __restrict__ K = q.K;
   const int64_t ld = q.ldk;
-  const int i = blockIdx.x;
   const int n = q.n, m = q.m;
   double* Kr = K + (int64_t)i * ld;
   if (i < n) {
     const double* Qr = q.Q + (int64_t)i * q.ldn;
-    for (int j = threadIdx.x; j < i; j += NT) Kr[j] = Qr[j];
-    if (threadIdx.x == 0) Kr[i] = kkt_xx(q, i, Qr[i]);
+    for (int j = tid; j < i; j += nth) Kr[j] = Qr[j];
+    if (tid == 0) Kr[i] = kkt_xx(q, i, Qr[i]);
   } else if (i < n + m) {
     const int r = i - n;
     const double* Ar = q.A + (int64_t)r * q.ldn;
-    for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Ar[j];
-    for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
-    if (threadIdx.x == 0) Kr[i] = kkt_aa(q, r);
+    for (int j = tid; j < n; j += nth) Kr[j] = Ar[j];
+    for (int j = n + tid; j < i; j += nth) Kr[j] = 0.0;
+    if (tid == 0) Kr[i] = kkt_aa(q, r);
   } else {
     const int r = i - n - m;
     const double* Cr = q.C + (int64_t)r * q.ldn;
-    for (int j = threadIdx.x; j < n; j += NT) Kr[j] = Cr[j];
-    for (int j = n + threadIdx.x; j < i; j += NT) Kr[j] = 0.0;
-    if (threadIdx.x == 0) Kr[i] = q.eqnone ? 0.0 : q.eqpen ? -q.scal[SC_MU_NEW] : -(q.delta * q.delta);
+    for (int j = tid; j < n; j += nth) Kr[j] = Cr[j];
+    for (int j = n + tid; j < i; j += nth) Kr[j] = 0.0;
+    if (tid == 0) Kr[i] = q.eqnone ? 0.0 : q.eqpen ? -q.scal[SC_MU_NEW] : -(q.delta * q.delta);
   }
+}
+
+__global__ __launch_bounds__(NT) void k_assemble(const QPDev* __restrict__ qs) {
+  assemble_row(qs[blockIdx.y], blockIdx.x, threadIdx.x, NT);
 }
 
 hipError_t qp_assemble(const QPBatch& qb, hipStream_t st) {
@@ -452,9 +492,8 @@ hipError_t qp_assemble(const QPBatch& qb, hipStream_t st) {
 
 // ---------------------------------------------------------------------------
 // Augmented rhs (formulations.txt, augmented system rhs rows 0..2).
-__global__ void k_rhs(const QPDev* __restrict__ qs) {
-  const QPDev& q = qs[blockIdx.y];
-  const int t = blockIdx.x * NT + threadIdx.x;
+// element t (< N) of the augmented rhs
+__device__ __forceinline__ void rhs_elem(const QPDev& q, int t) {
   const int n = q.n, m = q.m;
   if (t < n) {
     const int i = t;
@@ -493,6 +532,8 @@ __global__ void k_rhs(const QPDev* __restrict__ qs) {
   }
 }
 
+__global__ void k_rhs(const QPDev* __restrict__ qs) { rhs_elem(qs[blockIdx.y], blockIdx.x * NT + threadIdx.x); }
+
 hipError_t qp_rhs(const QPBatch& qb, hipStream_t st) {
   hipLaunchKernelGGL(k_rhs, grid2((qb.h.N + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d);
   return hipGetLastError();
@@ -505,10 +546,8 @@ struct DSel {
 };
 __device__ __forceinline__ DSel dsel(const QPDev& q, int which) { return DSel{which ? q.dir : q.daff}; }
 
-__global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
-  const QPDev& q = qs[blockIdx.y];
-  const DSel D = dsel(q, which);
-  const int t = blockIdx.x * NT + threadIdx.x;
+// element t (< N): the solution b -> the Newton directions D
+__device__ __forceinline__ void backsub_elem(const QPDev& q, const DSel& D, int t) {
   const int n = q.n, m = q.m;
   if (t < n) {
     const int i = t;
@@ -577,6 +616,11 @@ __global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
   }
 }
 
+__global__ void k_backsub(const QPDev* __restrict__ qs, int which) {
+  const QPDev& q = qs[blockIdx.y];
+  backsub_elem(q, dsel(q, which), blockIdx.x * NT + threadIdx.x);
+}
+
 hipError_t qp_backsub(const QPBatch& qb, int which, hipStream_t st) {
   hipLaunchKernelGGL(k_backsub, grid2((qb.h.N + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d, which);
   return hipGetLastError();
@@ -587,13 +631,9 @@ hipError_t qp_backsub(const QPBatch& qb, int which, hipStream_t st) {
 // non-negative Newton variables, plus -- when neither g nor h is a Newton
 // variable (box-only SlackedSlacks, or Slacks) -- explicit bounds on x
 // (l_x, u_x) and s (l_A, u_A), both always (the environment holds both).
-__global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs, int which) {
-  const QPDev& q = qs[blockIdx.y];
-  const DSel D = dsel(q, which);
-  __shared__ double sh[NT / 64];
-  double a = 1.0;
+// Element t (< n + m), folded into a.
+__device__ __forceinline__ void ratio_elem(const QPDev& q, const DSel& D, int t, double& a) {
   const int n = q.n, m = q.m;
-  const int total = n + m;
   const bool explicit_bounds = q.slacks || m == 0;
   auto nonneg = [&](int slot, int i) {
     const double d = D.d[slot][i];
@@ -603,27 +643,33 @@ __global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs,
     if (d < 0.0) a = fmin(a, (lo - v) / d);
     if (d > 0.0) a = fmin(a, (up - v) / d);
   };
-  for (int t = blockIdx.x * NT + threadIdx.x; t < total; t += gridDim.x * NT) {
-    if (t < n) {
-      const int i = t;
-      if (q.vlo) nonneg(LY, i);
-      if (q.vup) nonneg(LZ, i);
-      if (!q.slacks) {
-        if (q.vlo) nonneg(Y, i);
-        if (q.vup) nonneg(Z, i);
-      }
-      if (explicit_bounds) bounded(q.v[X][i], D.d[X][i], q.lx[i], q.ux[i]);
-    } else {
-      const int i = t - n;
-      if (q.alo) nonneg(LG, i);
-      if (q.aup) nonneg(LH, i);
-      if (!q.slacks) {
-        if (q.alo) nonneg(G, i);
-        if (q.aup) nonneg(H, i);
-      }
-      if (explicit_bounds) bounded(q.v[S][i], D.d[S][i], q.lA[i], q.uA[i]);
+  if (t < n) {
+    const int i = t;
+    if (q.vlo) nonneg(LY, i);
+    if (q.vup) nonneg(LZ, i);
+    if (!q.slacks) {
+      if (q.vlo) nonneg(Y, i);
+      if (q.vup) nonneg(Z, i);
     }
+    if (explicit_bounds) bounded(q.v[X][i], D.d[X][i], q.lx[i], q.ux[i]);
+  } else {
+    const int i = t - n;
+    if (q.alo) nonneg(LG, i);
+    if (q.aup) nonneg(LH, i);
+    if (!q.slacks) {
+      if (q.alo) nonneg(G, i);
+      if (q.aup) nonneg(H, i);
+    }
+    if (explicit_bounds) bounded(q.v[S][i], D.d[S][i], q.lA[i], q.uA[i]);
   }
+}
+
+__global__ __launch_bounds__(NT) void k_ratio_part(const QPDev* __restrict__ qs, int which) {
+  const QPDev& q = qs[blockIdx.y];
+  const DSel D = dsel(q, which);
+  __shared__ double sh[NT / 64];
+  double a = 1.0;
+  for (int t = blockIdx.x * NT + threadIdx.x; t < q.n + q.m; t += gridDim.x * NT) ratio_elem(q, D, t, a);
   a = block_min(a, sh);
   if (threadIdx.x == 0) q.part[blockIdx.x] = a;
 }
@@ -645,37 +691,49 @@ hipError_t qp_ratio(const QPBatch& qb, int which, int out_index, hipStream_t st)
 
 // mu at the affine trial point v + alpha_aff * daff (Optimizer.cpp:167-180):
 // |complementarity| of every row that carries e and mu, at the trial point.
+__device__ __forceinline__ void mu_aff_elem(const QPDev& q, int t, double al, double& s) {
+  const int n = q.n;
+  auto tv = [&](int slot, int i) { return q.v[slot][i] + al * q.daff[slot][i]; };
+  auto term = [&](double a, double b) { return fabs(-(a * b + (-(0.0 * 1.0)))); };
+  if (t < n) {
+    const int i = t;
+    if (q.slacks) {
+      if (q.vlo) s += term(tv(X, i) + (-q.lx[i]), tv(LY, i));  // ((X - L_x)*lambda_y)
+      if (q.vup) s += term(q.ux[i] + (-tv(X, i)), tv(LZ, i));  // ((U_x - X)*lambda_z)
+    } else {
+      if (q.vlo) s += term(tv(Y, i), tv(LY, i));
+      if (q.vup) s += term(tv(Z, i), tv(LZ, i));
+    }
+  } else {
+    const int i = t - n;
+    if (q.slacks) {
+      s += term(tv(S, i) + (-q.lA[i]), tv(LG, i));  // ((S - L_A)*lambda_g)
+      s += term(q.uA[i] + (-tv(S, i)), tv(LH, i));  // ((U_A - S)*lambda_h)
+    } else {
+      if (q.alo) s += term(tv(G, i), tv(LG, i));
+      if (q.aup) s += term(tv(H, i), tv(LH, i));
+    }
+  }
+}
 __global__ __launch_bounds__(NT) void k_mu_aff_part(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[NT / 64];
   const double al = q.scal[SC_ALPHA_AFF];
   double s = 0.0;
-  const int n = q.n, m = q.m;
-  auto tv = [&](int slot, int i) { return q.v[slot][i] + al * q.daff[slot][i]; };
-  auto term = [&](double a, double b) { return fabs(-(a * b + (-(0.0 * 1.0)))); };
-  for (int t = blockIdx.x * NT + threadIdx.x; t < n + m; t += gridDim.x * NT) {
-    if (t < n) {
-      const int i = t;
-      if (q.slacks) {
-        if (q.vlo) s += term(tv(X, i) + (-q.lx[i]), tv(LY, i));  // ((X - L_x)*lambda_y)
-        if (q.vup) s += term(q.ux[i] + (-tv(X, i)), tv(LZ, i));  // ((U_x - X)*lambda_z)
-      } else {
-        if (q.vlo) s += term(tv(Y, i), tv(LY, i));
-        if (q.vup) s += term(tv(Z, i), tv(LZ, i));
-      }
-    } else {
-      const int i = t - n;
-      if (q.slacks) {
-        s += term(tv(S, i) + (-q.lA[i]), tv(LG, i));  // ((S - L_A)*lambda_g)
-        s += term(q.uA[i] + (-tv(S, i)), tv(LH, i));  // ((U_A - S)*lambda_h)
-      } else {
-        if (q.alo) s += term(tv(G, i), tv(LG, i));
-        if (q.aup) s += term(tv(H, i), tv(LH, i));
-      }
-    }
-  }
+  for (int t = blockIdx.x * NT + threadIdx.x; t < q.n + q.m; t += gridDim.x * NT) mu_aff_elem(q, t, al, s);
   s = block_sum(s, sh);
   if (threadIdx.x == 0) q.part[blockIdx.x] = s;
+}
+// mu_aff, sigma = (mu_aff / mu)^3, mu_new = mu sigma (Optimizer.cpp:167-182)
+__device__ __forceinline__ double mu_aff_store(const QPDev& q, double s) {
+  const int cnt = comp_count(q);
+  const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
+  const double mu = q.scal[SC_MU];
+  const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
+  q.scal[SC_MU_AFF] = mu_aff;
+  q.scal[SC_SIGMA] = sigma;
+  q.scal[SC_MU_NEW] = mu * sigma;
+  return mu * sigma;
 }
 __global__ void k_mu_aff_final(const QPDev* __restrict__ qs, int nblocks) {
   const QPDev& q = qs[blockIdx.y];
@@ -683,15 +741,7 @@ __global__ void k_mu_aff_final(const QPDev* __restrict__ qs, int nblocks) {
   double s = 0.0;
   for (int b = threadIdx.x; b < nblocks; b += NT) s += q.part[b];
   s = block_sum(s, sh);
-  if (threadIdx.x == 0) {
-    const int cnt = comp_count(q);
-    const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
-    const double mu = q.scal[SC_MU];
-    const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
-    q.scal[SC_MU_AFF] = mu_aff;
-    q.scal[SC_SIGMA] = sigma;
-    q.scal[SC_MU_NEW] = mu * sigma;
-  }
+  if (threadIdx.x == 0) mu_aff_store(q, s);
 }
 
 hipError_t qp_mu_aff(const QPBatch& qb, hipStream_t st) {
@@ -707,10 +757,7 @@ hipError_t qp_mu_aff(const QPBatch& qb, hipStream_t st) {
 // dlambda_y_aff - 0 e); Slacks r_lambda_y = ((X - L_x) lambda_y - mu_new e) +
 // ((dX_aff - L_x) dlambda_y_aff - 0 e) -- the bound constant leaks into the
 // correction (the reference's Slacks defect, SURVEY.md App. C.1, reproduced).
-__global__ void k_corrector(const QPDev* __restrict__ qs) {
-  const QPDev& q = qs[blockIdx.y];
-  const int t = blockIdx.x * NT + threadIdx.x;
-  const double mu = q.scal[SC_MU_NEW];
+__device__ __forceinline__ void corrector_elem(const QPDev& q, int t, double mu) {
   const int n = q.n, m = q.m;
   const double* const* v = q.v;
   const double* const* da = q.daff;
@@ -747,6 +794,10 @@ __global__ void k_corrector(const QPDev* __restrict__ qs) {
     if (q.eqpen && i < q.p) q.r[LC][i] = -((q.d[i] + mu * v[LC][i]) + (-q.Cx[i]));
   }
 }
+__global__ void k_corrector(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  corrector_elem(q, blockIdx.x * NT + threadIdx.x, q.scal[SC_MU_NEW]);
+}
 
 hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st) {
   const int rows = qb.h.n + qb.h.m + (qb.h.eqpen ? qb.h.p : 0);
@@ -757,11 +808,7 @@ hipError_t qp_corrector_residuals(const QPBatch& qb, hipStream_t st) {
 // update_variables_(0.995 * alpha, ...) (Optimizer.cpp:216-231)
 // freeze != 0: a converged QP of a batch keeps its iterate (the reference
 // stops iterating it, Optimizer.cpp:133-135).
-__global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
-  const QPDev& q = qs[blockIdx.y];
-  if (freeze && q.scal[SC_CONVERGED] != 0.0) return;
-  const int t = blockIdx.x * NT + threadIdx.x;
-  const double s = 0.995 * q.scal[SC_ALPHA];
+__device__ __forceinline__ void update_elem(const QPDev& q, int t, double s) {
   const int n = q.n, m = q.m, p = q.p;
   auto up = [&](int slot, int i) { q.v[slot][i] = q.v[slot][i] + s * q.dir[slot][i]; };
   if (t < n) {
@@ -783,6 +830,11 @@ __global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
     up(LC, t);
     if (!q.eqnone && !q.eqpen) up(P, t);
   }
+}
+__global__ void k_update(const QPDev* __restrict__ qs, int freeze) {
+  const QPDev& q = qs[blockIdx.y];
+  if (freeze && q.scal[SC_CONVERGED] != 0.0) return;
+  update_elem(q, blockIdx.x * NT + threadIdx.x, 0.995 * q.scal[SC_ALPHA]);
 }
 
 hipError_t qp_update(const QPBatch& qb, int freeze, hipStream_t st) {
@@ -861,6 +913,242 @@ __global__ void k_save_initial(const QPDev* __restrict__ qs) {
 hipError_t qp_save_initial(const QPBatch& qb, hipStream_t st) {
   const int64_t g = (qb.h.state_len + NT - 1) / NT;
   hipLaunchKernelGGL(k_save_initial, grid2(g < 256 ? g : 256, qb.B), dim3(NT), 0, st, qb.d);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Fused per-QP step phases for batches of small systems (config C4): ONE
+// workgroup per QP runs every O(N) / O(n^2) phase between the factor and the
+// solves, so a Newton step is six launches (pre, factor, solve, mid, solve,
+// post) instead of ~25 -- at 128 QPs per GPU the short grid kernels above
+// were ~5 us each, a quarter of the step.  The element formulas are the
+// same device functions as the grid kernels (bitwise the same values); only
+// the reductions (res, comp, f, mu_aff) sum in a different order.
+constexpr int FT = 512;  // 8 waves
+
+// restart-if-converged, KKT assembly, affine rhs.  gridDim.x workgroups per
+// QP (blockIdx.y): the off-diagonal copy (independent of the iterate) is
+// split over all of them; workgroup 0 also restarts, writes the diagonal and
+// the rhs (which read the iterate) in that order.
+__global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, int restart, int* info) {
+  const QPDev& q = qs[blockIdx.y];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool lead = blockIdx.x == 0;
+  if (info && lead && blockIdx.y == 0 && tid == 0) *info = 0x7f7f7f7f;  // the factor's first-failure word
+  if (lead && restart && q.scal[SC_CONVERGED] != 0.0) {
+    for (int64_t t = tid; t < q.state_len; t += FT) {
+      q.v[0][t] = q.v0[t];
+      q.r[0][t] = q.r0[t];
+    }
+    __syncthreads();  // every thread has read SC_CONVERGED
+    if (tid == 0) {
+      const double restarts = q.scal[SC_RESTARTS];
+      for (int k = 0; k < SC_RESTARTS; ++k) q.scal[k] = q.scal0[k];
+      q.scal[SC_RESTARTS] = restarts + 1.0;
+    }
+    __syncthreads();  // v, r and mu_new restored before assembly reads them
+  }
+  // strict lower triangle in 128-column units (a wave per unit, a column
+  // pair per lane), eight units per wave in flight: one workgroup moves the
+  // QP's ~0.8 MB only with many loads outstanding
+  const int N = q.N, n = q.n, nm = q.n + q.m;
+  const int nch = (N + 127) / 128, units = N * nch;
+  for (int u0 = (blockIdx.x * (FT / 64) + wave) * 8; u0 < units; u0 += gridDim.x * (FT / 64) * 8) {
+    double v0[8], v1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int u = u0 + k, i = u / nch, j = (u % nch) * 128 + 2 * lane;
+      v0[k] = v1[k] = 0.0;
+      if (u < units) {
+        const double* src = i < n ? q.Q + (int64_t)i * q.ldn
+                           : i < nm ? q.A + (int64_t)(i - n) * q.ldn : q.C + (int64_t)(i - nm) * q.ldn;
+        const int lim = i < n ? i : n;  // source columns [0, lim); zeros in [n, i)
+        if (j < lim) v0[k] = src[j];
+        if (j + 1 < lim) v1[k] = src[j + 1];
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      const int u = u0 + k, i = u / nch, j = (u % nch) * 128 + 2 * lane;
+      if (u < units) {
+        double* Kr = q.K + (int64_t)i * q.ldk;
+        if (j < i) Kr[j] = v0[k];
+        if (j + 1 < i) Kr[j + 1] = v1[k];
+      }
+    }
+  }
+  if (!lead) return;
+  for (int i = tid; i < N; i += FT) {
+    double* Kd = q.K + (int64_t)i * q.ldk + i;
+    if (i < n) *Kd = kkt_xx(q, i, q.Q[(int64_t)i * q.ldn + i]);
+    else if (i < nm) *Kd = kkt_aa(q, i - n);
+    else *Kd = q.eqnone ? 0.0 : q.eqpen ? -q.scal[SC_MU_NEW] : -(q.delta * q.delta);
+  }
+  for (int t = tid; t < N; t += FT) rhs_elem(q, t);
+}
+
+// predictor back-substitution, alpha_aff, mu_aff / sigma, corrector rows,
+// corrector rhs
+__global__ __launch_bounds__(FT) void k_fused_mid(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.x];
+  __shared__ double sh[FT / 64];
+  const int tid = threadIdx.x;
+  const int N = q.N, nm = q.n + q.m;
+  const DSel D = dsel(q, 0);
+  for (int t = tid; t < N; t += FT) backsub_elem(q, D, t);
+  __syncthreads();
+  double a = 1.0;
+  for (int t = tid; t < nm; t += FT) ratio_elem(q, D, t, a);
+  a = block_allmin<FT>(a, sh);
+  if (tid == 0) q.scal[SC_ALPHA_AFF] = a;
+  double s = 0.0;
+  for (int t = tid; t < nm; t += FT) mu_aff_elem(q, t, a, s);
+  s = block_allsum<FT>(s, sh);
+  // every thread evaluates the same scalars; thread 0 stores them
+  const int cnt = comp_count(q);
+  const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
+  const double mu = q.scal[SC_MU];
+  const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
+  const double mu_new = mu * sigma;
+  const int rows = nm + (q.eqpen ? q.p : 0);
+  for (int t = tid; t < rows; t += FT) corrector_elem(q, t, mu_new);
+  __syncthreads();  // SC_MU read by every thread; corrector rows written
+  if (tid == 0) {
+    q.scal[SC_MU_AFF] = mu_aff;
+    q.scal[SC_SIGMA] = sigma;
+    q.scal[SC_MU_NEW] = mu_new;
+  }
+  for (int t = tid; t < N; t += FT) rhs_elem(q, t);
+}
+
+// corrector back-substitution, alpha, the update (one workgroup per QP)
+__global__ __launch_bounds__(FT) void k_fused_post(const QPDev* __restrict__ qs, int freeze) {
+  const QPDev& q = qs[blockIdx.x];
+  __shared__ double sh[FT / 64];
+  const int tid = threadIdx.x;
+  const int n = q.n, m = q.m, p = q.p, N = q.N;
+  const DSel D = dsel(q, 1);
+  const bool frozen = freeze && q.scal[SC_CONVERGED] != 0.0;
+  for (int t = tid; t < N; t += FT) backsub_elem(q, D, t);
+  __syncthreads();
+  double a = 1.0;
+  for (int t = tid; t < n + m; t += FT) ratio_elem(q, D, t, a);
+  a = block_allmin<FT>(a, sh);
+  if (tid == 0) q.scal[SC_ALPHA] = a;
+  if (!frozen) {
+    const int mx = max(n, max(m, p));
+    for (int t = tid; t < mx; t += FT) update_elem(q, t, 0.995 * a);
+  }
+}
+
+// Evaluation of the new iterate (Qx, Ax, Cx, A^T lambda_A, C^T lambda_C,
+// then residuals, f, res, mu): gridDim.x workgroups per QP (blockIdx.y)
+// share the matvec rows and transpose columns; the last to arrive (counter
+// q.done, reset by it) runs the residual pass and the stats.
+__global__ __launch_bounds__(FT) void k_fused_eval(const QPDev* __restrict__ qs) {
+  const QPDev& q = qs[blockIdx.y];
+  __shared__ double sh[FT / 64];
+  __shared__ unsigned last;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int n = q.n, m = q.m, p = q.p, N = q.N;
+  const int gw = blockIdx.x * (FT / 64) + wave, nw = gridDim.x * (FT / 64);
+  const double* x = q.v[X];
+  const int nr = n + m + p;
+  auto row_ptr = [&](int r) {
+    return r < n ? q.Q + (int64_t)r * q.ldn
+                 : r < n + m ? q.A + (int64_t)(r - n) * q.ldn : q.C + (int64_t)(r - n - m) * q.ldn;
+  };
+  // four rows per wave at a time (their loads interleaved); each row's sum
+  // in row_dot's order
+  for (int r0 = gw * 4; r0 < nr; r0 += nw * 4) {
+    double s0[4], s1[4];
+    const double* rp[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      s0[k] = s1[k] = 0.0;
+      rp[k] = row_ptr(r0 + k < nr ? r0 + k : r0);
+    }
+    int j = lane * 2;
+    for (; j + 1 < n; j += 128) {
+      const double2 b = *reinterpret_cast<const double2*>(x + j);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const double2 a = *reinterpret_cast<const double2*>(rp[k] + j);
+        s0[k] += a.x * b.x;
+        s1[k] += a.y * b.y;
+      }
+    }
+    if (j < n) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s0[k] += rp[k][j] * x[j];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const double d = wave_sum(s0[k] + s1[k]);
+      const int r = r0 + k;
+      if (lane == 0 && r < nr) st_sc1(r < n ? &q.Qx[r] : r < n + m ? &q.Ax[r - n] : &q.Cx[r - n - m], d);
+    }
+  }
+  // transposes: thread per column, rows in TCHUNK chunks (the grid order)
+  auto col_sum = [&](const double* M, const double* y, int rows, int j) {
+    double tot = 0.0;
+    for (int i0 = 0; i0 < rows; i0 += TCHUNK) {
+      const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
+      double c = 0.0;
+#pragma unroll 8
+      for (int i = i0; i < i1; ++i) c += M[(int64_t)i * q.ldn + j] * y[i];
+      tot += c;
+    }
+    return tot;
+  };
+  for (int j = blockIdx.x * FT + tid; j < n; j += gridDim.x * FT) {
+    if (m) st_sc1(&q.ATl[j], col_sum(q.A, q.v[LA], m, j));
+    if (p) st_sc1(&q.CTl[j], col_sum(q.C, q.v[LC], p, j));
+  }
+  // arrival (sync.h protocol: write-through data, vmcnt drained, barrier, one
+  // agent-scope atomic); no cache-wide fences
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0)
+    last = __hip_atomic_fetch_add(q.done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1u : 0u;
+  __syncthreads();
+  if (!last) return;
+  if (tid == 0) st_sc1(q.done, 0u);
+  double res2 = 0.0, comp = 0.0, fa = 0.0, fb = 0.0;
+  for (int t = tid; t < N; t += FT) residual_elem<true>(q, t, 0.0, res2, comp, fa, fb);
+  res2 = block_allsum<FT>(res2, sh);
+  comp = block_allsum<FT>(comp, sh);
+  fa = block_allsum<FT>(fa, sh);
+  fb = block_allsum<FT>(fb, sh);
+  if (tid == 0) {
+    const double res = sqrt(res2);
+    const int cnt = comp_count(q);
+    const double mu = cnt == 0 ? 0.0 : comp / (double)cnt;
+    q.scal[SC_F] = fa + fb;
+    q.scal[SC_RES] = res;
+    q.scal[SC_MU] = mu;
+    q.scal[SC_CONVERGED] = (res < 1e-8 && mu < 1e-8) ? 1.0 : 0.0;  // Optimizer.cpp:124,133
+  }
+}
+
+// about two workgroups per CU: a lone workgroup per QP cannot keep enough
+// loads in flight
+static int fused_split(int B) {
+  const int s = (2 * device_cus() + B - 1) / B;
+  return s < 1 ? 1 : (s > 8 ? 8 : s);
+}
+
+hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st) {
+  hipLaunchKernelGGL(k_fused_pre, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d, restart, info);
+  return hipGetLastError();
+}
+hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st) {
+  hipLaunchKernelGGL(k_fused_mid, dim3(qb.B), dim3(FT), 0, st, qb.d);
+  return hipGetLastError();
+}
+hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st) {
+  hipLaunchKernelGGL(k_fused_post, dim3(qb.B), dim3(FT), 0, st, qb.d, freeze);
+  hipLaunchKernelGGL(k_fused_eval, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d);
   return hipGetLastError();
 }
 

@@ -26,26 +26,32 @@ namespace {
 typedef Mfma<double> MF;
 typedef MF::acc_t acc_t;
 
-constexpr int SNW = 8;          // waves per workgroup: two per SIMD
-constexpr int SNT = 64 * SNW;   // threads
-constexpr int SFR = 64 / SNW;   // tile rows fetched per thread
-constexpr int SNN = 4 * 4 / SNW;  // 16-column MFMA blocks per wave (rows: 16 (w & 3)..)
+// SNW waves per workgroup (8: two per SIMD)
+template <int SNW>
+struct Cfg {
+  static constexpr int SNT = 64 * SNW;        // threads
+  static constexpr int SFR = 64 / SNW;        // tile rows fetched per thread
+  static constexpr int SNN = 4 * 4 / SNW;     // 16-column MFMA blocks per wave (rows: 16 (w & 3)..)
+};
 
 // 64 x 64 tile rows [0, nrows) of a row-major source (row stride lds): wave w
 // loads rows w, w+SNW, ... (one 512-byte row per load instruction); rows
 // past nrows read row 0 and are zeroed on the LDS store.
-__device__ __forceinline__ void tile_fetch(const double* __restrict__ src, int64_t lds, int nrows, double (&v)[SFR]) {
+template <int SNW>
+__device__ __forceinline__ void tile_fetch(const double* __restrict__ src, int64_t lds, int nrows,
+                                           double (&v)[Cfg<SNW>::SFR]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < SFR; ++i) {
+  for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
     const int rr = wave + SNW * i;
     v[i] = src[(int64_t)(rr < nrows ? rr : 0) * lds + lane];
   }
 }
-__device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&v)[SFR]) {
+template <int SNW>
+__device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&v)[Cfg<SNW>::SFR]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
-  for (int i = 0; i < SFR; ++i) {
+  for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
     const int rr = wave + SNW * i;
     dst[rr * DS + lane] = rr < nrows ? v[i] : 0.0;
   }
@@ -53,26 +59,29 @@ __device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&
 // this wave's part of the 64 x 64 result: rows 16 (w & 3) .. +15, column
 // blocks n0 + (0 .. SNN-1), n0 = SNN (w >> 2)
 __device__ __forceinline__ int tile_r0() { return 16 * ((threadIdx.x >> 6) & 3); }
-__device__ __forceinline__ int tile_n0() { return SNN * (threadIdx.x >> 8); }
+template <int SNW>
+__device__ __forceinline__ int tile_n0() { return Cfg<SNW>::SNN * (threadIdx.x >> 8); }
 // acc[n] (+)= sgn * As[rows, :] Bs[16 (n0 + n).., :]^T
-template <bool NEG>
-__device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[SNN]) {
+template <int SNW, bool NEG>
+__device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[Cfg<SNW>::SNN]) {
   const int lane = threadIdx.x & 63;
-  const int arow = tile_r0() + (lane & 15), n0 = tile_n0();
+  const int arow = tile_r0() + (lane & 15), n0 = tile_n0<SNW>();
 #pragma unroll 4
   for (int s = 0; s < 16; ++s) {
     const int k = 4 * s + (lane >> 4);
     const double a = NEG ? -As[arow * DS + k] : As[arow * DS + k];
 #pragma unroll
-    for (int n = 0; n < SNN; ++n) acc[n] = MF::mma(a, Bs[(16 * (n0 + n) + (lane & 15)) * DS + k], acc[n]);
+    for (int n = 0; n < Cfg<SNW>::SNN; ++n) acc[n] = MF::mma(a, Bs[(16 * (n0 + n) + (lane & 15)) * DS + k], acc[n]);
   }
 }
 }  // namespace
 
-__global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
+template <int SNW>
+__global__ __launch_bounds__(64 * SNW) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
                                                          double* __restrict__ D, double* __restrict__ Linv,
                                                          double* __restrict__ W, int* __restrict__ info, int64_t sK,
                                                          int64_t sD, int64_t sL, int64_t sW) {
+  constexpr int SFR = Cfg<SNW>::SFR, SNN = Cfg<SNW>::SNN;
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   const int64_t qp = blockIdx.x;
   K += qp * sK;
@@ -80,7 +89,7 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
   Linv += qp * sL;
   W += qp * sW;  // N x 64 row-major: the current block column's W = L D
   const int lane = threadIdx.x & 63;
-  const int r0 = tile_r0(), n0 = tile_n0();
+  const int r0 = tile_r0(), n0 = tile_n0<SNW>();
   double* As = smem;
   double* Bs = smem + 64 * DS;
   const int nblk = (N + 63) / 64;
@@ -93,21 +102,21 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
     __syncthreads();  // diag64_body's LDS is free; its L, D, L^{-1} stores are visible to the workgroup
     // ---- TRSM of the chunks below (block J is full: J0 + 64 < N)
     double v[SFR], u[SFR];
-    tile_fetch(Linv + (int64_t)J * 64 * 64, 64, 64, u);
-    tile_fetch(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    tile_fetch<SNW>(Linv + (int64_t)J * 64 * 64, 64, 64, u);
+    tile_fetch<SNW>(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
     double rd[SNN];
 #pragma unroll
     for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / D[J0 + 16 * (n0 + n) + (lane & 15)];
-    tile_put(Bs, 64, u);
+    tile_put<SNW>(Bs, 64, u);
     for (int c = J + 1; c < nblk; ++c) {
       const int rows = nrows(c);
-      tile_put(As, rows, v);
+      tile_put<SNW>(As, rows, v);
       __syncthreads();
-      if (c + 1 < nblk) tile_fetch(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
+      if (c + 1 < nblk) tile_fetch<SNW>(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
       acc_t acc[SNN];
 #pragma unroll
       for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
-      tile_mma<false>(As, Bs, acc);
+      tile_mma<SNW, false>(As, Bs, acc);
 #pragma unroll
       for (int n = 0; n < SNN; ++n) {
         const int col = 16 * (n0 + n) + (lane & 15);
@@ -126,12 +135,12 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
     // in row order (the next diagonal block first); L[c, J] staged once per
     // row of tiles
     int c = J + 1, q = J + 1;
-    tile_fetch(K + (int64_t)(64 * c) * ld + J0, ld, nrows(c), v);  // L[c, J]
-    tile_fetch(W + (int64_t)(64 * q) * 64, 64, nrows(q), u);       // W_q
+    tile_fetch<SNW>(K + (int64_t)(64 * c) * ld + J0, ld, nrows(c), v);  // L[c, J]
+    tile_fetch<SNW>(W + (int64_t)(64 * q) * 64, 64, nrows(q), u);       // W_q
     for (;;) {
       const int rows = nrows(c);
-      if (q == J + 1) tile_put(As, rows, v);
-      tile_put(Bs, nrows(q), u);
+      if (q == J + 1) tile_put<SNW>(As, rows, v);
+      tile_put<SNW>(Bs, nrows(q), u);
       // the target tile C: its loads stay in flight through the MFMA chain,
       // which accumulates -L W^T from zero; C is added at the end
       acc_t acc[SNN], cv[SNN];
@@ -160,10 +169,10 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
       }
       const bool more = cn < nblk;
       if (more) {
-        if (qn == J + 1) tile_fetch(K + (int64_t)(64 * cn) * ld + J0, ld, nrows(cn), v);
-        tile_fetch(W + (int64_t)(64 * qn) * 64, 64, nrows(qn), u);
+        if (qn == J + 1) tile_fetch<SNW>(K + (int64_t)(64 * cn) * ld + J0, ld, nrows(cn), v);
+        tile_fetch<SNW>(W + (int64_t)(64 * qn) * 64, 64, nrows(qn), u);
       }
-      tile_mma<true>(As, Bs, acc);
+      tile_mma<SNW, true>(As, Bs, acc);
 #pragma unroll
       for (int n = 0; n < SNN; ++n) {
         const int col = 16 * (n0 + n) + (lane & 15);
@@ -184,8 +193,10 @@ __global__ __launch_bounds__(SNT) void ldlt_small_kernel(double* __restrict__ K,
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs) {
   if (N <= 0 || bs.B <= 0) return hipSuccess;
-  hipLaunchKernelGGL(ldlt_small_kernel, dim3(bs.B), dim3(SNT), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD, bs.sL,
-                     bs.sW);
+  // 8 waves (two per SIMD) also when the batch leaves a CU per QP: 16 waves
+  // measured slower (N = 320, B = 128: 249 vs 190 us)
+  hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
+                     bs.sL, bs.sW);
   return hipGetLastError();
 }
 

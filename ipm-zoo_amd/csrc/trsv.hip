@@ -426,10 +426,16 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
                               double* b, int B, int64_t sK, int64_t sD, int64_t sL, int64_t sb, hipStream_t st) {
   if (N <= 0 || B <= 0) return hipSuccess;
   if (nbi == 64 && N <= TRSV_SMALL_NMAX) {
-    constexpr int NW = 8;
+    // 16 waves when the batch leaves a CU per QP, 8 when QPs share CUs
+    const bool wide = B <= device_cus();
+    const int NW = wide ? 16 : 8;
     const size_t lds = (2 * (size_t)((N + 63) & ~63) + NW * 64 + 64) * sizeof(double);
-    hipLaunchKernelGGL((trsv_small_kernel<NW>), dim3(B), dim3(64 * NW), lds, st, K, ld, N, D, Linv, b, sK, sD, sL,
-                       sb);
+    if (wide)
+      hipLaunchKernelGGL((trsv_small_kernel<16>), dim3(B), dim3(64 * 16), lds, st, K, ld, N, D, Linv, b, sK, sD, sL,
+                         sb);
+    else
+      hipLaunchKernelGGL((trsv_small_kernel<8>), dim3(B), dim3(64 * 8), lds, st, K, ld, N, D, Linv, b, sK, sD, sL,
+                         sb);
   } else if (nbi == 64)
     hipLaunchKernelGGL((trsv_batched_kernel<64>), dim3(B), dim3(TRSV_NT), 0, st, K, ld, N, D, Linv, b, sK, sD, sL, sb);
   else if (nbi == 128)
