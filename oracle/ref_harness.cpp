@@ -145,6 +145,8 @@ static SO::Settings settings_from(const std::string& ineq, const std::string& eq
   else if (eq == "PenaltyFunction") s.equality_handling = SO::EqualityHandling::PenaltyFunction;
   else if (eq == "SlackedSlacks") s.equality_handling = SO::EqualityHandling::SlackedSlacks;
   else if (eq == "Slacks") s.equality_handling = SO::EqualityHandling::Slacks;
+  else if (eq == "NaiveSlacks") s.equality_handling = SO::EqualityHandling::NaiveSlacks;
+  else if (eq == "PenaltyFunctionWithExtraDual") s.equality_handling = SO::EqualityHandling::PenaltyFunctionWithExtraDual;
   return s;
 }
 
@@ -172,8 +174,8 @@ static SO::Bounds bounds_from(const std::string& b) {
 
 // one Settings' formulation to stdout (exploration; fixtures use mode_formulation)
 static int mode_formulation_one(const std::string& ineq, const std::string& ineq_bounds,
-                                const std::string& var_bounds) {
-  SO::Settings s = settings_from(ineq, "none", ineq_bounds != "None");
+                                const std::string& var_bounds, const std::string& eq = "none") {
+  SO::Settings s = settings_from(ineq, eq, ineq_bounds != "None");
   s.inequalities = bounds_from(ineq_bounds);
   s.variable_bounds = bounds_from(var_bounds);
   const SO::VariableNames names;
@@ -548,6 +550,7 @@ int main(int argc, char** argv) {
   try {
     if (mode == "formulation") return mode_formulation(dir);
     if (mode == "formulation_one" && argc == 5) return mode_formulation_one(argv[2], argv[3], argv[4]);
+    if (mode == "formulation_one" && argc == 6) return mode_formulation_one(argv[2], argv[3], argv[4], argv[5]);
     if (mode == "ldlt" && argc == 6) return mode_ldlt(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk" && argc == 6) return mode_bk(dir, std::stoul(argv[3]), std::stoull(argv[4]), argv[5]);
     if (mode == "bk_zeros_at" && argc == 7)
