@@ -61,8 +61,10 @@ __device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&
 __device__ __forceinline__ int tile_r0() { return 16 * ((threadIdx.x >> 6) & 3); }
 template <int SNW>
 __device__ __forceinline__ int tile_n0() { return Cfg<SNW>::SNN * (threadIdx.x >> 8); }
-// acc[n] (+)= sgn * As[rows, :] Bs[16 (n0 + n).., :]^T
-template <int SNW, bool NEG>
+// acc[n] (+)= sgn * As[rows, :] Bs[16 (n0 + n).., :]^T.  LOWER: Bs is
+// lower triangular and only its lower part is meaningful (the diagonal
+// factor's L^{-1} image, left in LDS): entries k > row read as 0.
+template <int SNW, bool NEG, bool LOWER = false>
 __device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[Cfg<SNW>::SNN]) {
   const int lane = threadIdx.x & 63;
   const int arow = tile_r0() + (lane & 15), n0 = tile_n0<SNW>();
@@ -71,7 +73,11 @@ __device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc
     const int k = 4 * s + (lane >> 4);
     const double a = NEG ? -As[arow * DS + k] : As[arow * DS + k];
 #pragma unroll
-    for (int n = 0; n < Cfg<SNW>::SNN; ++n) acc[n] = MF::mma(a, Bs[(16 * (n0 + n) + (lane & 15)) * DS + k], acc[n]);
+    for (int n = 0; n < Cfg<SNW>::SNN; ++n) {
+      const int brow = 16 * (n0 + n) + (lane & 15);
+      const double b = Bs[brow * DS + k];
+      acc[n] = MF::mma(a, LOWER ? (k <= brow ? b : 0.0) : b, acc[n]);
+    }
   }
 }
 }  // namespace
@@ -99,15 +105,16 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_kernel(double* __restrict
     diag64_body<false, false, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
                                                   smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
     if (J == nblk - 1) break;
-    __syncthreads();  // diag64_body's LDS is free; its L, D, L^{-1} stores are visible to the workgroup
-    // ---- TRSM of the chunks below (block J is full: J0 + 64 < N)
+    __syncthreads();  // diag64_body's L, D, L^{-1} stores are visible to the workgroup
+    // ---- TRSM of the chunks below (block J is full: J0 + 64 < N), with
+    // L_JJ^{-1} and the pivots straight from diag64_body's LDS images (X in
+    // Bs, lower part; dsh) -- no global round trip on the chain
     double v[SFR], u[SFR];
-    tile_fetch<SNW>(Linv + (int64_t)J * 64 * 64, 64, 64, u);
     tile_fetch<SNW>(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    const double* dsh = smem + 2 * 64 * DS;
     double rd[SNN];
 #pragma unroll
-    for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / D[J0 + 16 * (n0 + n) + (lane & 15)];
-    tile_put<SNW>(Bs, 64, u);
+    for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / dsh[16 * (n0 + n) + (lane & 15)];
     for (int c = J + 1; c < nblk; ++c) {
       const int rows = nrows(c);
       tile_put<SNW>(As, rows, v);
@@ -116,7 +123,7 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_kernel(double* __restrict
       acc_t acc[SNN];
 #pragma unroll
       for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
-      tile_mma<SNW, false>(As, Bs, acc);
+      tile_mma<SNW, false, true>(As, Bs, acc);
 #pragma unroll
       for (int n = 0; n < SNN; ++n) {
         const int col = 16 * (n0 + n) + (lane & 15);
