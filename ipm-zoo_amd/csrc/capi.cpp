@@ -430,10 +430,15 @@ static int normal_factor_impl(ipmz_ctx* ctx, int n, int mp, double* K, int64_t l
   if (mp == 0) return IPMZ_OK;
   // Vt = B L^{-T}, S = E + Vt D^{-1} Vt^T (into the (2,2) block), Cholesky of S
   const WsLayout lh = ws_layout(n, nbo_for(ctx, n), ctx->nbi);
+  // the TRSM steps over 128-column blocks with the solve prep's X_J = L_JJ^{-1}
+  // (built by factor_impl for nbi = 64: half the sequential steps of the
+  // factor's 64 x 64 inverses), else over the factor's own nbi blocks
   const double* LinvH = reinterpret_cast<const double*>(w.wsH + lh.linv_off);
+  const double* XH = reinterpret_cast<const double*>(w.wsH + lh.prep_off);
   HIP_OK(hipMemcpy2DAsync(w.Vt, w.ldv * 8, K + (int64_t)n * ld, ld * 8, (size_t)n * 8, mp, hipMemcpyDeviceToDevice,
                           st));
-  HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, LinvH, ctx->nbi, st));
+  if (ctx->nbi == 64) HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, XH, IPMZ_SOLVE_BLOCK, st));
+  else HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, LinvH, ctx->nbi, st));
   double* K22 = K + (int64_t)n * ld + n;
   HIP_OK(ne_schur(K22, ld, mp, w.Vt, w.W, w.ldv, n, D, st));
   if ((rc = factor_impl(ctx, mp, K22, ld, D + n, w.wsS, nullptr))) return rc;
@@ -685,6 +690,10 @@ struct ipmz_qp {
   bool timing = false;
   std::vector<hipEvent_t> ev;  // phase boundary events
   hipEvent_t (*tr_pairs)[2] = nullptr;
+  // completion of the last multi-stream (eager) step: the next one is not
+  // enqueued before it (queue depth 1, see step_impl)
+  hipEvent_t step_done = nullptr;
+  bool step_pending = false;
   int tr_cap = 0;
   double ph_ms[IPMZ_PH_COUNT] = {0};
   double tr_flops = 0.0;
@@ -1083,7 +1092,23 @@ bool step_forks(const ipmz_qp* s) {
 int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
-  if (!(flags & IPMZ_STEP_GRAPH) || s->timing || step_forks(s)) return run_step(s, flags);
+  if (step_forks(s) && !s->timing) {
+    // A factorization that forks onto the look-ahead streams is enqueued
+    // eagerly (~130-160 launches and event waits over four queues); with
+    // the next step's packets already queued behind it the command processor
+    // slows the running step down (C2: 3.9 vs 3.1 ms per step back to back;
+    // tools/step_sync_ab.py), so at most one such step is in flight: the host
+    // waits for the previous one before enqueuing the next.
+    if (!s->step_done) HIP_OK(hipEventCreateWithFlags(&s->step_done, hipEventDisableTiming));
+    if (s->step_pending) HIP_OK(hipEventSynchronize(s->step_done));
+    s->step_pending = false;
+    const int rc = run_step(s, flags);
+    if (rc) return rc;
+    HIP_OK(hipEventRecord(s->step_done, s->ctx->stream));
+    s->step_pending = true;
+    return IPMZ_OK;
+  }
+  if (!(flags & IPMZ_STEP_GRAPH) || s->timing) return run_step(s, flags);
   hipStream_t st = s->ctx->stream;
   if (!s->gexec || s->graph_flags != flags) {
     if (s->gexec) hipGraphExecDestroy(s->gexec);
@@ -1169,6 +1194,7 @@ int ipmz_qp_destroy(ipmz_qp* s) {
   if (s->gexec) hipGraphExecDestroy(s->gexec);
   if (s->graph) hipGraphDestroy(s->graph);
   for (auto e : s->ev) hipEventDestroy(e);
+  if (s->step_done) hipEventDestroy(s->step_done);
   if (s->tr_pairs) {
     for (int i = 0; i < s->tr_cap; ++i) {
       hipEventDestroy(s->tr_pairs[i][0]);

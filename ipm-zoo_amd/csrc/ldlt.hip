@@ -302,6 +302,9 @@ hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, con
   g.C = C;
   g.ldc = ldc;
   g.lower = 0;
+  // in place (C == A) is safe only with one tile column per row band: N <= 128;
+  // 64-row bands double the grid of the normal equations' TRSM steps (512 rows)
+  if (M <= 4096) return launch_gemm<64, 128, EPI_STORE, 2, 4>(g, st);
   return launch_gemm<128, 128, EPI_STORE, 2, 4>(g, st);
 }
 

@@ -8,7 +8,8 @@
 //   x   = H^{-1} (r0 - B^T l).
 // Factor: Cholesky of H (as L D L^T with D > 0: the blocked LDL^T of
 // ldlt.hip on the leading n x n block), the triangular solve
-// Vt = B L^{-T} (right-looking over 64-column blocks, fp64 MFMA), the
+// Vt = B L^{-T} (right-looking over 128-column blocks with the solve prep's
+// X_J = L_JJ^{-1}, fp64 MFMA), the
 // rank-n update S = E + Vt D^{-1} Vt^T (fp64 MFMA, lower tiles only), and the
 // Cholesky of S.  Solve: two solves with H, one with S, two GEMVs with B.
 // B itself is left in K (the solve's GEMVs read it); Vt lives in the
@@ -83,7 +84,8 @@ hipError_t ne_check_pos(const double* D, int N, int offset, int* info, hipStream
 }
 
 // Vt <- Vt L^{-T} for the unit-lower n x n factor L (in K, ld) whose nb x nb
-// diagonal-block inverses are LinvH: right-looking over nb-column blocks
+// diagonal-block inverses are LinvH (row-major nb x nb each, zero outside a
+// partial last block): right-looking over nb-column blocks (nb <= 128)
 hipError_t ne_trsm_right(double* Vt, int64_t ldv, int rows, int n, const double* K, int64_t ld, const double* LinvH,
                          int nb, hipStream_t st) {
   hipError_t e = hipSuccess;
