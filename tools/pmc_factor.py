@@ -14,7 +14,11 @@ GEMMs, the panel chain and rows launches, the solve prep).  Corrections
 FETCH_SIZE reports half the bytes of a 16-B/lane read on gfx950 (doubled);
 SQ_INSTS_VALU_MFMA_MOPS_F64 counts 512-flop units.
 
-    python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir> <label> <N> > profiles/factor_traffic_c3.json
+    python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir[,dir...]> <label> <N> > profiles/factor_traffic_c3.json
+
+(the MFMA counters may come from several smaller passes, comma-separated:
+one large pass slows every dispatch enough that the panel path's cross-launch
+hand-offs can hit their spin limit under the profiler's serialization)
 """
 import csv
 import json
@@ -39,7 +43,12 @@ def load(d):
 def main():
     fetch, nf = load(sys.argv[1])
     write, _ = load(sys.argv[2])
-    mfma, _ = load(sys.argv[3])
+    mfma = defaultdict(lambda: defaultdict(float))
+    for d in sys.argv[3].split(","):
+        part, _ = load(d)
+        for k, cs in part.items():
+            for c, v in cs.items():
+                mfma[k][c] += v
     label = sys.argv[4] if len(sys.argv) > 4 else ""
     N = int(sys.argv[5]) if len(sys.argv) > 5 else 11264
     kernels = sorted(set(fetch) | set(write) | set(mfma))
