@@ -31,7 +31,10 @@ for s in ${STEPS:-smoke tests bench prof}; do
     # factor-phase counters of ONE bench step (tools/pmc_factor.py), one counter group per pass
     pmcf_fetch) step pmcf_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     pmcf_write) step pmcf_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcf_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
-    pmcf_mfma) step pmcf_mfma 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES -d "$OUT/pmcf_mfma" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    # (two small passes: one 4-counter pass slows every dispatch enough that the
+    # panel path's cross-launch hand-offs can time out under the profiler)
+    pmcf_mops) step pmcf_mops 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 -d "$OUT/pmcf_mops" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_busy) step pmcf_busy 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d "$OUT/pmcf_busy" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;

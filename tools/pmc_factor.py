@@ -6,7 +6,8 @@ separate rocprofv3 --pmc passes of ONE bench step
 
     pass fetch : FETCH_SIZE
     pass write : WRITE_SIZE
-    pass mfma  : SQ_INSTS_VALU_MFMA_MOPS_F64 SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CU_CYCLES
+    pass mops  : SQ_INSTS_VALU_MFMA_MOPS_F64
+    pass busy  : SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES
 
 The factor phase = every launch of the factor's kernels (trailing / strip
 GEMMs, the panel chain and rows launches, the solve prep).  Corrections
