@@ -189,6 +189,10 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
                                     Bunch-Kaufman (LinearSolvers.cpp:76-318); N <= 4096 */
 #define IPMZ_EQ_PENALTY 2        /* PenaltyFunction: -mu (lambda_C, lambda_C) block (mu I,
                                     mu = the iterate's environment mu), no p: LDL^T */
+#define IPMZ_EQ_PENALTY_EXTRA_DUAL 3 /* PenaltyFunctionWithExtraDual: the reference derives
+                                        PenaltyFunction's optimality conditions through it
+                                        (SymbolicOptimization.cpp:364-366) -- the same Newton
+                                        system (tests/golden/formulations.txt), solved alike */
 /* Settings::InequalityHandling (SymbolicOptimization.h:28-64) */
 #define IPMZ_INEQ_SLACKED_SLACKS 0 /* s with slacks g = s - l_A, h = u_A - s (and y, z
                                       for x): the reference default                  */

@@ -881,7 +881,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0 || B <= 0)
     return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
   if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE &&
-      cfg->equality_handling != IPMZ_EQ_PENALTY)
+      cfg->equality_handling != IPMZ_EQ_PENALTY && cfg->equality_handling != IPMZ_EQ_PENALTY_EXTRA_DUAL)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
   if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + cfg->m + cfg->p > IPMZ_BK_NMAX)
     return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
@@ -905,7 +905,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->N = cfg->n + cfg->m + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
-  s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY;
+  s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY || cfg->equality_handling == IPMZ_EQ_PENALTY_EXTRA_DUAL;
   s->slacks = ih == IPMZ_INEQ_SLACKS;
   s->vlo = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_LOWER;
   s->vup = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_UPPER;

@@ -111,7 +111,8 @@ struct IterationRecord {
 enum class EqualityHandling {
   Regularization = IPMZ_EQ_REGULARIZATION,
   None = IPMZ_EQ_NONE,
-  PenaltyFunction = IPMZ_EQ_PENALTY
+  PenaltyFunction = IPMZ_EQ_PENALTY,
+  PenaltyFunctionWithExtraDual = IPMZ_EQ_PENALTY_EXTRA_DUAL  // the same Newton system (SymbolicOptimization.cpp:364-366)
 };
 
 // Settings::Bounds and Settings::InequalityHandling (SymbolicOptimization.h:

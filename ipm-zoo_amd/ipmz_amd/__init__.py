@@ -62,6 +62,7 @@ class IpmzError(AssertionError):
 EQ_REGULARIZATION = 0  # Settings::EqualityHandling::Regularization (include/ipmz.h IPMZ_EQ_*)
 EQ_NONE = 1            # zero (lambda_C, lambda_C) block, Bunch-Kaufman factor
 EQ_PENALTY = 2         # PenaltyFunction: -mu (lambda_C, lambda_C) block, LDL^T
+EQ_PENALTY_EXTRA_DUAL = 3  # PenaltyFunctionWithExtraDual: the same Newton system (reference-derived)
 INEQ_SLACKED_SLACKS = 0  # Settings::InequalityHandling (include/ipmz.h IPMZ_INEQ_*)
 INEQ_SLACKS = 1          # no g/h/y/z slacks (the reference's corrector defect reproduced)
 BOUNDS_BOTH = 0          # Settings::Bounds (include/ipmz.h IPMZ_BOUNDS_*)

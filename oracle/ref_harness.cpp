@@ -205,6 +205,12 @@ static int mode_formulation(const std::string& dir) {
       {"SlackedSlacks", "none", true, "Both", "Lower"}, {"SlackedSlacks", "none", true, "Both", "Upper"},
       {"SlackedSlacks", "none", true, "Both", "None"}, {"SlackedSlacks", "none", true, "Lower", "Both"},
       {"SlackedSlacks", "none", true, "Upper", "Both"}, {"Slacks", "none", false, "None", "Both"},
+      // equality handlings beyond the numerically used ones (their Newton
+      // systems: PenaltyFunctionWithExtraDual is the system PenaltyFunction is
+      // mapped to, SymbolicOptimization.cpp:364-366), and NaiveSlacks
+      {"SlackedSlacks", "PenaltyFunctionWithExtraDual", true, "Both", "Both"},
+      {"SlackedSlacks", "SlackedSlacks", true, "Both", "Both"},
+      {"NaiveSlacks", "none", true, "Both", "Both"},
   };
   for (const auto& c : cases) {
     auto s = settings_from(c.ineq, c.eq, c.has_ineq);

@@ -125,3 +125,18 @@ def test_penalty_full_solve(ctx):
     iters, tr = g.solve(100)
     assert iters == it and tr[-1]["converged"] == 1.0
     assert np.abs(g.vars() - o.vars()).max() < 1e-8
+
+
+def test_penalty_extra_dual_matches_penalty(ctx):
+    # IPMZ_EQ_PENALTY_EXTRA_DUAL: the reference's PenaltyFunctionWithExtraDual
+    # system is PenaltyFunction's (tests/test_oracle_eqnone.py): bit for bit
+    n, m, p, seed = 48, 12, 6, 4
+    a = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_PENALTY)
+    b = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_PENALTY_EXTRA_DUAL)
+    a.generate(seed)
+    b.generate(seed)
+    for _ in range(3):
+        a.step()
+        b.step()
+        assert np.array_equal(a.vars(), b.vars()) and np.array_equal(a.dir(), b.dir())
+

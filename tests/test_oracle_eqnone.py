@@ -95,3 +95,14 @@ def test_penalty_formulation_and_kkt():
     o.iterate()
     d = o.split(o.daff())
     assert "p" not in o.order and len(d["lambda_C"]) == p
+
+
+def test_penalty_extra_dual_is_the_same_newton_system():
+    # Settings::EqualityHandling::PenaltyFunctionWithExtraDual: the reference
+    # derives PenaltyFunction's optimality conditions through it
+    # (SymbolicOptimization.cpp:364-366), and its symbolic output for both is
+    # the same Newton system, shorthand and augmented system -- so
+    # IPMZ_EQ_PENALTY_EXTRA_DUAL runs the PenaltyFunction path
+    pf = _section("=== inequality_handling=SlackedSlacks equalities=PenaltyFunction inequalities=Both")
+    px = _section("=== inequality_handling=SlackedSlacks equalities=PenaltyFunctionWithExtraDual inequalities=Both")
+    assert pf.split("\n", 1)[1] == px.split("\n", 1)[1]
