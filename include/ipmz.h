@@ -201,6 +201,11 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
                                       dX_aff for X in (X - L_x),
                                       reproduced.  Bounds must be IPMZ_BOUNDS_BOTH
                                       (inequality bounds: when m > 0). */
+#define IPMZ_INEQ_NAIVE_SLACKS 2   /* no s: l_A + g = A x, A x + h = u_A with duals lambda_g,
+                                      lambda_h as KKT rows (N = n + 2m + p); the reference's
+                                      evaluator asserts on its zero block, Evaluation.cpp:
+                                      57-60.  Both inequality bounds; not with the
+                                      normal-equations reduction. */
 /* Settings::Bounds for inequality_bounds / variable_bounds */
 #define IPMZ_BOUNDS_BOTH 0
 #define IPMZ_BOUNDS_LOWER 1

@@ -678,7 +678,7 @@ struct ipmz_qp {
   bool eqnone = false;
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
-  bool slacks = false;
+  bool slacks = false, naive = false;
   bool vlo = true, vup = true, alo = true, aup = true;
   int* ipiv = nullptr;
   int64_t sP = 0;
@@ -710,7 +710,7 @@ int64_t slot_len(const ipmz_qp* s, int slot) {
     case LZ: return s->vup ? s->n : 0;
     case Y: return (s->vlo && !s->slacks) ? s->n : 0;
     case Z: return (s->vup && !s->slacks) ? s->n : 0;
-    case LA: case S: return s->m;
+    case LA: case S: return s->naive ? 0 : s->m;
     case LG: return s->alo ? s->m : 0;
     case LH: return s->aup ? s->m : 0;
     case G: return (s->alo && !s->slacks) ? s->m : 0;
@@ -730,12 +730,16 @@ double* dev_array(ipmz_qp* s, int64_t count, int64_t* stride_out = nullptr) {
   return static_cast<double*>(ptr);
 }
 
-// slot pointers into one contiguous Newton-order vector
+// slot pointers into one contiguous Newton-order vector (the reference's
+// order; NaiveSlacks puts its duals lambda_g, lambda_h ahead of lambda_C,
+// formulations.txt)
 void carve(const ipmz_qp* s, double* base, double** slots) {
+  static const int naive_order[NSLOT] = {X, LG, LH, LC, P, LY, LZ, G, H, Y, Z, LA, S};
   int64_t off = 0;
   for (int k = 0; k < NSLOT; ++k) {
-    slots[k] = base + off;
-    off += slot_len(s, k);
+    const int slot = s->naive ? naive_order[k] : k;
+    slots[slot] = base + off;
+    off += slot_len(s, slot);
   }
 }
 
@@ -883,11 +887,15 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE &&
       cfg->equality_handling != IPMZ_EQ_PENALTY && cfg->equality_handling != IPMZ_EQ_PENALTY_EXTRA_DUAL)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
-  if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + cfg->m + cfg->p > IPMZ_BK_NMAX)
+  const int mk = cfg->inequality_handling == IPMZ_INEQ_NAIVE_SLACKS ? 2 * cfg->m : cfg->m;
+  if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + mk + cfg->p > IPMZ_BK_NMAX)
     return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
                                   "N <= " + std::to_string(IPMZ_BK_NMAX));
   const int ih = cfg->inequality_handling, ib = cfg->inequality_bounds, vb = cfg->variable_bounds;
-  if (ih != IPMZ_INEQ_SLACKED_SLACKS && ih != IPMZ_INEQ_SLACKS) return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
+  if (ih != IPMZ_INEQ_SLACKED_SLACKS && ih != IPMZ_INEQ_SLACKS && ih != IPMZ_INEQ_NAIVE_SLACKS)
+    return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
+  if (ih == IPMZ_INEQ_NAIVE_SLACKS && cfg->m > 0 && ib != IPMZ_BOUNDS_BOTH)
+    return fail(IPMZ_ERR_INVALID, "InequalityHandling::NaiveSlacks: both inequality bounds");
   if (ib < IPMZ_BOUNDS_BOTH || ib > IPMZ_BOUNDS_NONE || vb < IPMZ_BOUNDS_BOTH || vb > IPMZ_BOUNDS_NONE)
     return fail(IPMZ_ERR_INVALID, "unknown bounds setting");
   if (cfg->m > 0 && ib == IPMZ_BOUNDS_NONE)
@@ -902,11 +910,12 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->n = cfg->n;
   s->m = cfg->m;
   s->p = cfg->p;
-  s->N = cfg->n + cfg->m + cfg->p;
+  s->N = cfg->n + mk + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
   s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY || cfg->equality_handling == IPMZ_EQ_PENALTY_EXTRA_DUAL;
   s->slacks = ih == IPMZ_INEQ_SLACKS;
+  s->naive = ih == IPMZ_INEQ_NAIVE_SLACKS;
   s->vlo = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_LOWER;
   s->vup = vb == IPMZ_BOUNDS_BOTH || vb == IPMZ_BOUNDS_UPPER;
   s->alo = ib == IPMZ_BOUNDS_BOTH || ib == IPMZ_BOUNDS_LOWER;
@@ -996,6 +1005,8 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.eqnone = s->eqnone ? 1 : 0;
     q.eqpen = s->eqpen ? 1 : 0;
     q.slacks = s->slacks ? 1 : 0;
+    q.naive = s->naive ? 1 : 0;
+    q.mk = s->naive ? 2 * m : m;
     q.vlo = s->vlo ? 1 : 0;
     q.vup = s->vup ? 1 : 0;
     q.alo = s->alo ? 1 : 0;
@@ -1348,7 +1359,7 @@ int ipmz_qp_set_reduction(ipmz_qp* s, int reduction) {
   if (!s) return fail(IPMZ_ERR_INVALID, "null qp");
   if (reduction != IPMZ_REDUCTION_AUGMENTED && reduction != IPMZ_REDUCTION_NORMAL)
     return fail(IPMZ_ERR_INVALID, "unknown reduction");
-  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed || s->eqnone || s->eqpen))
+  if (reduction == IPMZ_REDUCTION_NORMAL && (s->B != 1 || s->mixed || s->eqnone || s->eqpen || s->naive))
     return fail(IPMZ_ERR_INVALID, "normal equations: single QPs, not with mixed precision, Regularization equalities");
   HIP_OK(hipSetDevice(s->ctx->device));
   if (reduction == IPMZ_REDUCTION_NORMAL && !s->nws) {

@@ -186,6 +186,8 @@ struct QPDev {
   // Settings (oracle/ipmz_oracle.cpp QP): InequalityHandling::Slacks, and the
   // Lower / Upper halves of Settings::variable_bounds and ::inequalities
   int slacks, vlo, vup, alo, aup;
+  int naive;  // InequalityHandling::NaiveSlacks: no s / lambda_A; lambda_g, lambda_h are KKT rows
+  int mk;     // KKT rows of the inequalities: m, or 2 m (NaiveSlacks); N = n + mk + p
   // problem data (row-major, ld = ldn)
   const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;
   double* v[NSLOT];

@@ -158,8 +158,10 @@ __global__ void k_init_iterate(const QPDev* __restrict__ qs) {
     if (q.vup && !q.slacks) q.v[Z][t] = 1.0;
   }
   if (t < q.m) {
-    q.v[S][t] = 0.5 * (q.lA[t] + q.uA[t]);
-    q.v[LA][t] = 1.0;
+    if (!q.naive) {
+      q.v[S][t] = 0.5 * (q.lA[t] + q.uA[t]);
+      q.v[LA][t] = 1.0;
+    }
     if (q.alo) q.v[LG][t] = 1.0;
     if (q.aup) q.v[LH][t] = 1.0;
     if (q.alo && !q.slacks) q.v[G][t] = 1.0;
@@ -212,6 +214,12 @@ __global__ __launch_bounds__(NT) void k_matvec_rows(const QPDev* __restrict__ qs
   if (lane == 0) out[row] = s;
 }
 
+// the vector A^T multiplies in r_x: lambda_A, or (lambda_h - lambda_g) for
+// NaiveSlacks ("(A^T * (lambda_h - lambda_g))", formulations.txt)
+__device__ __forceinline__ double a_dual(const QPDev& q, int i) {
+  return q.naive ? q.v[LH][i] + (-q.v[LG][i]) : q.v[LA][i];
+}
+
 // A^T lambda_A -> ATl, C^T lambda_C -> CTl: column blocks of NT x row chunks
 // of 128, deterministic two-pass (chunk partials, then an ordered sum).
 constexpr int TCHUNK = 128;
@@ -220,13 +228,12 @@ __global__ __launch_bounds__(NT) void k_matvec_t_part(const QPDev* __restrict__ 
   const QPDev& q = qs[blockIdx.z];
   const int rows = MV == MV_A ? q.m : q.p, cols = q.n;
   const double* M = MV == MV_A ? q.A : q.C;
-  const double* y = MV == MV_A ? q.v[LA] : q.v[LC];
   const int j = blockIdx.x * NT + threadIdx.x;
   const int i0 = blockIdx.y * TCHUNK;
   if (j >= cols) return;
   const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
   double s = 0.0;
-  for (int i = i0; i < i1; ++i) s += M[(int64_t)i * q.ldn + j] * y[i];
+  for (int i = i0; i < i1; ++i) s += M[(int64_t)i * q.ldn + j] * (MV == MV_A ? a_dual(q, i) : q.v[LC][i]);
   q.tpart[(int64_t)blockIdx.y * cols + j] = s;
 }
 template <int MV>
@@ -310,6 +317,19 @@ __device__ __forceinline__ void residual_elem(const QPDev& q, int t, double mu, 
     }
     fa += (0.5 * q.v[X][i]) * mv(&q.Qx[i]);
     fb += q.c[i] * q.v[X][i];
+  } else if (t < n + m && q.naive) {
+    const int i = t - n;
+    const double ax = mv(&q.Ax[i]);
+    const double rlg = (q.lA[i] + q.v[G][i]) + (-ax);             // (l_A + g - (A*x))
+    const double rlh = (q.v[H][i] + ax) + (-q.uA[i]);             // (h + (A*x) - u_A)
+    const double rg = q.v[G][i] * q.v[LG][i] + (-(mu * 1.0));     // ((G*lambda_g) - (mu*e_A))
+    const double rh = q.v[H][i] * q.v[LH][i] + (-(mu * 1.0));
+    q.r[LG][i] = rlg;
+    q.r[LH][i] = rlh;
+    q.r[G][i] = rg;
+    q.r[H][i] = rh;
+    res2 += rlg * rlg + rlh * rlh + rg * rg + rh * rh;
+    comp += fabs(rg) + fabs(rh);
   } else if (t < n + m) {
     const int i = t - n;
     const double rla = mv(&q.Ax[i]) + (-q.v[S][i]);  // ((A*x) - s)
@@ -460,12 +480,19 @@ __device__ __forceinline__ double kkt_aa(const QPDev& q, int i) {
 __device__ __forceinline__ void assemble_row(const QPDev& q, int i, int tid, int nth) {
   double* __restrict__ K = q.K;
   const int64_t ld = q.ldk;
-  const int n = q.n, m = q.m;
+  const int n = q.n, m = q.m, mk = q.mk;
   double* Kr = K + (int64_t)i * ld;
   if (i < n) {
     const double* Qr = q.Q + (int64_t)i * q.ldn;
     for (int j = tid; j < i; j += nth) Kr[j] = Qr[j];
     if (tid == 0) Kr[i] = kkt_xx(q, i, Qr[i]);
+  } else if (i < n + mk && q.naive) {  // | -A | -(L_g^{-1}*G) | 0 |  and  | A | 0 | -(L_h^{-1}*H) |
+    const bool hrow = i >= n + m;
+    const int r = hrow ? i - n - m : i - n;
+    const double* Ar = q.A + (int64_t)r * q.ldn;
+    for (int j = tid; j < n; j += nth) Kr[j] = hrow ? Ar[j] : -Ar[j];
+    for (int j = n + tid; j < i; j += nth) Kr[j] = 0.0;
+    if (tid == 0) Kr[i] = hrow ? -(ipmz_inv(q.v[LH][r]) * q.v[H][r]) : -(ipmz_inv(q.v[LG][r]) * q.v[G][r]);
   } else if (i < n + m) {
     const int r = i - n;
     const double* Ar = q.A + (int64_t)r * q.ldn;
@@ -473,7 +500,7 @@ __device__ __forceinline__ void assemble_row(const QPDev& q, int i, int tid, int
     for (int j = n + tid; j < i; j += nth) Kr[j] = 0.0;
     if (tid == 0) Kr[i] = kkt_aa(q, r);
   } else {
-    const int r = i - n - m;
+    const int r = i - n - mk;
     const double* Cr = q.C + (int64_t)r * q.ldn;
     for (int j = tid; j < n; j += nth) Kr[j] = Cr[j];
     for (int j = n + tid; j < i; j += nth) Kr[j] = 0.0;
@@ -510,6 +537,14 @@ __device__ __forceinline__ void rhs_elem(const QPDev& q, int t) {
     else if (q.vup) q.b[i] = tz + (-rx);  // ((Z^{-1}*(r_z - (L_z*r_lz))) - r_x)
     else if (q.vlo) q.b[i] = -(rx + ty);  // -(r_x + (Y^{-1}*(r_y - (L_y*r_ly))))
     else q.b[i] = -rx;
+  } else if (t < n + q.mk && q.naive) {
+    if (t < n + m) {  // ((L_g^{-1}*r_g) - r_lg)
+      const int i = t - n;
+      q.b[t] = ipmz_inv(q.v[LG][i]) * q.r[G][i] + (-q.r[LG][i]);
+    } else {  // ((L_h^{-1}*r_h) - r_lh)
+      const int i = t - n - m;
+      q.b[t] = ipmz_inv(q.v[LH][i]) * q.r[H][i] + (-q.r[LH][i]);
+    }
   } else if (t < n + m) {
     const int i = t - n;
     const double rla = q.r[LA][i], rs = q.r[S][i];
@@ -527,7 +562,7 @@ __device__ __forceinline__ void rhs_elem(const QPDev& q, int t) {
       q.b[t] = ((ipmz_inv(q.v[LH][i]) * (q.r[H][i] + (-(q.v[H][i] * rs)))) + (-rla)) + (-q.r[LH][i]);
     }
   } else if (t < q.N) {
-    const int i = t - n - m;
+    const int i = t - n - q.mk;
     q.b[t] = (q.eqnone || q.eqpen) ? -q.r[LC][i] : q.delta * q.r[P][i] + (-q.r[LC][i]);
   }
 }
@@ -570,6 +605,18 @@ __device__ __forceinline__ void backsub_elem(const QPDev& q, const DSel& D, int 
                      ((ipmz_inv(q.v[LZ][i]) * q.r[Z][i] + (-q.r[LZ][i])) + (-dx)));
       D.d[Z][i] = -(ipmz_inv(q.v[LZ][i]) * (q.r[Z][i] + q.v[Z][i] * D.d[LZ][i]));
     }
+  } else if (t < n + q.mk && q.naive) {
+    if (t < n + m) {  // -(L_g^{-1}*(r_g + (G*dl_g)))
+      const int i = t - n;
+      const double dlg = q.b[t];
+      D.d[LG][i] = dlg;
+      D.d[G][i] = -(ipmz_inv(q.v[LG][i]) * (q.r[G][i] + q.v[G][i] * dlg));
+    } else {
+      const int i = t - n - m;
+      const double dlh = q.b[t];
+      D.d[LH][i] = dlh;
+      D.d[H][i] = -(ipmz_inv(q.v[LH][i]) * (q.r[H][i] + q.v[H][i] * dlh));
+    }
   } else if (t < n + m) {
     const int i = t - n;
     const double dla = q.b[t], rs = q.r[S][i];
@@ -609,7 +656,7 @@ __device__ __forceinline__ void backsub_elem(const QPDev& q, const DSel& D, int 
       D.d[H][i] = -(ipmz_inv(q.v[LH][i]) * (q.r[H][i] + q.v[H][i] * dlh));
     }
   } else if (t < q.N) {
-    const int i = t - n - m;
+    const int i = t - n - q.mk;
     const double dlc = q.b[t];
     D.d[LC][i] = dlc;
     if (!q.eqnone && !q.eqpen) D.d[P][i] = -(q.r[P][i] + q.delta * dlc);
@@ -819,8 +866,10 @@ __device__ __forceinline__ void update_elem(const QPDev& q, int t, double s) {
     if (q.vup && !q.slacks) up(Z, t);
   }
   if (t < m) {
-    up(LA, t);
-    up(S, t);
+    if (!q.naive) {
+      up(LA, t);
+      up(S, t);
+    }
     if (q.alo) up(LG, t);
     if (q.aup) up(LH, t);
     if (q.alo && !q.slacks) up(G, t);
@@ -951,7 +1000,7 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
   // strict lower triangle in 128-column units (a wave per unit, a column
   // pair per lane), eight units per wave in flight: one workgroup moves the
   // QP's ~0.8 MB only with many loads outstanding
-  const int N = q.N, n = q.n, nm = q.n + q.m;
+  const int N = q.N, n = q.n, m = q.m, nm = q.n + q.mk;
   const int nch = (N + 127) / 128, units = N * nch;
   for (int u0 = (blockIdx.x * (FT / 64) + wave) * 8; u0 < units; u0 += gridDim.x * (FT / 64) * 8) {
     double v0[8], v1[8];
@@ -960,11 +1009,14 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
       const int u = u0 + k, i = u / nch, j = (u % nch) * 128 + 2 * lane;
       v0[k] = v1[k] = 0.0;
       if (u < units) {
+        // NaiveSlacks: the lambda_g rows hold -A, the lambda_h rows A
+        const bool ah = q.naive && i >= n + m && i < nm;
         const double* src = i < n ? q.Q + (int64_t)i * q.ldn
-                           : i < nm ? q.A + (int64_t)(i - n) * q.ldn : q.C + (int64_t)(i - nm) * q.ldn;
+                           : i < nm ? q.A + (int64_t)(ah ? i - n - m : i - n) * q.ldn : q.C + (int64_t)(i - nm) * q.ldn;
+        const bool neg = q.naive && i >= n && i < n + m;
         const int lim = i < n ? i : n;  // source columns [0, lim); zeros in [n, i)
-        if (j < lim) v0[k] = src[j];
-        if (j + 1 < lim) v1[k] = src[j + 1];
+        if (j < lim) v0[k] = neg ? -src[j] : src[j];
+        if (j + 1 < lim) v1[k] = neg ? -src[j + 1] : src[j + 1];
       }
     }
 #pragma unroll
@@ -981,6 +1033,8 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
   for (int i = tid; i < N; i += FT) {
     double* Kd = q.K + (int64_t)i * q.ldk + i;
     if (i < n) *Kd = kkt_xx(q, i, q.Q[(int64_t)i * q.ldn + i]);
+    else if (q.naive && i < n + m) *Kd = -(ipmz_inv(q.v[LG][i - n]) * q.v[G][i - n]);
+    else if (q.naive && i < nm) *Kd = -(ipmz_inv(q.v[LH][i - n - m]) * q.v[H][i - n - m]);
     else if (i < nm) *Kd = kkt_aa(q, i - n);
     else *Kd = q.eqnone ? 0.0 : q.eqpen ? -q.scal[SC_MU_NEW] : -(q.delta * q.delta);
   }
@@ -1090,20 +1144,20 @@ __global__ __launch_bounds__(FT) void k_fused_eval(const QPDev* __restrict__ qs)
     }
   }
   // transposes: thread per column, rows in TCHUNK chunks (the grid order)
-  auto col_sum = [&](const double* M, const double* y, int rows, int j) {
+  auto col_sum = [&](const double* M, auto yf, int rows, int j) {
     double tot = 0.0;
     for (int i0 = 0; i0 < rows; i0 += TCHUNK) {
       const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
       double c = 0.0;
 #pragma unroll 8
-      for (int i = i0; i < i1; ++i) c += M[(int64_t)i * q.ldn + j] * y[i];
+      for (int i = i0; i < i1; ++i) c += M[(int64_t)i * q.ldn + j] * yf(i);
       tot += c;
     }
     return tot;
   };
   for (int j = blockIdx.x * FT + tid; j < n; j += gridDim.x * FT) {
-    if (m) st_sc1(&q.ATl[j], col_sum(q.A, q.v[LA], m, j));
-    if (p) st_sc1(&q.CTl[j], col_sum(q.C, q.v[LC], p, j));
+    if (m) st_sc1(&q.ATl[j], col_sum(q.A, [&](int i) { return a_dual(q, i); }, m, j));
+    if (p) st_sc1(&q.CTl[j], col_sum(q.C, [&](int i) { return q.v[LC][i]; }, p, j));
   }
   // arrival (sync.h protocol: write-through data, vmcnt drained, barrier, one
   // agent-scope atomic); no cache-wide fences

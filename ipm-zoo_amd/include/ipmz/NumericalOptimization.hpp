@@ -116,10 +116,14 @@ enum class EqualityHandling {
 };
 
 // Settings::Bounds and Settings::InequalityHandling (SymbolicOptimization.h:
-// 28-39): the numeric path runs SlackedSlacks and Slacks (Slacks with Both
-// bounds only); NaiveSlacks is rejected.
+// 28-39): SlackedSlacks, Slacks (Both bounds only) and NaiveSlacks (both
+// inequality bounds).
 enum class Bounds { None = IPMZ_BOUNDS_NONE, Lower = IPMZ_BOUNDS_LOWER, Upper = IPMZ_BOUNDS_UPPER, Both = IPMZ_BOUNDS_BOTH };
-enum class InequalityHandling { Slacks = IPMZ_INEQ_SLACKS, SlackedSlacks = IPMZ_INEQ_SLACKED_SLACKS };
+enum class InequalityHandling {
+  Slacks = IPMZ_INEQ_SLACKS,
+  SlackedSlacks = IPMZ_INEQ_SLACKED_SLACKS,
+  NaiveSlacks = IPMZ_INEQ_NAIVE_SLACKS
+};
 
 // The subset of Settings (SymbolicOptimization.h:58-64) that selects the
 // Newton system; defaults are this library's (Regularization when equality

@@ -65,6 +65,7 @@ EQ_PENALTY = 2         # PenaltyFunction: -mu (lambda_C, lambda_C) block, LDL^T
 EQ_PENALTY_EXTRA_DUAL = 3  # PenaltyFunctionWithExtraDual: the same Newton system (reference-derived)
 INEQ_SLACKED_SLACKS = 0  # Settings::InequalityHandling (include/ipmz.h IPMZ_INEQ_*)
 INEQ_SLACKS = 1          # no g/h/y/z slacks (the reference's corrector defect reproduced)
+INEQ_NAIVE_SLACKS = 2    # no s; lambda_g, lambda_h as KKT rows (N = n + 2m + p)
 BOUNDS_BOTH = 0          # Settings::Bounds (include/ipmz.h IPMZ_BOUNDS_*)
 BOUNDS_LOWER = 1
 BOUNDS_UPPER = 2
@@ -378,7 +379,7 @@ class Optimizer:
         _check(lib.ipmz_qp_create(self.ctx.h, ctypes.byref(cfg), ctypes.byref(h)), "ipmz_qp_create")
         self.h = h
         self.n, self.m, self.p = n, m, p
-        self.N = n + m + p
+        self.N = lib.ipmz_qp_kkt_dim(h)  # n + m + p, or n + 2m + p (NaiveSlacks)
         self.state_len = lib.ipmz_qp_state_len(h)
 
     @classmethod
@@ -495,7 +496,7 @@ class Batch(Optimizer):
         _check(lib.ipmz_batch_create(self.ctx.h, ctypes.byref(cfg), batch, ctypes.byref(h)), "ipmz_batch_create")
         self.h = h
         self.n, self.m, self.p = n, m, p
-        self.N = n + m + p
+        self.N = lib.ipmz_qp_kkt_dim(h)  # n + m + p, or n + 2m + p (NaiveSlacks)
         self.batch = batch
         self.state_len = lib.ipmz_qp_state_len(h)
 

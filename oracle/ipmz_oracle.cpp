@@ -79,6 +79,12 @@ struct QP {
   // Defaults: SlackedSlacks, Bounds::Both.
   bool slacks = false;
   bool vlo = true, vup = true, alo = true, aup = true;
+  // InequalityHandling::NaiveSlacks (formulations.txt): no s and no lambda_A;
+  // l_A + g = A x and A x + h = u_A with their own duals lambda_g, lambda_h,
+  // which become KKT rows: the augmented system is [x, lambda_g, lambda_h,
+  // lambda_C] (n + 2m + p).  The reference's evaluator asserts on its zero
+  // (lambda_g, lambda_h) block (Evaluation.cpp:57-60); Bounds::Both only.
+  bool naive = false;
   Vec Q, c, A, lA, uA, C, d, lx, ux;
   Vec v[NSLOT];       // iterate
   Vec daff[NSLOT], dir[NSLOT];
@@ -90,7 +96,7 @@ struct QP {
       case LZ: return vup ? n : 0;
       case Y: return vlo && !slacks ? n : 0;
       case Z: return vup && !slacks ? n : 0;
-      case LA: case S: return m;
+      case LA: case S: return naive ? 0 : m;
       case LG: return alo ? m : 0;
       case LH: return aup ? m : 0;
       case G: return alo && !slacks ? m : 0;
@@ -99,7 +105,8 @@ struct QP {
       default: return p;
     }
   }
-  int64_t N() const { return n + m + p; }
+  int64_t mk() const { return naive ? 2 * m : m; }  // KKT rows of the inequalities
+  int64_t N() const { return n + mk() + p; }
 };
 
 // ---------------------------------------------------------------------------
@@ -135,7 +142,15 @@ void residuals(const QP& q, double mu, Residuals& R) {
   const Vec* v = q.v;
   Vec Qx(n), ATl(n), CTl(n), Ax(m), Cx(p);
   matvec(q.Q, n, n, v[X].data(), Qx.data());
-  if (m) { matvec_t(q.A, m, n, v[LA].data(), ATl.data()); matvec(q.A, m, n, v[X].data(), Ax.data()); }
+  if (m && q.naive) {  // (A^T * (lambda_h - lambda_g))
+    Vec dl(m);
+    for (int64_t i = 0; i < m; ++i) dl[i] = v[LH][i] + (-v[LG][i]);
+    matvec_t(q.A, m, n, dl.data(), ATl.data());
+    matvec(q.A, m, n, v[X].data(), Ax.data());
+  } else if (m) {
+    matvec_t(q.A, m, n, v[LA].data(), ATl.data());
+    matvec(q.A, m, n, v[X].data(), Ax.data());
+  }
   if (p) { matvec_t(q.C, p, n, v[LC].data(), CTl.data()); matvec(q.C, p, n, v[X].data(), Cx.data()); }
   for (int64_t i = 0; i < n; ++i) {
     // r_x := (c [+ lambda_z] + (Q*x) [+ (A^T*lambda_A)] [+ (C^T*lambda_C)] [- lambda_y])
@@ -159,7 +174,13 @@ void residuals(const QP& q, double mu, Residuals& R) {
       }
     }
   }
-  for (int64_t i = 0; i < m; ++i) {
+  for (int64_t i = 0; i < m && q.naive; ++i) {
+    R.r[LG][i] = (q.lA[i] + v[G][i]) + (-Ax[i]);        // (l_A + g - (A*x))
+    R.r[LH][i] = (v[H][i] + Ax[i]) + (-q.uA[i]);        // (h + (A*x) - u_A)
+    R.r[G][i] = v[G][i] * v[LG][i] + (-(mu * 1.0));     // ((G*lambda_g) - (mu*e_A))
+    R.r[H][i] = v[H][i] * v[LH][i] + (-(mu * 1.0));
+  }
+  for (int64_t i = 0; i < m && !q.naive; ++i) {
     R.r[LA][i] = Ax[i] + (-v[S][i]);  // ((A*x) - s)
     if (q.alo && q.aup) R.r[S][i] = -((v[LA][i] + v[LG][i]) + (-v[LH][i]));  // -(lambda_A + lambda_g - lambda_h)
     else if (q.alo) R.r[S][i] = -(v[LA][i] + v[LG][i]);                      // -(lambda_A + lambda_g)
@@ -198,8 +219,11 @@ inline void comp_rows(const QP& q, int out[4]) {
 // Newton-variable order of the reference (absent blocks dropped).
 std::vector<int> order(const QP& q) {
   std::vector<int> o;
-  for (int s = 0; s < NSLOT; ++s)
+  static const int naive_order[NSLOT] = {X, LG, LH, LC, P, LY, LZ, G, H, Y, Z, LA, S};
+  for (int k = 0; k < NSLOT; ++k) {
+    const int s = q.naive ? naive_order[k] : k;
     if (q.size(s) > 0) o.push_back(s);
+  }
   return o;
 }
 
@@ -298,19 +322,30 @@ void assemble(const QP& q, double* K) {
     for (int64_t j = 0; j < n; ++j) K[i * N + j] = q.Q[i * n + j];
     K[i * N + i] = kkt_xx(q, i, q.Q[i * n + i]);  // elementwise_diag_mat_op
   }
-  for (int64_t r = 0; r < m; ++r) {
+  for (int64_t r = 0; r < m && q.naive; ++r) {  // | -A | -(L_g^{-1}*G) | 0 |, | A | 0 | -(L_h^{-1}*H) |
+    for (int64_t j = 0; j < n; ++j) {
+      K[(n + r) * N + j] = -q.A[r * n + j];
+      K[j * N + n + r] = -q.A[r * n + j];
+      K[(n + m + r) * N + j] = q.A[r * n + j];
+      K[j * N + n + m + r] = q.A[r * n + j];
+    }
+    K[(n + r) * N + n + r] = -(inv(q.v[LG][r]) * q.v[G][r]);
+    K[(n + m + r) * N + n + m + r] = -(inv(q.v[LH][r]) * q.v[H][r]);
+  }
+  for (int64_t r = 0; r < m && !q.naive; ++r) {
     for (int64_t j = 0; j < n; ++j) {
       K[(n + r) * N + j] = q.A[r * n + j];
       K[j * N + n + r] = q.A[r * n + j];
     }
     K[(n + r) * N + n + r] = kkt_aa(q, r);
   }
+  const int64_t c0 = n + q.mk();
   for (int64_t r = 0; r < p; ++r) {
     for (int64_t j = 0; j < n; ++j) {
-      K[(n + m + r) * N + j] = q.C[r * n + j];
-      K[j * N + n + m + r] = q.C[r * n + j];
+      K[(c0 + r) * N + j] = q.C[r * n + j];
+      K[j * N + c0 + r] = q.C[r * n + j];
     }
-    K[(n + m + r) * N + n + m + r] = q.eq_none ? 0.0 : q.eq_pen ? -q.mu : -(q.delta * q.delta);
+    K[(c0 + r) * N + c0 + r] = q.eq_none ? 0.0 : q.eq_pen ? -q.mu : -(q.delta * q.delta);
   }
 }
 
@@ -333,7 +368,11 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
     else if (q.vlo) b[i] = -(rx + ty);               // -(r_x + (Y^{-1}*(r_y - (L_y*r_ly))))
     else b[i] = -rx;                                 // -r_x
   }
-  for (int64_t i = 0; i < m; ++i) {
+  for (int64_t i = 0; i < m && q.naive; ++i) {
+    b[n + i] = inv(v[LG][i]) * R.r[G][i] + (-R.r[LG][i]);      // ((L_g^{-1}*r_g) - r_lg)
+    b[n + m + i] = inv(v[LH][i]) * R.r[H][i] + (-R.r[LH][i]);  // ((L_h^{-1}*r_h) - r_lh)
+  }
+  for (int64_t i = 0; i < m && !q.naive; ++i) {
     const double rla = R.r[LA][i], rs = R.r[S][i];
     if (q.slacks) {
       const double a = inv(q.uA[i] + (-v[S][i])) * R.r[LH][i], c = inv(v[S][i] + (-q.lA[i])) * R.r[LG][i];
@@ -349,7 +388,7 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
     }
   }
   for (int64_t i = 0; i < p; ++i)  // None: -r_lambda_C ; Regularization: (delta*r_p) - r_lambda_C
-    b[n + m + i] = (q.eq_none || q.eq_pen) ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
+    b[n + q.mk() + i] = (q.eq_none || q.eq_pen) ? -R.r[LC][i] : q.delta * R.r[P][i] + (-R.r[LC][i]);
 }
 
 // Eliminated-variable back-substitution (delta_definitions evaluated in
@@ -357,7 +396,11 @@ void augmented_rhs(const QP& q, const Residuals& R, double* b) {
 void back_substitute(const QP& q, const Residuals& R, Vec* D) {
   const int64_t n = q.n, m = q.m, p = q.p;
   const Vec* v = q.v;
-  for (int64_t i = 0; i < m; ++i) {
+  for (int64_t i = 0; i < m && q.naive; ++i) {
+    D[G][i] = -(inv(v[LG][i]) * (R.r[G][i] + v[G][i] * D[LG][i]));  // -(L_g^{-1}*(r_g + (G*dl_g)))
+    D[H][i] = -(inv(v[LH][i]) * (R.r[H][i] + v[H][i] * D[LH][i]));
+  }
+  for (int64_t i = 0; i < m && !q.naive; ++i) {
     const double dla = D[LA][i], rs = R.r[S][i];
     if (q.slacks) {
       const double a = inv(q.uA[i] + (-v[S][i])) * R.r[LH][i], c = inv(v[S][i] + (-q.lA[i])) * R.r[LG][i];
@@ -576,8 +619,13 @@ void search_direction(QP& q, const Residuals& R, const Factor& F, Vec* out) {
   else solve_ldlt(N, F.L.data(), N, F.Dd.data(), b.data());
   for (int s = 0; s < NSLOT; ++s) out[s].assign(q.size(s), 0.0);
   std::memcpy(out[X].data(), b.data(), sizeof(double) * n);
-  std::memcpy(out[LA].data(), b.data() + n, sizeof(double) * m);
-  std::memcpy(out[LC].data(), b.data() + n + m, sizeof(double) * q.p);
+  if (q.naive) {
+    std::memcpy(out[LG].data(), b.data() + n, sizeof(double) * m);
+    std::memcpy(out[LH].data(), b.data() + n + m, sizeof(double) * m);
+  } else {
+    std::memcpy(out[LA].data(), b.data() + n, sizeof(double) * m);
+  }
+  std::memcpy(out[LC].data(), b.data() + n + q.mk(), sizeof(double) * q.p);
   back_substitute(q, R, out);
 }
 
@@ -904,10 +952,13 @@ void ipmzo_set_equality_none(void* h) {
 // SlackedSlacks, 1 Slacks) and the bounds (IPMZ_BOUNDS_*: 0 None, 1 Lower,
 // 2 Upper, 3 Both) of the inequalities and of the variables.  Resizes the
 // slots and restores build_environment's initial iterate.
-int ipmzo_set_formulation(void* h, int slacks, int ineq_bounds, int var_bounds) {
+// handling: 0 SlackedSlacks, 1 Slacks, 2 NaiveSlacks
+int ipmzo_set_formulation(void* h, int handling, int ineq_bounds, int var_bounds) {
   QP& q = *static_cast<QP*>(h);
   if (q.m > 0 && ineq_bounds == 0) return -1;  // the reference then drops A entirely: not modelled
-  q.slacks = slacks != 0;
+  q.slacks = handling == 1;
+  q.naive = handling == 2;
+  if (q.naive && q.m > 0 && ineq_bounds != 3) return -1;  // NaiveSlacks: both inequality bounds
   q.alo = (ineq_bounds & 1) != 0;
   q.aup = (ineq_bounds & 2) != 0;
   q.vlo = (var_bounds & 1) != 0;
@@ -919,7 +970,7 @@ int ipmzo_set_formulation(void* h, int slacks, int ineq_bounds, int var_bounds) 
     q.dir[s].assign(q.size(s), 0.0);
   }
   for (int64_t i = 0; i < q.n; ++i) q.v[X][i] = 0.5 * (q.lx[i] + q.ux[i]);
-  for (int64_t i = 0; i < q.m; ++i) q.v[S][i] = 0.5 * (q.lA[i] + q.uA[i]);
+  for (int64_t i = 0; i < q.m && !q.naive; ++i) q.v[S][i] = 0.5 * (q.lA[i] + q.uA[i]);
   return 0;
 }
 

@@ -28,13 +28,19 @@ BOUNDS = {"None": 0, "Lower": 1, "Upper": 2, "Both": 3}
 
 
 class Form:
-    """Formulation: inequality handling (slacks=True: InequalityHandling::Slacks)
-    and the bounds of the inequalities / variables (BOUNDS values)."""
+    """Formulation: inequality handling (slacks=True: InequalityHandling::Slacks;
+    naive=True: InequalityHandling::NaiveSlacks) and the bounds of the
+    inequalities / variables (BOUNDS values)."""
 
-    def __init__(self, slacks=False, ineq_bounds=3, var_bounds=3):
+    def __init__(self, slacks=False, ineq_bounds=3, var_bounds=3, naive=False):
         self.slacks = bool(slacks)
+        self.naive = bool(naive)
         self.ineq_bounds = ineq_bounds
         self.var_bounds = var_bounds
+
+    @property
+    def handling(self):  # ipmzo_set_formulation / the C ABI's IPMZ_INEQ_*
+        return 2 if self.naive else 1 if self.slacks else 0
 
 
 def slot_size(name, n, m, p, eq_none=False, form=None):
@@ -44,7 +50,8 @@ def slot_size(name, n, m, p, eq_none=False, form=None):
     alo, aup = bool(f.ineq_bounds & 1), bool(f.ineq_bounds & 2)
     sizes = {"x": n, "lambda_y": n if vlo else 0, "lambda_z": n if vup else 0,
              "y": n if vlo and not f.slacks else 0, "z": n if vup and not f.slacks else 0,
-             "lambda_A": m, "s": m, "lambda_g": m if alo else 0, "lambda_h": m if aup else 0,
+             "lambda_A": 0 if f.naive else m, "s": 0 if f.naive else m,
+             "lambda_g": m if alo else 0, "lambda_h": m if aup else 0,
              "g": m if alo and not f.slacks else 0, "h": m if aup and not f.slacks else 0}
     if name in sizes:
         return sizes[name]
@@ -53,9 +60,14 @@ def slot_size(name, n, m, p, eq_none=False, form=None):
     return p
 
 
+NAIVE_ORDER = ["x", "lambda_g", "lambda_h", "lambda_C", "p", "lambda_y", "lambda_z", "g", "h", "y", "z"]
+
+
 def newton_order(n, m, p, eq_none=False, form=None):
-    """Reference Newton-variable order with absent blocks dropped."""
-    return [s for s in SLOTS if slot_size(s, n, m, p, eq_none, form) > 0]
+    """Reference Newton-variable order with absent blocks dropped (NaiveSlacks:
+    formulations.txt, its duals lambda_g, lambda_h ahead of lambda_C)."""
+    slots = NAIVE_ORDER if form is not None and form.naive else SLOTS
+    return [s for s in slots if slot_size(s, n, m, p, eq_none, form) > 0]
 
 
 def _dp(a):
@@ -200,7 +212,7 @@ class OracleQP:
             lib().ipmzo_set_equality_none(self.h)
         if form is not None:
             ib = form.ineq_bounds if m else 3
-            if lib().ipmzo_set_formulation(self.h, int(form.slacks), ib, form.var_bounds) != 0:
+            if lib().ipmzo_set_formulation(self.h, form.handling, ib, form.var_bounds) != 0:
                 raise ValueError("unsupported formulation")
         self.N = lib().ipmzo_kkt_dim(self.h)
         self.L = lib().ipmzo_state_len(self.h)

@@ -126,9 +126,64 @@ def test_formulation_batch_matches_single(ctx):
 @pytest.mark.parametrize("kw,msg", [
     (dict(inequality_bounds=3), "m > 0 with no inequality bound"),
     (dict(inequality_handling=1, variable_bounds=1), "Slacks with one-sided bounds"),
-    (dict(inequality_handling=2), "NaiveSlacks"),
+    (dict(inequality_handling=2, inequality_bounds=1), "NaiveSlacks with one-sided inequality bounds"),
+    (dict(inequality_handling=3), "unknown inequality handling"),
     (dict(variable_bounds=4), "unknown bounds"),
 ])
 def test_formulation_rejected(ctx, kw, msg):
     with pytest.raises(I.IpmzError):
         I.Optimizer(16, 4, 0, ctx, **kw)
+
+
+# InequalityHandling::NaiveSlacks: the reference's symbolic engine defines it
+# (tests/golden/formulations.txt) but its evaluator asserts on the zero
+# (lambda_g, lambda_h) block (Evaluation.cpp:57-60), so there is no reference
+# trace: the GPU path is checked against the oracle's restatement (parity
+# pinned to the reference's formulas only, tests/test_oracle_formulations.py)
+@pytest.mark.parametrize("n,m,p,seed", [(48, 16, 6, 7), (300, 70, 30, 3)])
+def test_naive_slacks_vs_oracle(ctx, n, m, p, seed):
+    form = oracle.Form(naive=True)
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), form=form)
+    g = I.Optimizer(n, m, p, ctx, inequality_handling=I.INEQ_NAIVE_SLACKS)
+    g.generate(seed)
+    assert g.N == n + 2 * m + p == o.N
+    assert np.array_equal(g.vars(), o.vars())
+    assert np.array_equal(g.kkt(), np.tril(o.kkt()))
+    for it in range(8):
+        s0 = g.scalars()
+        done, rec = o.iterate()
+        for k in ("f", "res", "mu"):
+            assert abs(s0[k] - rec[k]) <= 1e-12 * max(1.0, abs(rec[k])), (it, k)
+        if done:
+            assert s0["converged"] == 1.0
+            break
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (it, k, s1[k], rec[k])
+        for which, (a, b) in enumerate(((g.daff(), o.daff()), (g.dir(), o.dir()))):
+            sa, sb = o.split(a), o.split(b)
+            for s in o.order:
+                _close(sa[s], sb[s], (it, which, s))
+            assert np.abs(sa["x"] - sb["x"]).max() < DX_TOL, (it, which)
+        g.set_vars(o.vars())
+
+
+def test_naive_slacks_batch_and_solve(ctx):
+    n, m, p, B = 64, 16, 8, 3
+    bt = I.Batch(n, m, p, B, ctx, inequality_handling=I.INEQ_NAIVE_SLACKS)
+    bt.generate(5)
+    g = I.Optimizer(n, m, p, ctx, inequality_handling=I.INEQ_NAIVE_SLACKS)
+    g.generate(6)  # QP 1 of the batch
+    iters, tr = g.solve(100)
+    assert tr[-1]["converged"] == 1.0 and iters < 40
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, 6), form=oracle.Form(naive=True))
+    for it in range(100):
+        done, _ = o.iterate()
+        if done:
+            break
+    assert iters == it
+    assert np.abs(o.split(g.vars())["x"] - o.split(o.vars())["x"]).max() < 1e-8
+    bt.step()
+    with pytest.raises(I.IpmzError):
+        g.set_reduction(I.REDUCTION_NORMAL)
