@@ -193,6 +193,12 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
                                         PenaltyFunction's optimality conditions through it
                                         (SymbolicOptimization.cpp:364-366) -- the same Newton
                                         system (tests/golden/formulations.txt), solved alike */
+#define IPMZ_EQ_SLACKED_SLACKS 4 /* equality SlackedSlacks: t with slacks v = t - d, w = d - t
+                                    (l = u = d), their duals lambda_v, lambda_w; the KKT
+                                    (lambda_C, lambda_C) block -((V^-1 L_v) + (W^-1 L_w))^-1.
+                                    With InequalityHandling::SlackedSlacks and both
+                                    inequality bounds; the reference's evaluator asserts
+                                    on its zero blocks (Evaluation.cpp:57-60) */
 /* Settings::InequalityHandling (SymbolicOptimization.h:28-64) */
 #define IPMZ_INEQ_SLACKED_SLACKS 0 /* s with slacks g = s - l_A, h = u_A - s (and y, z
                                       for x): the reference default                  */

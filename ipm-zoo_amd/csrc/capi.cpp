@@ -679,6 +679,10 @@ struct ipmz_qp {
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
   bool slacks = false, naive = false;
+  // EqualityHandling::SlackedSlacks: m, p below are the step's (m + p equality
+  // rows run as l = u = d inequalities, p = 0); m_usr, p_usr the data's
+  bool eqss = false;
+  int m_usr = 0, p_usr = 0;
   bool vlo = true, vup = true, alo = true, aup = true;
   int* ipiv = nullptr;
   int64_t sP = 0;
@@ -885,7 +889,8 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   if (cfg->n <= 0 || cfg->m < 0 || cfg->p < 0 || B <= 0)
     return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
   if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE &&
-      cfg->equality_handling != IPMZ_EQ_PENALTY && cfg->equality_handling != IPMZ_EQ_PENALTY_EXTRA_DUAL)
+      cfg->equality_handling != IPMZ_EQ_PENALTY && cfg->equality_handling != IPMZ_EQ_PENALTY_EXTRA_DUAL &&
+      cfg->equality_handling != IPMZ_EQ_SLACKED_SLACKS)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
   const int mk = cfg->inequality_handling == IPMZ_INEQ_NAIVE_SLACKS ? 2 * cfg->m : cfg->m;
   if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + mk + cfg->p > IPMZ_BK_NMAX)
@@ -896,6 +901,9 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
   if (ih == IPMZ_INEQ_NAIVE_SLACKS && cfg->m > 0 && ib != IPMZ_BOUNDS_BOTH)
     return fail(IPMZ_ERR_INVALID, "InequalityHandling::NaiveSlacks: both inequality bounds");
+  if (cfg->equality_handling == IPMZ_EQ_SLACKED_SLACKS && (ih != IPMZ_INEQ_SLACKED_SLACKS || ib != IPMZ_BOUNDS_BOTH))
+    return fail(IPMZ_ERR_INVALID, "EqualityHandling::SlackedSlacks: with InequalityHandling::SlackedSlacks and both "
+                                  "inequality bounds");
   if (ib < IPMZ_BOUNDS_BOTH || ib > IPMZ_BOUNDS_NONE || vb < IPMZ_BOUNDS_BOTH || vb > IPMZ_BOUNDS_NONE)
     return fail(IPMZ_ERR_INVALID, "unknown bounds setting");
   if (cfg->m > 0 && ib == IPMZ_BOUNDS_NONE)
@@ -908,8 +916,11 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->ctx = ctx;
   s->B = B;
   s->n = cfg->n;
-  s->m = cfg->m;
-  s->p = cfg->p;
+  s->m_usr = cfg->m;
+  s->p_usr = cfg->p;
+  s->eqss = cfg->equality_handling == IPMZ_EQ_SLACKED_SLACKS;
+  s->m = s->eqss ? cfg->m + cfg->p : cfg->m;
+  s->p = s->eqss ? 0 : cfg->p;
   s->N = cfg->n + mk + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
@@ -928,7 +939,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   int64_t sQ, sA, sC, sn, sm, sp, sS, sNb, sScal, sPart, sT;
   double* Q = dev_array(s, (int64_t)n * s->ldn, &sQ);
   double* A = dev_array(s, (int64_t)m * s->ldn, &sA);
-  double* C = dev_array(s, (int64_t)p * s->ldn, &sC);
+  double* C = dev_array(s, (int64_t)p * s->ldn, &sC);  // (eqss: C is rows m_usr.. of A)
   double* c = dev_array(s, n, &sn);
   double* lx = dev_array(s, n);
   double* ux = dev_array(s, n);
@@ -938,7 +949,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   double* lA = dev_array(s, m, &sm);
   double* uA = dev_array(s, m);
   double* Ax = dev_array(s, m);
-  double* d = dev_array(s, p, &sp);
+  double* d = dev_array(s, s->p_usr, &sp);
   double* Cx = dev_array(s, p);
   double* v = dev_array(s, s->state_len, &sS);
   double* r = dev_array(s, s->state_len);
@@ -1006,6 +1017,9 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.eqpen = s->eqpen ? 1 : 0;
     q.slacks = s->slacks ? 1 : 0;
     q.naive = s->naive ? 1 : 0;
+    q.eqss = s->eqss ? 1 : 0;
+    q.m_usr = s->m_usr;
+    q.p_usr = s->p_usr;
     q.mk = s->naive ? 2 * m : m;
     q.vlo = s->vlo ? 1 : 0;
     q.vup = s->vup ? 1 : 0;
@@ -1013,7 +1027,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.aup = s->aup ? 1 : 0;
     q.Q = Q + i * sQ;
     q.A = A + i * sA;
-    q.C = C + i * sC;
+    q.C = s->eqss ? q.A + (int64_t)s->m_usr * s->ldn : C + i * sC;
     q.c = c + i * sn;
     q.lx = lx + i * sn;
     q.ux = ux + i * sn;
@@ -1062,28 +1076,32 @@ int check_index(ipmz_qp* s, int i) {
 
 int load_one(ipmz_qp* s, int i, const double* Q, const double* c, const double* A, const double* lA, const double* uA,
              const double* C, const double* d, const double* lx, const double* ux) {
-  if (!Q || !c || !lx || !ux || (s->m && (!A || !lA || !uA)) || (s->p && (!C || !d)))
+  if (!Q || !c || !lx || !ux || (s->m_usr && (!A || !lA || !uA)) || (s->p_usr && (!C || !d)))
     return fail(IPMZ_ERR_INVALID, "load: missing data block");
   // EnvironmentBuilder.cpp:12-17 (the reference ASSERTs; here an error code)
   for (int k = 0; k < s->n; ++k)
     if (!(lx[k] < ux[k])) return fail(IPMZ_ERR_INVALID, "l_x < u_x violated at " + std::to_string(k));
-  for (int k = 0; k < s->m; ++k)
+  for (int k = 0; k < s->m_usr; ++k)
     if (!(lA[k] <= uA[k])) return fail(IPMZ_ERR_INVALID, "l_A <= u_A violated at " + std::to_string(k));
   HIP_OK(hipSetDevice(s->ctx->device));
   hipStream_t st = s->ctx->stream;
   const QPDev& q = s->hq[i];
   const size_t rowb = (size_t)s->n * 8, ldb = (size_t)s->ldn * 8;
   HIP_OK(hipMemcpy2DAsync((void*)q.Q, ldb, Q, rowb, rowb, s->n, hipMemcpyHostToDevice, st));
-  if (s->m) HIP_OK(hipMemcpy2DAsync((void*)q.A, ldb, A, rowb, rowb, s->m, hipMemcpyHostToDevice, st));
-  if (s->p) HIP_OK(hipMemcpy2DAsync((void*)q.C, ldb, C, rowb, rowb, s->p, hipMemcpyHostToDevice, st));
+  if (s->m_usr) HIP_OK(hipMemcpy2DAsync((void*)q.A, ldb, A, rowb, rowb, s->m_usr, hipMemcpyHostToDevice, st));
+  if (s->p_usr) HIP_OK(hipMemcpy2DAsync((void*)q.C, ldb, C, rowb, rowb, s->p_usr, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync((void*)q.c, c, rowb, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync((void*)q.lx, lx, rowb, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync((void*)q.ux, ux, rowb, hipMemcpyHostToDevice, st));
-  if (s->m) {
-    HIP_OK(hipMemcpyAsync((void*)q.lA, lA, (size_t)s->m * 8, hipMemcpyHostToDevice, st));
-    HIP_OK(hipMemcpyAsync((void*)q.uA, uA, (size_t)s->m * 8, hipMemcpyHostToDevice, st));
+  if (s->m_usr) {
+    HIP_OK(hipMemcpyAsync((void*)q.lA, lA, (size_t)s->m_usr * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync((void*)q.uA, uA, (size_t)s->m_usr * 8, hipMemcpyHostToDevice, st));
   }
-  if (s->p) HIP_OK(hipMemcpyAsync((void*)q.d, d, (size_t)s->p * 8, hipMemcpyHostToDevice, st));
+  if (s->p_usr) HIP_OK(hipMemcpyAsync((void*)q.d, d, (size_t)s->p_usr * 8, hipMemcpyHostToDevice, st));
+  if (s->eqss && s->p_usr) {  // the equality rows as l = u = d
+    HIP_OK(hipMemcpyAsync((void*)(q.lA + s->m_usr), d, (size_t)s->p_usr * 8, hipMemcpyHostToDevice, st));
+    HIP_OK(hipMemcpyAsync((void*)(q.uA + s->m_usr), d, (size_t)s->p_usr * 8, hipMemcpyHostToDevice, st));
+  }
   HIP_OK(hipStreamSynchronize(st));
   return IPMZ_OK;
 }
@@ -1183,14 +1201,64 @@ int scalars_impl(ipmz_qp* s, double* out, int count) {
   return s->loaded ? qp_status(s) : IPMZ_OK;
 }
 
+// EqualityHandling::SlackedSlacks: the step's slots hold [lambda_g lambda_v],
+// [lambda_h lambda_w], [g v], [h w]; the reference's Newton order is
+// lambda_g, lambda_h, lambda_v, lambda_w, ..., g, h, v, w (formulations.txt).
+// perm[k] = the step-vector index of reference-order element k.
+std::vector<int64_t> eqss_perm(const ipmz_qp* s) {
+  const int64_t n = s->n, m = s->m_usr, p = s->p_usr, mp = m + p;
+  const int64_t ny = s->vlo ? n : 0, nz = s->vup ? n : 0;
+  std::vector<int64_t> perm;
+  perm.reserve((size_t)s->state_len);
+  auto run = [&](int64_t from, int64_t len) {
+    for (int64_t k = 0; k < len; ++k) perm.push_back(from + k);
+  };
+  int64_t off = n + 2 * mp;  // x, [lambda_A lambda_C], [s t]: same order
+  run(0, off);
+  const int64_t LGo = off, LHo = off + mp;  // [lambda_g lambda_v], [lambda_h lambda_w]
+  run(LGo, m);
+  run(LHo, m);
+  run(LGo + m, p);
+  run(LHo + m, p);
+  off += 2 * mp;
+  run(off, ny + nz);  // lambda_y, lambda_z
+  off += ny + nz;
+  const int64_t Go = off, Ho = off + mp;  // [g v], [h w]
+  run(Go, m);
+  run(Ho, m);
+  run(Go + m, p);
+  run(Ho + m, p);
+  off += 2 * mp;
+  run(off, s->state_len - off);  // y, z
+  return perm;
+}
+
 int get_state_impl(ipmz_qp* s, int i, int which, double* out) {
   if (which < 0 || which > 3 || !out) return fail(IPMZ_ERR_INVALID, "bad arguments");
   HIP_OK(hipSetDevice(s->ctx->device));
   const QPDev& q = s->hq[i];
   const double* src = which == 0 ? q.v[0] : which == 1 ? q.daff[0] : which == 2 ? q.dir[0] : q.r[0];
+  if (s->eqss) {
+    std::vector<double> tmp((size_t)s->state_len);
+    HIP_OK(hipMemcpyAsync(tmp.data(), src, s->state_len * 8, hipMemcpyDeviceToHost, s->ctx->stream));
+    HIP_OK(hipStreamSynchronize(s->ctx->stream));
+    const auto perm = eqss_perm(s);
+    for (int64_t k = 0; k < s->state_len; ++k) out[k] = tmp[(size_t)perm[(size_t)k]];
+    return IPMZ_OK;
+  }
   HIP_OK(hipMemcpyAsync(out, src, s->state_len * 8, hipMemcpyDeviceToHost, s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   return IPMZ_OK;
+}
+
+// a host iterate in the reference's order -> the step's order
+std::vector<double> state_in(const ipmz_qp* s, const double* in) {
+  std::vector<double> v(in, in + s->state_len);
+  if (s->eqss) {
+    const auto perm = eqss_perm(s);
+    for (int64_t k = 0; k < s->state_len; ++k) v[(size_t)perm[(size_t)k]] = in[k];
+  }
+  return v;
 }
 }  // namespace
 
@@ -1305,8 +1373,9 @@ int ipmz_qp_get_state(ipmz_qp* s, int which, double* out) {
 int ipmz_qp_set_state(ipmz_qp* s, const double* in) {
   if (!s || !in) return fail(IPMZ_ERR_INVALID, "bad arguments");
   HIP_OK(hipSetDevice(s->ctx->device));
+  const std::vector<double> v = state_in(s, in);
   for (int i = 0; i < s->B; ++i)
-    HIP_OK(hipMemcpyAsync(s->hq[i].v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
+    HIP_OK(hipMemcpyAsync(s->hq[i].v[0], v.data(), s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
   HIP_OK(qp_evaluate(s->qb, s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   s->loaded = true;
@@ -1444,7 +1513,8 @@ int ipmz_batch_set_state(ipmz_qp* s, int index, const double* in) {
   if (rc) return rc;
   if (!in) return fail(IPMZ_ERR_INVALID, "null state");
   HIP_OK(hipSetDevice(s->ctx->device));
-  HIP_OK(hipMemcpyAsync(s->hq[index].v[0], in, s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
+  const std::vector<double> v = state_in(s, in);
+  HIP_OK(hipMemcpyAsync(s->hq[index].v[0], v.data(), s->state_len * 8, hipMemcpyHostToDevice, s->ctx->stream));
   HIP_OK(qp_evaluate(s->qb, s->ctx->stream));
   HIP_OK(hipStreamSynchronize(s->ctx->stream));
   return IPMZ_OK;

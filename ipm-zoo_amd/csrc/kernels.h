@@ -187,6 +187,11 @@ struct QPDev {
   // Lower / Upper halves of Settings::variable_bounds and ::inequalities
   int slacks, vlo, vup, alo, aup;
   int naive;  // InequalityHandling::NaiveSlacks: no s / lambda_A; lambda_g, lambda_h are KKT rows
+  // EqualityHandling::SlackedSlacks: the p equality rows run as inequality
+  // rows with l = u = d (m = m_usr + p_usr, p = 0 inside the step; the
+  // formulas are the same, formulations.txt), t starting at 1
+  // (EnvironmentBuilder.cpp: s_A_eq = 1).  m_usr / p_usr: the data's rows.
+  int eqss, m_usr, p_usr;
   int mk;     // KKT rows of the inequalities: m, or 2 m (NaiveSlacks); N = n + mk + p
   // problem data (row-major, ld = ldn)
   const double *Q, *c, *A, *lA, *uA, *C, *d, *lx, *ux;

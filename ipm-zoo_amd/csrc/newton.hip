@@ -93,7 +93,7 @@ __global__ void k_gen_Q(const QPDev* __restrict__ qs, uint64_t seed0) {
 }
 __global__ void k_gen_rect(const QPDev* __restrict__ qs, uint64_t seed0, int which) {
   const QPDev& q = qs[blockIdx.y];
-  const int n = q.n, rows = which ? q.p : q.m;
+  const int n = q.n, rows = which ? q.p_usr : q.m_usr;
   const int64_t ld = q.ldn;
   const uint64_t seed = seed0 + blockIdx.y, tag = which ? TAG_C_EQ : TAG_A;
   double* M = const_cast<double*>(which ? q.C : q.A);
@@ -106,7 +106,7 @@ __global__ void k_gen_rect(const QPDev* __restrict__ qs, uint64_t seed0, int whi
 }
 __global__ void k_gen_vec(const QPDev* __restrict__ qs, uint64_t seed0) {
   const QPDev& q = qs[blockIdx.y];
-  const int n = q.n, m = q.m, p = q.p;
+  const int n = q.n, m = q.m_usr, p = q.p_usr;
   const uint64_t seed = seed0 + blockIdx.y;
   double *c = const_cast<double*>(q.c), *lA = const_cast<double*>(q.lA), *uA = const_cast<double*>(q.uA);
   double *d = const_cast<double*>(q.d), *lx = const_cast<double*>(q.lx), *ux = const_cast<double*>(q.ux);
@@ -120,7 +120,10 @@ __global__ void k_gen_vec(const QPDev* __restrict__ qs, uint64_t seed0) {
     lA[t] = -1.0;
     uA[t] = 1.0;
   }
-  if (t < p) d[t] = (2.0 * ipmz_u01(seed, TAG_D, t, 0) - 1.0) * 0.1;
+  if (t < p) {
+    d[t] = (2.0 * ipmz_u01(seed, TAG_D, t, 0) - 1.0) * 0.1;
+    if (q.eqss) lA[m + t] = uA[m + t] = d[t];  // the equality rows as l = u = d
+  }
 }
 
 static inline int max3(int a, int b, int c) { return a > b ? (a > c ? a : c) : (b > c ? b : c); }
@@ -131,15 +134,15 @@ hipError_t qp_generate(const QPBatch& qb, uint64_t seed0, hipStream_t st) {
   const QPDev& h = qb.h;
   const int64_t gq = ((int64_t)h.n * h.n + NT - 1) / NT;
   hipLaunchKernelGGL(k_gen_Q, grid2(gq < 2048 ? gq : 2048, qb.B), dim3(NT), 0, st, qb.d, seed0);
-  if (h.m) {
-    const int64_t g = ((int64_t)h.m * h.n + NT - 1) / NT;
+  if (h.m_usr) {
+    const int64_t g = ((int64_t)h.m_usr * h.n + NT - 1) / NT;
     hipLaunchKernelGGL(k_gen_rect, grid2(g < 1024 ? g : 1024, qb.B), dim3(NT), 0, st, qb.d, seed0, 0);
   }
-  if (h.p) {
-    const int64_t g = ((int64_t)h.p * h.n + NT - 1) / NT;
+  if (h.p_usr) {
+    const int64_t g = ((int64_t)h.p_usr * h.n + NT - 1) / NT;
     hipLaunchKernelGGL(k_gen_rect, grid2(g < 1024 ? g : 1024, qb.B), dim3(NT), 0, st, qb.d, seed0, 1);
   }
-  const int mx = max3(h.n, h.m, h.p);
+  const int mx = max3(h.n, h.m_usr, h.p_usr);
   hipLaunchKernelGGL(k_gen_vec, grid2((mx + NT - 1) / NT, qb.B), dim3(NT), 0, st, qb.d, seed0);
   return hipGetLastError();
 }
@@ -159,7 +162,7 @@ __global__ void k_init_iterate(const QPDev* __restrict__ qs) {
   }
   if (t < q.m) {
     if (!q.naive) {
-      q.v[S][t] = 0.5 * (q.lA[t] + q.uA[t]);
+      q.v[S][t] = (q.eqss && t >= q.m_usr) ? 1.0 : 0.5 * (q.lA[t] + q.uA[t]);  // t = 1 (EnvironmentBuilder.cpp)
       q.v[LA][t] = 1.0;
     }
     if (q.alo) q.v[LG][t] = 1.0;

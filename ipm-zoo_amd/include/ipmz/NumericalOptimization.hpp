@@ -112,7 +112,8 @@ enum class EqualityHandling {
   Regularization = IPMZ_EQ_REGULARIZATION,
   None = IPMZ_EQ_NONE,
   PenaltyFunction = IPMZ_EQ_PENALTY,
-  PenaltyFunctionWithExtraDual = IPMZ_EQ_PENALTY_EXTRA_DUAL  // the same Newton system (SymbolicOptimization.cpp:364-366)
+  PenaltyFunctionWithExtraDual = IPMZ_EQ_PENALTY_EXTRA_DUAL,  // the same Newton system (SymbolicOptimization.cpp:364-366)
+  SlackedSlacks = IPMZ_EQ_SLACKED_SLACKS
 };
 
 // Settings::Bounds and Settings::InequalityHandling (SymbolicOptimization.h:

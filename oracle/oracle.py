@@ -281,3 +281,70 @@ class OracleQP:
             out[s] = flat[off:off + k]
             off += k
         return out
+
+
+def eqss_merge(qp):
+    """EqualityHandling::SlackedSlacks restated as inequality rows: C x - t = 0,
+    d <= t <= d, i.e. A' = [A; C], l' = [l_A; d], u' = [u_A; d], p' = 0
+    (SymbolicOptimization.cpp:150-161 against 108-125; the two blocks' formulas
+    are the same with l_A = u_A = d, tests/test_oracle_formulations.py)."""
+    n, m, p = qp["n"], qp["m"], qp["p"]
+    return dict(qp, m=m + p, p=0, A=np.vstack([qp["A"], qp["C"]]), lA=np.concatenate([qp["lA"], qp["d"]]),
+                uA=np.concatenate([qp["uA"], qp["d"]]), C=np.zeros((0, n)), d=np.zeros(0))
+
+
+class EqSlackedOracle:
+    """OracleQP over eqss_merge(qp), in the reference's variable order
+    (x, lambda_A, lambda_C, s, t, lambda_g, lambda_h, lambda_v, lambda_w,
+    lambda_y, lambda_z, g, h, v, w, y, z) and with t starting at 1
+    (EnvironmentBuilder.cpp:62), as capi.cpp's eqss_perm."""
+
+    def __init__(self, qp):
+        n, m, p = qp["n"], qp["m"], qp["p"]
+        self.qp = qp
+        self.o = OracleQP(eqss_merge(qp))
+        mp = m + p
+        perm = list(range(n + 2 * mp))  # x, [lambda_A lambda_C], [s t]
+        off = n + 2 * mp
+        for base in (off, off + 2 * mp + 2 * n):  # [lambda_g lambda_v][lambda_h lambda_w], then [g v][h w]
+            perm += list(range(base, base + m)) + list(range(base + mp, base + mp + m))
+            perm += list(range(base + m, base + mp)) + list(range(base + mp + m, base + 2 * mp))
+            if base == off:
+                perm += list(range(off + 2 * mp, off + 2 * mp + 2 * n))  # lambda_y, lambda_z
+        perm += list(range(len(perm), self.o.L))  # y, z
+        self.perm = np.array(perm)
+        assert sorted(perm) == list(range(self.o.L))
+        self.N, self.L = self.o.N, self.o.L
+        self.sizes = dict(x=n, lambda_A=m, lambda_C=p, s=m, t=p, lambda_g=m, lambda_h=m, lambda_v=p, lambda_w=p,
+                          lambda_y=n, lambda_z=n, g=m, h=m, v=p, w=p, y=n, z=n)
+        self.order = [k for k in self.sizes if self.sizes[k]]
+        v = self.o.vars()
+        v[n + 2 * m + p: n + 2 * mp] = 1.0  # t
+        self.o.set_vars(v)
+
+    def vars(self):
+        return self.o.vars()[self.perm]
+
+    def daff(self):
+        return self.o.daff()[self.perm]
+
+    def dir(self):
+        return self.o.dir()[self.perm]
+
+    def set_vars(self, v):
+        w = np.empty(self.L)
+        w[self.perm] = v
+        self.o.set_vars(w)
+
+    def iterate(self):
+        return self.o.iterate()
+
+    def kkt(self):
+        return self.o.kkt()
+
+    def split(self, flat):
+        out, off = {}, 0
+        for s in self.order:
+            out[s] = flat[off:off + self.sizes[s]]
+            off += self.sizes[s]
+        return out

@@ -24,6 +24,7 @@
 //                                   iterations through the reference's own
 //                                   Optimizer private methods
 //                                   (Optimizer.cpp:127-219)
+//     [<ineq> <ineq bounds> <var bounds> [<p> <equality handling>]]
 //   component_eq <dir> <n> <m> <p> <seed> <tag>
 //                                   C3 structure (Regularization equalities):
 //                                   reference Evaluation for every non-scalar
@@ -377,6 +378,37 @@ struct IterRecord {
   Mat vars, d_aff, d;
 };
 
+// The augmented lhs as get_as_matrix_ (Optimizer.cpp:387-391) builds it, with
+// the scalar blocks the reference's evaluate_matrix asserts on
+// (Evaluation.cpp:57-60) expanded here: a scalar diagonal block -> s*I, a
+// scalar off-diagonal block must be 0 (EqualityHandling::SlackedSlacks has a
+// zero lambda_A / lambda_C block).  Matrix blocks are the reference's own.
+static Mat augmented_kkt(NO::Optimizer& opt) {
+  const auto& lhs = opt.augmented_system_.lhs;
+  const auto& vars = opt.augmented_system_.variables;
+  const size_t nb = lhs.size();
+  std::vector<size_t> off(nb + 1, 0);
+  for (size_t i = 0; i < nb; ++i) off[i + 1] = off[i] + opt.vector_sizes_.at(vars[i]);
+  Mat K(off[nb], Vec(off[nb], 0.0));
+  for (size_t bi = 0; bi < nb; ++bi)
+    for (size_t bj = 0; bj < nb; ++bj) {
+      const auto val = NO::Evaluation::evaluate(lhs[bi][bj], opt.env_);
+      if (std::holds_alternative<double>(val)) {
+        const double sv = std::get<double>(val);
+        if (bi == bj) {
+          for (size_t k = off[bi]; k < off[bi + 1]; ++k) K[k][k] = sv;
+        } else if (sv != 0.0) {
+          throw std::runtime_error("non-zero scalar off-diagonal block");
+        }
+        continue;
+      }
+      const Mat M = NO::Evaluation::evaluate_matrix(lhs[bi][bj], opt.env_);
+      for (size_t a = 0; a < M.size(); ++a)
+        for (size_t b = 0; b < M[a].size(); ++b) K[off[bi] + a][off[bj] + b] = M[a][b];
+    }
+  return K;
+}
+
 static IterRecord reference_iteration(NO::Optimizer& opt) {
   IterRecord r{};
   auto& env = opt.env_;
@@ -385,7 +417,7 @@ static IterRecord reference_iteration(NO::Optimizer& opt) {
   r.f = NO::Evaluation::evaluate_scalar(opt.objective_, env);
   r.res = opt.get_residual_norm_(full_rhs);
   r.mu = opt.get_mu_(full_rhs);
-  r.kkt = opt.get_as_matrix_(opt.augmented_system_.lhs);
+  r.kkt = augmented_kkt(opt);
   auto [L, D] = NO::LinearSolvers::ldlt_decomposition(r.kkt);
   r.D = D;
   env.at(oe.mu) = NO::Evaluation::val_scalar(0.0);
@@ -435,18 +467,20 @@ static IterRecord reference_iteration(NO::Optimizer& opt) {
 
 static int mode_newton(const std::string& dir, size_t n, size_t m, uint64_t seed, int iters, const std::string& tag,
                        const std::string& ineq = "SlackedSlacks", const std::string& ineq_bounds = "",
-                       const std::string& var_bounds = "Both") {
-  const QP q = make_qp(n, m, 0, seed);
+                       const std::string& var_bounds = "Both", size_t p = 0, const std::string& eq = "none") {
+  const QP q = make_qp(n, m, p, seed);
   NO::Data data;
   data.Q = q.Q;
   data.c = q.c;
   data.A_ineq = q.A;
   data.l_A_ineq = q.lA;
   data.u_A_ineq = q.uA;
+  data.A_eq = q.C;
+  data.b_eq = q.d;
   data.l_x = q.lx;
   data.u_x = q.ux;
   const SO::VariableNames names;
-  SO::Settings s = settings_from(ineq, "none", m > 0);
+  SO::Settings s = settings_from(ineq, eq, m > 0);
   if (!ineq_bounds.empty()) s.inequalities = bounds_from(ineq_bounds);
   s.variable_bounds = bounds_from(var_bounds);
   const auto oe = SO::get_optimization_expressions(names);
@@ -569,6 +603,9 @@ int main(int argc, char** argv) {
     if (mode == "newton" && argc == 11)  // + <ineq handling> <inequality bounds> <variable bounds>
       return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
                          argv[7], argv[8], argv[9], argv[10]);
+    if (mode == "newton" && argc == 13)  // + <p> <equality handling>
+      return mode_newton(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoull(argv[5]), std::stoi(argv[6]),
+                         argv[7], argv[8], argv[9], argv[10], std::stoul(argv[11]), argv[12]);
     if (mode == "component_eq" && argc == 8)
       return mode_component_eq(dir, std::stoul(argv[3]), std::stoul(argv[4]), std::stoul(argv[5]),
                                std::stoull(argv[6]), argv[7]);

@@ -59,6 +59,15 @@ CASES = [
     # InequalityHandling::Slacks: runs but stagnates (SURVEY.md App. C.1 corrector defect); 12 iterations
     ("newton", 48, 16, 7, 12, "Slacks", "Both", "Both", "sl"),
     ("newton", 48, 0, 7, 12, "Slacks", "None", "Both", "slbox"),
+    # equality rows (p = 8) and the other handlings (+ <p> <equality handling>); the
+    # harness expands the scalar blocks the reference's evaluate_matrix asserts on
+    # (-delta^2 I, the zero lambda_A / lambda_C block), every other value is the
+    # reference's own
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Both", 8, "Regularization", "reg"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Both", 8, "PenaltyFunction", "pen"),
+    ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Both", 8, "SlackedSlacks", "eqss"),
+    ("newton", 48, 16, 7, 100, "NaiveSlacks", "Both", "Both", 0, "none", "naive"),
+    ("newton", 48, 16, 7, 100, "NaiveSlacks", "Both", "Both", 8, "Regularization", "naivereg"),
 ]
 
 
@@ -68,8 +77,9 @@ def main():
     subprocess.run([HARNESS, "formulation", HERE], check=True)
     for case in CASES:
         mode, tag = case[0], case[-1]
-        if mode == "newton" and len(case) == 9:  # harness order: ... <iters> <tag> <ineq> <ineq bounds> <var bounds>
-            args = [HARNESS, mode, HERE] + [str(a) for a in case[1:5]] + [tag] + list(case[5:8])
+        if mode == "newton" and len(case) in (9, 11):
+            # harness order: ... <iters> <tag> <ineq> <ineq bounds> <var bounds> [<p> <equality handling>]
+            args = [HARNESS, mode, HERE] + [str(a) for a in case[1:5]] + [tag] + [str(a) for a in case[5:-1]]
         else:
             args = [HARNESS, mode, HERE] + [str(a) for a in case[1:-1]] + [tag]
         subprocess.run(args, check=True)

@@ -2,8 +2,9 @@
 28-64): one-sided / absent variable and inequality bounds and
 InequalityHandling::Slacks (with the reference's corrector defect), through
 the C ABI, against the reference's own Newton traces (tests/golden/
-{vlo,vup,vnone,alo,aup,vlo0,sl,slbox}_*, made by tests/golden/make_golden.py)
-and against the oracle at blocked-factor sizes.
+{vlo,vup,vnone,alo,aup,vlo0,sl,slbox}_*, and for the equality handlings and
+NaiveSlacks {reg,pen,naive,naivereg,eqss}_*, made by tests/golden/
+make_golden.py) and against the oracle at blocked-factor sizes.
 
 Tolerances as tests/test_gpu_parity.py: element-wise formulas (initial
 iterate, KKT assembly) bit-identical; directions 1e-9 relative per block and
@@ -135,11 +136,57 @@ def test_formulation_rejected(ctx, kw, msg):
         I.Optimizer(16, 4, 0, ctx, **kw)
 
 
-# InequalityHandling::NaiveSlacks: the reference's symbolic engine defines it
-# (tests/golden/formulations.txt) but its evaluator asserts on the zero
-# (lambda_g, lambda_h) block (Evaluation.cpp:57-60), so there is no reference
-# trace: the GPU path is checked against the oracle's restatement (parity
-# pinned to the reference's formulas only, tests/test_oracle_formulations.py)
+# Equality rows and the other handlings against the reference's own Newton
+# iterations (make_golden.py "reg" = C3's structure, "pen", "naive",
+# "naivereg", "eqss"; the harness expands only the scalar blocks the
+# reference's evaluate_matrix asserts on).  From the reference's iterate each
+# iteration: scalars, both directions per block, the update.
+EQ_CASES = [
+    ("reg", 8, dict(), lambda qp: oracle.OracleQP(qp)),
+    ("pen", 8, dict(equality_handling=I.EQ_PENALTY), lambda qp: oracle.OracleQP(qp, eq_penalty=True)),
+    ("pex", 8, dict(equality_handling=I.EQ_PENALTY_EXTRA_DUAL), lambda qp: oracle.OracleQP(qp, eq_penalty=True)),
+    ("naive", 0, dict(inequality_handling=I.INEQ_NAIVE_SLACKS),
+     lambda qp: oracle.OracleQP(qp, form=oracle.Form(naive=True))),
+    ("naivereg", 8, dict(inequality_handling=I.INEQ_NAIVE_SLACKS),
+     lambda qp: oracle.OracleQP(qp, form=oracle.Form(naive=True))),
+    ("eqss", 8, dict(equality_handling=I.EQ_SLACKED_SLACKS), oracle.EqSlackedOracle),
+]
+
+
+@pytest.mark.parametrize("tag,p,kw,mk", EQ_CASES, ids=[c[0] for c in EQ_CASES])
+def test_equality_golden_trace(ctx, tag, p, kw, mk):
+    n, m = 48, 16
+    fx = "pen" if tag == "pex" else tag  # PenaltyFunctionWithExtraDual: the same Newton system
+    names, rows, conv = trace(fx)
+    o = mk(oracle.gen_qp(n, m, p, 7))
+    g = I.Optimizer(n, m, p, ctx, **kw)
+    g.generate(7)
+    assert g.state_len == len(load(f"{fx}_it0_vars.bin")) and g.N == o.N
+    assert np.array_equal(g.vars(), load(f"{fx}_it0_vars.bin"))
+    assert np.array_equal(g.kkt(), np.tril(sym_from_lower(load(f"{fx}_it0_kkt.bin"), o.N)))
+    for it, ref in enumerate(rows):
+        g.set_vars(load(f"{fx}_it{it}_vars.bin"))
+        s0 = g.scalars()
+        for k in ("f", "res", "mu"):
+            assert abs(s0[k] - ref[k]) <= 1e-12 * max(1.0, abs(ref[k])), (tag, it, k, s0[k], ref[k])
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - ref[k]) <= 1e-9 * max(1.0, abs(ref[k])), (tag, it, k, s1[k], ref[k])
+        for got, which in ((g.daff(), "daff"), (g.dir(), "d")):
+            so, sg = o.split(load(f"{fx}_it{it}_{which}.bin")), o.split(got)
+            for s in o.order:
+                _close(sg[s], so[s], (tag, it, which, s))
+            assert np.abs(sg["x"] - so["x"]).max() < DX_TOL, (tag, it, which)
+        if it + 1 < len(rows):
+            _close(g.vars(), load(f"{fx}_it{it + 1}_vars.bin"), (tag, it, "update"))
+    g.set_vars(load(f"{fx}_it{len(rows) - 1}_vars.bin"))
+    g.step()
+    assert g.scalars()["converged"] == 1.0
+
+
+# InequalityHandling::NaiveSlacks at blocked-factor sizes against the oracle
+# (pinned above to the reference's iterations at n = 48)
 @pytest.mark.parametrize("n,m,p,seed", [(48, 16, 6, 7), (300, 70, 30, 3)])
 def test_naive_slacks_vs_oracle(ctx, n, m, p, seed):
     form = oracle.Form(naive=True)
@@ -187,3 +234,95 @@ def test_naive_slacks_batch_and_solve(ctx):
     bt.step()
     with pytest.raises(I.IpmzError):
         g.set_reduction(I.REDUCTION_NORMAL)
+
+
+# EqualityHandling::SlackedSlacks at blocked-factor sizes, in a batch, through
+# the normal equations, and its state permutation
+def _eqss_iterations(g, o, iters, label):
+    for it in range(iters):
+        s0 = g.scalars()
+        done, rec = o.iterate()
+        for k in ("f", "res", "mu"):
+            assert abs(s0[k] - rec[k]) <= 1e-12 * max(1.0, abs(rec[k])), (label, it, k)
+        if done:
+            assert s0["converged"] == 1.0
+            return
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (label, it, k, s1[k], rec[k])
+        for which, (a, b) in enumerate(((g.daff(), o.daff()), (g.dir(), o.dir()))):
+            sa, sb = o.split(a), o.split(b)
+            for s in o.order:
+                _close(sa[s], sb[s], (label, it, which, s))
+            assert np.abs(sa["x"] - sb["x"]).max() < DX_TOL, (label, it, which)
+        g.set_vars(o.vars())
+
+
+@pytest.mark.parametrize("n,m,p,seed", [(300, 70, 30, 3), (200, 0, 40, 4)])
+def test_eq_slacked_slacks_vs_oracle(ctx, n, m, p, seed):
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, seed))
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_SLACKED_SLACKS)
+    g.generate(seed)
+    assert g.N == n + m + p == o.N and g.state_len == o.L
+    assert np.array_equal(g.vars(), o.vars())
+    assert np.array_equal(g.kkt(), np.tril(o.kkt()))
+    _eqss_iterations(g, o, 5, "augmented")
+
+
+def test_eq_slacked_slacks_normal_equations(ctx):
+    n, m, p, seed = 160, 40, 24, 9
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, seed))
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_SLACKED_SLACKS)
+    g.generate(seed)
+    g.set_reduction(I.REDUCTION_NORMAL)
+    _eqss_iterations(g, o, 4, "normal")
+
+
+def test_eq_slacked_slacks_state_order(ctx):
+    n, m, p = 40, 6, 5
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_SLACKED_SLACKS)
+    g.generate(2)
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, 2))
+    sp = o.split(g.vars())
+    assert np.all(sp["t"] == 1.0) and np.all(sp["lambda_v"] == 1.0) and np.all(sp["w"] == 1.0)
+    v = np.arange(g.state_len, dtype=np.float64) + 0.5  # set -> get is the identity in the reference's order
+    g.set_vars(v)
+    assert np.array_equal(g.vars(), v)
+
+
+def test_eq_slacked_slacks_batch_and_solve(ctx):
+    n, m, p, B = 64, 16, 8, 3
+    kw = dict(equality_handling=I.EQ_SLACKED_SLACKS)
+    bt = I.Batch(n, m, p, B, ctx, **kw)
+    bt.generate(5)
+    g = I.Optimizer(n, m, p, ctx, **kw)
+    g.generate(6)  # QP 1 of the batch
+    assert np.array_equal(bt.state(1), g.vars())
+    bt.step()
+    g.step()
+    ref = bt.batch_scalars()
+    sc = g.scalars()
+    for k in ("alpha_aff", "alpha", "mu_aff"):
+        assert abs(ref[1, I.SC[k]] - sc[k]) <= 1e-12 * max(1.0, abs(sc[k])), k
+    assert np.abs(bt.state(1) - g.vars()).max() < 1e-12
+    g.generate(6)
+    iters, tr = g.solve(100)
+    assert tr[-1]["converged"] == 1.0
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, 6))
+    for it in range(100):
+        done, _ = o.iterate()
+        if done:
+            break
+    assert iters == it
+    sg = o.split(g.vars())
+    assert np.abs(sg["x"] - o.split(o.vars())["x"]).max() < 1e-8
+    qp = oracle.gen_qp(n, m, p, 6)
+    assert np.abs(qp["C"] @ sg["x"] - qp["d"]).max() < 1e-7  # C x = d at the optimum
+
+
+@pytest.mark.parametrize("kw", [dict(inequality_handling=1), dict(inequality_handling=2),
+                                dict(inequality_bounds=1)])
+def test_eq_slacked_slacks_rejected(ctx, kw):
+    with pytest.raises(I.IpmzError):
+        I.Optimizer(16, 4, 2, ctx, equality_handling=I.EQ_SLACKED_SLACKS, **kw)

@@ -1,12 +1,11 @@
-"""InequalityHandling::NaiveSlacks in the CPU oracle (§8f row f4).
-
-The reference's symbolic engine defines the formulation (its Newton system,
-shorthand and augmented system are tests/golden/formulations.txt), but its
-evaluator asserts on the zero (lambda_g, lambda_h) block (Evaluation.cpp:
-57-60): no reference trace exists, so the restatement is pinned to the
-reference's own formulas (the layout and blocks below) and checked for
-self-consistency (the Newton direction solves the Newton system; the
-optimum is the SlackedSlacks one)."""
+"""InequalityHandling::NaiveSlacks and EqualityHandling::SlackedSlacks in
+the CPU oracle (§8f row f4): the formulations against the reference's own
+formulas (tests/golden/formulations.txt) and for self-consistency (the
+Newton direction solves the Newton system; the optimum is the SlackedSlacks
+one).  Both are also pinned to the reference's Newton iterations
+(tests/test_oracle_golden.py "naive", "naivereg", "eqss"), made by a harness
+that expands the zero (lambda_g, lambda_h) / (lambda_A, lambda_C) block the
+reference's evaluator asserts on (Evaluation.cpp:57-60)."""
 import os
 
 import numpy as np
@@ -80,3 +79,47 @@ def test_naive_slacks_reaches_the_slacked_slacks_optimum():
         assert done == 1
         out[naive] = o.split(o.vars())["x"]
     assert np.abs(out[True] - out[False]).max() < 1e-8
+
+
+
+def _rename_a_to_c(t):
+    """The lambda_A / s / g / h block's text with the lambda_C / t / v / w names."""
+    import re
+    for a, b in ((r"\lambda_{A}", r"\lambda_{C}"), (r"\lambda_{g}", r"\lambda_{v}"), (r"\lambda_{h}", r"\lambda_{w}"),
+                 (r"\Lambda_{g}", r"\Lambda_{v}"), (r"\Lambda_{h}", r"\Lambda_{w}"), ("r_{s}", "r_{t}"),
+                 ("r_{g}", "r_{v}"), ("r_{h}", "r_{w}"), ("e_{A}", "e_{C}"), ("l_A", "d"), ("u_A", "d")):
+        t = t.replace(a, b)
+    t = re.sub(r"\bG\b", "V", t)
+    t = re.sub(r"\bH\b", "W", t)
+    t = re.sub(r"\bA\b", "C", t)
+    t = re.sub(r"(?<![_{\\])\bs\b", "t", t)
+    t = re.sub(r"(?<![_{\\])\bg\b", "v", t)
+    t = re.sub(r"(?<![_{\\])\bh\b", "w", t)
+    return t
+
+
+def test_equality_slacked_slacks_is_the_inequality_block_with_d():
+    # EqualityHandling::SlackedSlacks (SymbolicOptimization.cpp:150-161): every
+    # lambda_C / t / v / w formula is the lambda_A / s / g / h one renamed, with
+    # l_A = u_A = d -- what oracle.eqss_merge and the GPU's [A; C] rows rely on
+    sec = _section("=== inequality_handling=SlackedSlacks equalities=SlackedSlacks inequalities=Both")
+    defs = {}
+    for ln in sec.splitlines():
+        if " := " in ln:
+            k, v = ln.strip().split(" := ")
+            defs.setdefault(k, v)
+    pairs = [(r"r_{\lambda_{A}}", r"r_{\lambda_{C}}"), ("r_{s}", "r_{t}"), (r"r_{\lambda_{g}}", r"r_{\lambda_{v}}"),
+             (r"r_{\lambda_{h}}", r"r_{\lambda_{w}}"), ("r_{g}", "r_{v}"), ("r_{h}", "r_{w}"),
+             (r"\Delta s", r"\Delta t"), (r"\Delta g", r"\Delta v"), (r"\Delta h", r"\Delta w"),
+             (r"\Delta \lambda_{g}", r"\Delta \lambda_{v}"), (r"\Delta \lambda_{h}", r"\Delta \lambda_{w}")]
+    for a, c in pairs:
+        got, want = defs[c], _rename_a_to_c(defs[a])
+        if got != want:  # (v + d - t) vs (l_A + g - s): the same sum with the operands commuted
+            assert sorted(got.strip("()").replace(" - ", " + -").split(" + ")) == \
+                sorted(want.strip("()").replace(" - ", " + -").split(" + ")), (c, got, want)
+    aug = sec[sec.index("-- augmented system"):sec.index("-- normal equations")]
+    rows = [ln.strip().strip("|").split(" | ") for ln in aug.splitlines() if ln.strip().startswith("|")]
+    assert rows[2][2].strip() == _rename_a_to_c(rows[1][1].strip())
+    assert rows[1][2].strip() == "0" and rows[2][1].strip() == "0"
+    rhs = [ln.strip() for ln in aug.split("rhs:")[1].split("delta_definitions:")[0].splitlines() if ln.strip()]
+    assert rhs[2] == _rename_a_to_c(rhs[1])
