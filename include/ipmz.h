@@ -161,12 +161,19 @@ int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld,
  * LinearSolvers.cpp:76-207) and overwriting_solve_bunch_kaufman
  * (LinearSolvers.h:28-31, :209-318); never called by the reference's
  * Optimizer (solve_indefinite_ is ASSERT(false), Optimizer.cpp:75).
- * Device: A row-major (lower triangle factored in place), N <= 4096; ipiv:
+ * Device: A row-major (lower triangle factored in place), any N; ipiv:
  * device int[N] in the reference's convention (>= 0: 1x1 pivot with that
  * interchange; < 0: -kp on both rows of a 2x2 pivot).  fix_kp = 0 keeps the
  * reference's kp = 0 for a second all-zero column (LinearSolvers.cpp:111-116),
  * 1 records kp = k.  Returns 0, or 1 + the first all-zero column. */
 int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp);
+/* Same, with the kernel chosen: IPMZ_BK_AUTO (the whole-device factor from
+ * N = 768 up), IPMZ_BK_WORKGROUP (one workgroup, N <= 4096), IPMZ_BK_GRID
+ * (every CU, a grid barrier per pivot step).  Both are bitwise the reference. */
+#define IPMZ_BK_AUTO 0
+#define IPMZ_BK_WORKGROUP 1
+#define IPMZ_BK_GRID 2
+int ipmz_bk_factor_ex(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp, int algo);
 int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* ipiv, double* b);
 /* Host signatures of the reference (value semantics, reference pivoting
  * including its kp = 0 defect): F = A with the lower triangle factored. */

@@ -21,6 +21,7 @@
 // fix_kp = 1 records kp = k (LAPACK's choice).
 #include "common.h"
 #include "kernels.h"
+#include "sync.h"
 
 namespace ipmz {
 
@@ -316,6 +317,381 @@ __global__ __launch_bounds__(BKT) void k_bk_solve(const double* __restrict__ Lb,
       k -= 2;
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// The same factorization over the whole device (one matrix, N beyond one
+// workgroup's reach -- EqualityHandling::None at headline size).
+//
+// The pivot choice is sequential in k and the trailing update of step k is
+// all of the work, HBM-bound (the reference's right-looking rank-1 / rank-2
+// update touches the trailing triangle once per step, (N-k)^2/2 elements
+// read and written).  G workgroups (one per CU) stay resident for the whole
+// factor and meet at a grid barrier once per step (twice when the row search
+// runs).  Ownership is fixed: row i belongs to workgroup i mod G and, inside
+// it, column j to thread j mod 1024, so every element of the matrix is only
+// ever touched by one thread -- the bulk update needs no cross-XCD coherence
+// at all.  What crosses workgroups goes through small write-through buffers:
+//   * the next two pivot columns, staged by their owning threads during the
+//     update (colbuf, two parities), with each workgroup's (max, argmax) of
+//     the next pivot column (so the column search costs no extra pass);
+//   * the row search's row i_max and column i_max (prow, pcol) with their
+//     per-workgroup maxima;
+// and the symmetric interchange is never applied as a pass of its own: the
+// pivot columns after the interchange are read through the swap map from
+// those buffers, and each owner rewrites the few interchanged elements of its
+// own rows while updating them.  Arithmetic is element by element the
+// reference's (same expressions, same operand order, -ffp-contract=off), so
+// F and ipiv are bitwise those of LinearSolvers.cpp:76-207, as for the
+// one-workgroup kernel above.
+namespace bkg {
+constexpr int T = 1024;  // threads per workgroup: column j -> thread j mod T
+static_assert(T == BKT, "block_argmax reduces over BKT threads");
+
+struct Layout {
+  int64_t ctrl, colbuf, cpv, cpi, rp1, rp2, prow, pcol, total;
+};
+IPMZ_HOST_DEVICE Layout layout(int n, int G) {
+  Layout l;
+  int64_t o = 0;
+  auto take = [&](int64_t bytes) {
+    const int64_t at = o;
+    o += (bytes + 255) / 256 * 256;
+    return at;
+  };
+  l.ctrl = take(256);
+  l.colbuf = take(4 * (int64_t)n * 8);  // [parity][2 columns][n]
+  l.cpv = take(2 * (int64_t)G * 8);
+  l.cpi = take(2 * (int64_t)G * 4);
+  l.rp1 = take((int64_t)G * 8);
+  l.rp2 = take((int64_t)G * 8);
+  l.prow = take((int64_t)n * 8);
+  l.pcol = take((int64_t)n * 8);
+  l.total = o;
+  return l;
+}
+
+// One pass: mode 0 stages columns lo, lo+1 only; mode 1 / 2 is the update
+// of a 1x1 / 2x2 pivot at column k (lo = k + mode), with the interchange of
+// rows / columns kk = lo - 1 and kp when swap.
+struct Pass {
+  int mode, k, lo, kp;
+  bool swap;
+  double r, d11, d22, d21;
+  const double *ck0, *ck1, *prow, *pcol;  // staged pre-interchange columns k, k+1; row / column i_max
+  double *nb0, *nb1;                      // staging out: columns lo, lo+1
+  double* cpv;                            // this workgroup's (max, argmax) slot of column lo
+  int* cpi;
+};
+// the pivot columns AFTER the interchange (LinearSolvers.cpp:137-164 applied
+// to the staged pre-interchange data)
+__device__ __forceinline__ double c0v(const Pass& P, int i) {
+  if (P.mode == 1) {
+    if (!P.swap) return ld_sc1(P.ck0 + i);
+    if (i == P.k) return ld_sc1(P.prow + P.kp);  // a(kp, kp)
+    if (i < P.kp) return ld_sc1(P.prow + i);     // a(kp, i)
+    if (i == P.kp) return ld_sc1(P.prow + P.k);  // a(kp, k) stays
+    return ld_sc1(P.pcol + i);                   // a(i, kp)
+  }
+  if (P.swap && i == P.k + 1) return ld_sc1(P.prow + P.k);  // a(kk, k) <-> a(kp, k)
+  if (P.swap && i == P.kp) return ld_sc1(P.ck0 + P.k + 1);
+  return ld_sc1(P.ck0 + i);
+}
+__device__ __forceinline__ double c1v(const Pass& P, int i) {  // mode 2, i >= k + 1
+  if (!P.swap) return ld_sc1(P.ck1 + i);
+  if (i == P.k + 1) return ld_sc1(P.prow + P.kp);
+  if (i < P.kp) return ld_sc1(P.prow + i);
+  if (i == P.kp) return ld_sc1(P.prow + P.k + 1);  // a(kp, kk) stays
+  return ld_sc1(P.pcol + i);
+}
+
+__device__ void pass(double* __restrict__ A, int64_t ld, int n, const Pass& P, double* rc0, double* rc1,
+                     double* rsub, int g, int G, int nq) {
+  const int tid = threadIdx.x, lo = P.lo;
+  const int q_lo = lo <= g ? 0 : (lo - g + G - 1) / G;  // first owned row >= lo
+  if (P.mode) {
+    const double* ckS = P.mode == 1 ? P.ck0 : P.ck1;
+    for (int q = q_lo + tid; q < nq; q += T) {
+      const int i = g + q * G;
+      rc0[q] = c0v(P, i);
+      if (P.mode == 2) rc1[q] = c1v(P, i);
+      if (P.swap && i > P.kp) rsub[q] = ld_sc1(ckS + i);  // a(i, kp) <- a(i, kk)
+    }
+  }
+  __syncthreads();
+  if (P.mode) {
+    // the interchanged elements outside the update range, and the L column(s)
+    // (LinearSolvers.cpp:176-178, 199-202) -- by the owners of column k, k+1
+    const int k = P.k;
+    if (tid == (k & (T - 1))) {
+      if (P.mode == 1 && P.swap && k % G == g) A[(int64_t)k * ld + k] = ld_sc1(P.prow + P.kp);
+      if (P.mode == 2 && P.swap && (k + 1) % G == g) A[(int64_t)(k + 1) * ld + k] = ld_sc1(P.prow + k);
+      for (int q = q_lo; q < nq; ++q) {
+        const int i = g + q * G;
+        A[(int64_t)i * ld + k] = P.mode == 1 ? rc0[q] * P.r : P.d21 * (P.d11 * rc0[q] - rc1[q]);
+      }
+    }
+    if (P.mode == 2 && tid == ((k + 1) & (T - 1))) {
+      if (P.swap && (k + 1) % G == g) A[(int64_t)(k + 1) * ld + k + 1] = ld_sc1(P.prow + P.kp);
+      for (int q = q_lo; q < nq; ++q) {
+        const int i = g + q * G;
+        A[(int64_t)i * ld + k + 1] = P.d21 * (P.d22 * rc1[q] - rc0[q]);
+      }
+    }
+  }
+  const bool kprow = P.swap && P.kp % G == g;
+  double mx = 0.0;
+  int mi = 0x7fffffff;
+  for (int j = lo + (((tid - lo) % T) + T) % T; j < n; j += T) {
+    if (!P.mode && j > lo + 1) break;
+    double w0 = 0.0, w1 = 0.0, subj = 0.0;
+    if (P.mode == 1) {
+      w0 = P.r * c0v(P, j);
+    } else if (P.mode == 2) {
+      const double a0 = c0v(P, j), a1 = c1v(P, j);
+      w0 = P.d21 * (P.d11 * a0 - a1);
+      w1 = P.d21 * (P.d22 * a1 - a0);
+    }
+    if (kprow && j <= P.kp) subj = ld_sc1((P.mode == 1 ? P.ck0 : P.ck1) + (j < P.kp ? j : lo - 1));
+    const bool stage0 = j == lo, stage1 = j == lo + 1;
+    int q = j <= g ? 0 : (j - g + G - 1) / G;
+    // rows in groups of 4: the loads of a group are in flight together
+    for (; q < nq; q += 4) {
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int i = g + (q + u) * G;
+        v[u] = q + u < nq ? A[(int64_t)i * ld + j] : 0.0;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (q + u >= nq) break;
+        const int i = g + (q + u) * G;
+        double x = v[u];
+        if (P.swap) {
+          if (i == P.kp && j <= P.kp) x = subj;
+          else if (i > P.kp && j == P.kp) x = rsub[q + u];
+        }
+        if (P.mode == 1) x = x - w0 * rc0[q + u];  // a(i,j) -= (r a(j,k)) a(i,k)
+        else if (P.mode == 2) x = x - (rc0[q + u] * w0 + rc1[q + u] * w1);
+        if (P.mode) A[(int64_t)i * ld + j] = x;
+        if (stage0) {
+          st_sc1(P.nb0 + i, x);
+          const double t = fabs(x);
+          if (i > lo && t > mx) {  // strictly greater, rows ascending: the first maximum
+            mx = t;
+            mi = i;
+          }
+        } else if (stage1) {
+          st_sc1(P.nb1 + i, x);
+        }
+      }
+    }
+  }
+  if (lo < n && tid == (lo & (T - 1))) {
+    st_sc1(P.cpv, mx);
+    st_sc1(P.cpi, mi);
+  }
+}
+
+// grid barrier: every wave drains its stores, one arrival per workgroup on a
+// monotonic counter, wait for target = (barrier number) x G.  A spin past
+// SPIN_TICKS (or another workgroup's) raises the sticky error word.
+__device__ __forceinline__ bool gbar(unsigned* cnt, unsigned* err, unsigned target, unsigned* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned ok = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (unsigned it = 0; ld_sc1(cnt) < target; ++it) {
+      if ((it & 255u) == 255u &&
+          (ld_sc1(err) != 0u || __builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS)) {
+        st_sc1(err, 1u);
+        ok = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+__device__ double block_fmax(double v, double* sv) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = wave_max(v);
+  __syncthreads();
+  if (lane == 0) sv[wave] = v;
+  __syncthreads();
+  double s = 0.0;
+  for (int w = 0; w < BKW; ++w) s = fmax(s, sv[w]);
+  return s;
+}
+}  // namespace bkg
+
+__global__ __launch_bounds__(bkg::T) void k_bk_grid(double* __restrict__ A, int64_t ld, int n,
+                                                     int* __restrict__ ipiv, int* __restrict__ infop, int fix_kp,
+                                                     char* __restrict__ ws) {
+  using namespace bkg;
+  extern __shared__ double rows[];  // rc0, rc1, rsub of the owned rows
+  __shared__ double sv[BKW];
+  __shared__ int si[BKW];
+  __shared__ unsigned s_ok;
+  const int G = gridDim.x, g = blockIdx.x, tid = threadIdx.x;
+  const Layout L = layout(n, G);
+  unsigned* ctrl = reinterpret_cast<unsigned*>(ws + L.ctrl);
+  double* colbuf = reinterpret_cast<double*>(ws + L.colbuf);
+  double* cpv = reinterpret_cast<double*>(ws + L.cpv);
+  int* cpi = reinterpret_cast<int*>(ws + L.cpi);
+  double* rp1 = reinterpret_cast<double*>(ws + L.rp1);
+  double* rp2 = reinterpret_cast<double*>(ws + L.rp2);
+  double* prow = reinterpret_cast<double*>(ws + L.prow);
+  double* pcol = reinterpret_cast<double*>(ws + L.pcol);
+  const int nq = g < n ? (n - g + G - 1) / G : 0;
+  double *rc0 = rows, *rc1 = rows + nq, *rsub = rows + 2 * nq;
+  const double alpha = 0x1.47e0f66afed07p-1;  // (1 + sqrt(17)) / 8, LinearSolvers.cpp:82
+  unsigned nbar = 0;
+  int par = 0;  // parity of the last staging pass
+  auto run = [&](Pass P) -> bool {
+    const int out = par ^ 1;
+    P.nb0 = colbuf + (2 * out) * (int64_t)n;
+    P.nb1 = colbuf + (2 * out + 1) * (int64_t)n;
+    P.cpv = cpv + out * G + g;
+    P.cpi = cpi + out * G + g;
+    pass(A, ld, n, P, rc0, rc1, rsub, g, G, nq);
+    par = out;
+    return gbar(ctrl, ctrl + 1, (++nbar) * (unsigned)G, &s_ok);
+  };
+  auto stage = [&](int lo) {
+    Pass P{};
+    P.mode = 0;
+    P.lo = lo;
+    return run(P);
+  };
+  int info = 0, ref_info = 0;
+  bool ok = stage(0);
+  for (int k = 0; ok && k < n;) {
+    const double* ck0 = colbuf + (2 * par) * (int64_t)n;
+    const double* ck1 = colbuf + (2 * par + 1) * (int64_t)n;
+    // ---- column search from the per-workgroup maxima (LinearSolvers.cpp:104-107)
+    double cmax = 0.0;
+    int imax = 0;
+    {
+      double v = 0.0;
+      int ix = 0x7fffffff;
+      if (tid < G) {
+        v = ld_sc1(cpv + par * G + tid);
+        ix = ld_sc1(cpi + par * G + tid);
+      }
+      block_argmax(v, ix, sv, si, cmax, imax);
+    }
+    const double akk = fabs(ld_sc1(ck0 + k));
+    int step = 1, kp = 0;
+    bool zero_col = false;
+    if (akk == 0.0 && cmax == 0.0) {
+      zero_col = true;
+      if (info == 0) info = k + 1;
+      if (ref_info == 0) {
+        ref_info = k;
+        kp = k;
+      } else if (fix_kp) {
+        kp = k;
+      }
+    } else if (akk >= alpha * cmax) {
+      kp = k;
+    } else {
+      // ---- row search (LinearSolvers.cpp:121-134): row i_max left of the
+      // diagonal (its owner) and column i_max below it (every owner), each
+      // published for the interchange
+      double r1 = 0.0, r2 = 0.0;
+      if (imax % G == g)
+        for (int j = k + (((tid - k) % T) + T) % T; j <= imax; j += T) {
+          const double x = A[(int64_t)imax * ld + j];
+          st_sc1(prow + j, x);
+          if (j < imax) r1 = fmax(r1, fabs(x));
+        }
+      if (tid == (imax & (T - 1))) {
+        const int q0 = imax < g ? 0 : (imax - g) / G + 1;  // owned rows > imax
+        for (int q = q0; q < nq; ++q) {
+          const int i = g + q * G;
+          const double x = A[(int64_t)i * ld + imax];
+          st_sc1(pcol + i, x);
+          r2 = fmax(r2, fabs(x));
+        }
+      }
+      r1 = block_fmax(r1, sv);
+      r2 = block_fmax(r2, sv);
+      if (tid == 0) {
+        st_sc1(rp1 + g, r1);
+        st_sc1(rp2 + g, r2);
+      }
+      ok = gbar(ctrl, ctrl + 1, (++nbar) * (unsigned)G, &s_ok);
+      if (!ok) break;
+      r1 = block_fmax(tid < G ? ld_sc1(rp1 + tid) : 0.0, sv);
+      r2 = block_fmax(tid < G ? ld_sc1(rp2 + tid) : 0.0, sv);
+      const double rmax = r1 < r2 ? r2 : r1;  // std::max
+      if (akk * rmax >= alpha * cmax * cmax) kp = k;
+      else if (fabs(ld_sc1(prow + imax)) >= alpha * rmax) kp = imax;
+      else {
+        kp = imax;
+        step = 2;
+      }
+    }
+    if (g == 0 && tid == 0) {
+      if (step == 1) ipiv[k] = kp;
+      else ipiv[k] = ipiv[k + 1] = -kp;
+    }
+    if (zero_col) {  // no interchange, no update: stage the next column
+      if (k + 1 < n) ok = stage(k + 1);
+      k += 1;
+      continue;
+    }
+    Pass P{};
+    P.mode = step;
+    P.k = k;
+    P.lo = k + step;
+    P.kp = kp;
+    P.swap = kp != k + step - 1;
+    P.ck0 = ck0;
+    P.ck1 = ck1;
+    P.prow = prow;
+    P.pcol = pcol;
+    if (step == 1) {
+      P.r = 1.0 / c0v(P, k);
+    } else {
+      const double d21 = c0v(P, k + 1);
+      const double d11 = c1v(P, k + 1) / d21;
+      const double d22 = c0v(P, k) / d21;
+      const double t = 1.0 / (d11 * d22 - 1.0);
+      P.d11 = d11;
+      P.d22 = d22;
+      P.d21 = t / d21;
+    }
+    ok = run(P);
+    k += step;
+  }
+  if (g == 0 && tid == 0) *infop = info;
+}
+
+size_t bk_grid_ws_bytes(int n) { return (size_t)bkg::layout(n, device_cus()).total; }
+
+hipError_t bk_factor_grid(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, void* ws,
+                          hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int G = device_cus();
+  const int nq = (n + G - 1) / G;
+  char* w = static_cast<char*>(ws);
+  hipError_t e = hipMemsetAsync(w + bkg::layout(n, G).ctrl, 0, 256, st);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_bk_grid, dim3(G), dim3(bkg::T), 3 * (size_t)nq * sizeof(double), st, A, ld, n, ipiv, info,
+                     fix_kp, w);
+  return hipGetLastError();
+}
+
+const unsigned* bk_grid_err_word(const void* ws, int n) {
+  return reinterpret_cast<const unsigned*>(static_cast<const char*>(ws) + bkg::layout(n, device_cus()).ctrl) + 1;
 }
 
 hipError_t bk_factor(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, int batch, int64_t sA,

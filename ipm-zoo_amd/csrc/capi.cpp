@@ -499,18 +499,32 @@ int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld,
 
 // Bunch-Kaufman (f3) ----------------------------------------------------------
 int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp) {
-  if (!ctx || N < 0 || ld < N || (N > 0 && (!A || !ipiv))) return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: bad arguments");
-  if (N > IPMZ_BK_NMAX) return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: N > 4096 (one-workgroup factor)");
+  return ipmz_bk_factor_ex(ctx, N, A, ld, ipiv, fix_kp, IPMZ_BK_AUTO);
+}
+
+int ipmz_bk_factor_ex(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp, int algo) {
+  if (!ctx || N < 0 || ld < N || (N > 0 && (!A || !ipiv)) || algo < IPMZ_BK_AUTO || algo > IPMZ_BK_GRID)
+    return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: bad arguments");
+  const bool grid = algo == IPMZ_BK_GRID || (algo == IPMZ_BK_AUTO && N >= IPMZ_BK_GRID_MIN);
+  if (!grid && N > IPMZ_BK_NMAX) return fail(IPMZ_ERR_INVALID, "ipmz_bk_factor: N > 4096 for the one-workgroup factor");
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
-  int* dinfo = nullptr;
-  HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dinfo), sizeof(int), ctx->stream));
+  const size_t wsb = grid ? bk_grid_ws_bytes(N) : 0;
+  char* dws = nullptr;
+  HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&dws), 256 + wsb, ctx->stream));
+  int* dinfo = reinterpret_cast<int*>(dws);
   int rc = IPMZ_OK, info = 0;
-  if (bk_factor(A, ld, N, ipiv, dinfo, fix_kp, 1, 0, 0, ctx->stream) != hipSuccess ||
-      hipMemcpyAsync(&info, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+  unsigned err = 0;
+  const hipError_t e = grid ? bk_factor_grid(A, ld, N, ipiv, dinfo, fix_kp, dws + 256, ctx->stream)
+                            : bk_factor(A, ld, N, ipiv, dinfo, fix_kp, 1, 0, 0, ctx->stream);
+  if (e != hipSuccess || hipMemcpyAsync(&info, dinfo, sizeof(int), hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
+      (grid && hipMemcpyAsync(&err, bk_grid_err_word(dws + 256, N), 4, hipMemcpyDeviceToHost, ctx->stream) !=
+                   hipSuccess) ||
       hipStreamSynchronize(ctx->stream) != hipSuccess)
     rc = fail(IPMZ_ERR_HIP, "ipmz_bk_factor: launch failed");
-  hipFreeAsync(dinfo, ctx->stream);
+  else if (err)
+    rc = fail(IPMZ_ERR_HIP, "ipmz_bk_factor: a grid barrier of the whole-device factor timed out; the factor is invalid");
+  hipFreeAsync(dws, ctx->stream);
   return rc ? rc : info;
 }
 
@@ -676,6 +690,7 @@ struct ipmz_qp {
   bool normal = false;
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
+  char* bkws = nullptr;  // the whole-device Bunch-Kaufman factor's workspace (B == 1, N >= IPMZ_BK_GRID_MIN)
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
   bool slacks = false, naive = false;
@@ -771,6 +786,10 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
 // info_reset: the caller already reset the batched factor's info word
 int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   if (s->eqnone) {  // zero diagonal block: symmetric_indefinite_factorization (reference kp behaviour)
+    if (s->bkws) {
+      HIP_OK(bk_factor_grid(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->bkws, s->ctx->stream));
+      return IPMZ_OK;
+    }
     HIP_OK(bk_factor(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->B, s->sK, s->sP, s->ctx->stream));
     return IPMZ_OK;
   }
@@ -893,9 +912,9 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
       cfg->equality_handling != IPMZ_EQ_SLACKED_SLACKS)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
   const int mk = cfg->inequality_handling == IPMZ_INEQ_NAIVE_SLACKS ? 2 * cfg->m : cfg->m;
-  if (cfg->equality_handling == IPMZ_EQ_NONE && cfg->n + mk + cfg->p > IPMZ_BK_NMAX)
-    return fail(IPMZ_ERR_INVALID, "EqualityHandling::None factors with Bunch-Kaufman (one workgroup per system): "
-                                  "N <= " + std::to_string(IPMZ_BK_NMAX));
+  if (cfg->equality_handling == IPMZ_EQ_NONE && B > 1 && cfg->n + mk + cfg->p > IPMZ_BK_NMAX)
+    return fail(IPMZ_ERR_INVALID, "EqualityHandling::None in batches factors with Bunch-Kaufman one workgroup per "
+                                  "system: N <= " + std::to_string(IPMZ_BK_NMAX));
   const int ih = cfg->inequality_handling, ib = cfg->inequality_bounds, vb = cfg->variable_bounds;
   if (ih != IPMZ_INEQ_SLACKED_SLACKS && ih != IPMZ_INEQ_SLACKS && ih != IPMZ_INEQ_NAIVE_SLACKS)
     return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
@@ -981,7 +1000,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     s->bLinv = dev_array(s, nblk * ctx->nbi * ctx->nbi, &s->sL);
     s->bW = dev_array(s, (int64_t)N * nbo_for(ctx, N), &s->sW);
     void* w = nullptr;
-    ok = s->bLinv && s->bW && hipMalloc(&w, 256) == hipSuccess;
+    ok = s->bLinv && s->bW && hipMalloc(&w, (size_t)(B * 4 > 256 ? B * 4 : 256)) == hipSuccess;  // one info per QP
     if (ok) s->allocs.push_back(w);
     s->binfo = static_cast<int*>(w);
   }
@@ -995,6 +1014,11 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
       ok = hipMalloc(&w, 256) == hipSuccess;
       if (ok) s->allocs.push_back(w);
       s->binfo = static_cast<int*>(w);
+    }
+    if (ok && B == 1 && N >= IPMZ_BK_GRID_MIN) {
+      ok = hipMalloc(&w, bk_grid_ws_bytes(N)) == hipSuccess;
+      if (ok) s->allocs.push_back(w);
+      s->bkws = static_cast<char*>(w);
     }
   }
   if (!ok) {
@@ -1188,7 +1212,14 @@ int qp_status(ipmz_qp* s) {
     return rc;
   }
   if (s->B == 1 && !s->eqnone) return ws_status(st, s->ws, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step");
-  return IPMZ_OK;  // batched / Bunch-Kaufman kernels have no cross-workgroup spins
+  if (s->bkws) {
+    unsigned e = 0;
+    HIP_OK(hipMemcpyAsync(&e, bk_grid_err_word(s->bkws, s->N), 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (e) return fail(IPMZ_ERR_HIP, "Newton step: a grid barrier of the whole-device Bunch-Kaufman factor timed "
+                                     "out; the step is invalid");
+  }
+  return IPMZ_OK;  // batched / one-workgroup Bunch-Kaufman kernels have no cross-workgroup spins
 }
 
 int scalars_impl(ipmz_qp* s, double* out, int count) {

@@ -155,6 +155,13 @@ hipError_t bk_factor(double* A, int64_t ld, int n, int* ipiv, int* info, int fix
                      int64_t sP, hipStream_t st);
 hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double* b, int batch, int64_t sA, int64_t sP,
                     int64_t sb, hipStream_t st);
+// the whole-device factor of ONE matrix (any n; one workgroup per CU, a grid
+// barrier per step): workspace bytes, launch, and its sticky error word
+// (nonzero after a barrier spin timed out -- the factor is then invalid)
+#define IPMZ_BK_GRID_MIN 768  // auto: the grid factor from this order up (single matrices)
+size_t bk_grid_ws_bytes(int n);
+hipError_t bk_factor_grid(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, void* ws, hipStream_t st);
+const unsigned* bk_grid_err_word(const void* ws, int n);
 
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };

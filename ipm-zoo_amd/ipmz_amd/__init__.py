@@ -44,7 +44,7 @@ EXPORTS = [
     "ipmz_batch_get_state", "ipmz_batch_set_state", "ipmz_batch_solve",
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
-    "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
+    "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_factor_ex", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
     "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject", "ipmz_batch_summary",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
@@ -141,6 +141,7 @@ def _load():
         "ipmz_normal_solve": ([_VP, _I, _I, _VP, _I64, _VP, _VP, _VP], _I),
         "ipmz_qp_set_reduction": ([_VP, _I], _I),
         "ipmz_bk_factor": ([_VP, _I, _VP, _I64, _VP, _I], _I),
+        "ipmz_bk_factor_ex": ([_VP, _I, _VP, _I64, _VP, _I, _I], _I),
         "ipmz_bk_solve": ([_VP, _I, _VP, _I64, _VP, _VP], _I),
         "ipmz_symmetric_indefinite_factorization": ([_VP, _I, _P, _P, ctypes.POINTER(ctypes.c_int)], _I),
         "ipmz_overwriting_solve_bunch_kaufman": ([_VP, _I, _P, ctypes.POINTER(ctypes.c_int), _P], _I),
@@ -241,8 +242,13 @@ class Context:
         return float(stat[0]), int(stat[1])
 
     # -- Bunch-Kaufman on device memory (f3) --
-    def bk_factor(self, N, A_ptr, ld, ipiv_ptr, fix_kp=False):
-        return _check(lib.ipmz_bk_factor(self.h, N, _VP(A_ptr), ld, _VP(ipiv_ptr), int(fix_kp)), "ipmz_bk_factor")
+    BK_AUTO, BK_WORKGROUP, BK_GRID = 0, 1, 2
+
+    def bk_factor(self, N, A_ptr, ld, ipiv_ptr, fix_kp=False, algo=0):
+        """symmetric_indefinite_factorization in place (LinearSolvers.cpp:76-207);
+        algo: BK_AUTO, BK_WORKGROUP (one workgroup, N <= 4096) or BK_GRID (every CU)."""
+        return _check(lib.ipmz_bk_factor_ex(self.h, N, _VP(A_ptr), ld, _VP(ipiv_ptr), int(fix_kp), int(algo)),
+                      "ipmz_bk_factor")
 
     def bk_solve(self, N, F_ptr, ld, ipiv_ptr, b_ptr):
         return _check(lib.ipmz_bk_solve(self.h, N, _VP(F_ptr), ld, _VP(ipiv_ptr), _VP(b_ptr)), "ipmz_bk_solve")

@@ -732,6 +732,12 @@ ArgMax absmax(const double* A, int64_t ld, int64_t b, int64_t e, int64_t fixed, 
 }
 }  // namespace
 
+static std::vector<double> a_col(const double* A, int64_t ld, int64_t k, int64_t n) {
+  std::vector<double> c(n, 0.0);
+  for (int64_t i = k; i < n; ++i) c[i] = A[i * ld + k];
+  return c;
+}
+
 static int bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, bool fix_kp) {
   const double alpha = (1.0 + std::sqrt(17.0)) / 8.0;
   auto a = [&](int64_t i, int64_t j) -> double& { return A[i * ld + j]; };
@@ -768,12 +774,23 @@ static int bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, bool fix_k
         std::swap(a(kp, kp), a(kk, kk));
         if (step == 2) std::swap(a(kk, k), a(kp, k));
       }
+      // The updates below are the reference's loops (LinearSolvers.cpp:155-192)
+      // with the (j, i) loops exchanged: every element gets the same single
+      // expression from the same unscaled pivot-column values (staged first,
+      // since the reference scales a(j, k) only after its column j), so the
+      // result is bitwise the serial loop's; rows run in parallel.
+      const int64_t j0 = k + step;
+      std::vector<double> c0(a_col(A, ld, k, n)), c1(step == 2 ? a_col(A, ld, k + 1, n) : std::vector<double>());
       if (step == 1) {  // rank-1: A -= W (1/d) W^T, column k -> L(k)
         const double r = 1.0 / a(k, k);
-        for (int64_t j = k + 1; j < n; ++j) {
-          const double f = r * a(j, k);
-          for (int64_t i = j; i < n; ++i) a(i, j) -= f * a(i, k);
-          a(j, k) *= r;
+        std::vector<double> f(n);
+        for (int64_t j = j0; j < n; ++j) f[j] = r * c0[j];
+#pragma omp parallel for schedule(dynamic, 32) if (n - k > 512)
+        for (int64_t i = j0; i < n; ++i) {
+          double* Ai = A + i * ld;
+          const double ci = c0[i];
+          for (int64_t j = j0; j <= i; ++j) Ai[j] -= f[j] * ci;
+          Ai[k] *= r;
         }
       } else if (k < n - 1) {  // rank-2 with the inverse of the 2x2 block
         double d21 = a(k + 1, k);
@@ -781,12 +798,18 @@ static int bk_factor(int64_t n, double* A, int64_t ld, int64_t* ipiv, bool fix_k
         const double d22 = a(k, k) / d21;
         const double t = 1.0 / (d11 * d22 - 1.0);
         d21 = t / d21;
-        for (int64_t j = k + 2; j < n; ++j) {
-          const double wk = d21 * (d11 * a(j, k) - a(j, k + 1));
-          const double wk1 = d21 * (d22 * a(j, k + 1) - a(j, k));
-          for (int64_t i = j; i < n; ++i) a(i, j) -= (a(i, k) * wk + a(i, k + 1) * wk1);
-          a(j, k) = wk;
-          a(j, k + 1) = wk1;
+        std::vector<double> wk(n), wk1(n);
+        for (int64_t j = j0; j < n; ++j) {
+          wk[j] = d21 * (d11 * c0[j] - c1[j]);
+          wk1[j] = d21 * (d22 * c1[j] - c0[j]);
+        }
+#pragma omp parallel for schedule(dynamic, 32) if (n - k > 512)
+        for (int64_t i = j0; i < n; ++i) {
+          double* Ai = A + i * ld;
+          const double ui = c0[i], vi = c1[i];
+          for (int64_t j = j0; j <= i; ++j) Ai[j] -= (ui * wk[j] + vi * wk1[j]);
+          Ai[k] = wk[i];
+          Ai[k + 1] = wk1[i];
         }
       }
     }

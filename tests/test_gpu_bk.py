@@ -90,3 +90,74 @@ def test_bk_zero_column0_device_info(ctx):
     assert info == 1
     assert np.array_equal(piv.cpu().numpy(), load("bkz0_16_ipiv.bin").astype(np.int32))
     assert np.array_equal(A.cpu().numpy(), load("bkz0_16_F.bin").reshape(N, N))
+
+
+# ---------------------------------------------------------------------------
+# The whole-device factor (k_bk_grid: every CU, one grid barrier per pivot
+# step, fixed row ownership): the same bitwise contract at any N.
+def _dev_factor(ctx, K, algo, fix_kp=False):
+    N = K.shape[0]
+    A = torch.from_numpy(np.ascontiguousarray(K)).cuda()
+    piv = torch.zeros(max(N, 1), dtype=torch.int32, device="cuda")
+    info = ctx.bk_factor(N, A.data_ptr(), N, piv.data_ptr(), fix_kp=fix_kp, algo=algo)
+    return A.cpu().numpy(), piv.cpu().numpy()[:N], info
+
+
+@pytest.mark.parametrize("N,tag", [(8, "bk8"), (64, "bk64"), (8, "bkr8"), (64, "bkr64"), (200, "bkr200"),
+                                   (16, "bkz16"), (16, "bkz0_16")])
+def test_bk_grid_golden(ctx, N, tag):
+    K = load(f"{tag}_K.bin").reshape(N, N)
+    F, piv, info = _dev_factor(ctx, K, ctx.BK_GRID)
+    assert np.array_equal(piv, load(f"{tag}_ipiv.bin").astype(np.int32))
+    assert np.array_equal(F, load(f"{tag}_F.bin").reshape(N, N))  # upper triangle untouched too
+
+
+def _kkt_zero_block(n, m, seed):
+    # [[H, B^T], [B, 0]]: the zero block forces interchanges and 2x2 pivots
+    rng = np.random.default_rng(seed)
+    H = rng.uniform(-1, 1, (n, n)) / n
+    H = H + H.T + np.diag(rng.uniform(0.5, 1.5, n))
+    B = rng.uniform(-1, 1, (m, n))
+    K = np.zeros((n + m, n + m))
+    K[:n, :n] = H
+    K[n:, :n] = B
+    K[:n, n:] = B.T
+    return K
+
+
+@pytest.mark.parametrize("N,zeros", [(1, 0), (2, 0), (5, 0), (300, 0), (1000, 2), (2500, 0), (6000, 3)])
+def test_bk_grid_vs_oracle_bitwise(ctx, N, zeros):
+    K = _indef(N, N + 7, zeros)
+    F, piv, info = _dev_factor(ctx, K, ctx.BK_GRID)
+    Fo, po, io = oracle.bk_factor(K)
+    assert np.array_equal(piv, po.astype(np.int32))
+    assert np.array_equal(np.tril(F), np.tril(Fo))
+    assert np.array_equal(np.triu(F, 1), np.triu(K, 1))
+    assert info == (io + 1 if zeros else 0)
+
+
+@pytest.mark.parametrize("n,m", [(700, 300), (4000, 800)])
+def test_bk_grid_kkt_vs_oracle_bitwise(ctx, n, m):
+    K = _kkt_zero_block(n, m, n)
+    F, piv, _ = _dev_factor(ctx, K, ctx.BK_GRID)
+    Fo, po, _ = oracle.bk_factor(K)
+    assert (po < 0).any() and (po != np.arange(n + m)).any()  # 2x2 pivots and interchanges happened
+    assert np.array_equal(piv, po.astype(np.int32))
+    assert np.array_equal(np.tril(F), np.tril(Fo))
+
+
+def test_bk_grid_equals_workgroup(ctx):
+    K = _kkt_zero_block(1200, 400, 3)
+    Fg, pg, _ = _dev_factor(ctx, K, ctx.BK_GRID)
+    Fw, pw, _ = _dev_factor(ctx, K, ctx.BK_WORKGROUP)
+    assert np.array_equal(pg, pw) and np.array_equal(Fg, Fw)
+
+
+def test_bk_grid_fix_kp(ctx):
+    N = 16
+    K = load("bkz16_K.bin").reshape(N, N)
+    for fix in (False, True):
+        _, piv, info = _dev_factor(ctx, K, ctx.BK_GRID, fix_kp=fix)
+        _, po, info_o = oracle.bk_factor(K, fix_kp=fix)
+        assert info == info_o + 1
+        assert np.array_equal(piv, po.astype(np.int32))

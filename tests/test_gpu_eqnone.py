@@ -80,9 +80,28 @@ def test_batch_vs_oracle(ctx):
             bt.set_state(i, o.vars())
 
 
+@pytest.mark.parametrize("n,m,p,seed,iters", [(900, 120, 60, 5, 2), (4096, 512, 256, 7, 1)])
+def test_newton_steps_grid_factor_vs_oracle(ctx, n, m, p, seed, iters):
+    # N = 1080 and 4864: the whole-device Bunch-Kaufman factor (bk.hip
+    # k_bk_grid, IPMZ_BK_GRID_MIN = 768), the second beyond one workgroup's
+    # former N <= 4096 limit
+    o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), eq_none=True)
+    g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_NONE)
+    g.generate(seed)
+    for it in range(iters):
+        done, rec = o.iterate()
+        assert not done
+        g.step()
+        s1 = g.scalars()
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            assert abs(s1[k] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (it, k)
+        _compare(o, g, f"iter {it}")
+        g.set_vars(o.vars())
+
+
 def test_limits_and_exclusions(ctx):
-    with pytest.raises(I.IpmzError, match="Bunch-Kaufman"):
-        I.Optimizer(4000, 100, 10, ctx, equality_handling=I.EQ_NONE)
+    with pytest.raises(I.IpmzError, match="Bunch-Kaufman"):  # batches: one workgroup per system
+        I.Batch(4000, 100, 10, 2, ctx, equality_handling=I.EQ_NONE)
     g = I.Optimizer(32, 8, 4, ctx, equality_handling=I.EQ_NONE)
     with pytest.raises(I.IpmzError):
         g.set_reduction(I.REDUCTION_NORMAL)
