@@ -168,7 +168,7 @@ int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld,
  * 1 records kp = k.  Returns 0, or 1 + the first all-zero column. */
 int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp);
 /* Same, with the kernel chosen: IPMZ_BK_AUTO (the whole-device factor from
- * N = 768 up), IPMZ_BK_WORKGROUP (one workgroup, N <= 4096), IPMZ_BK_GRID
+ * N = 512 up), IPMZ_BK_WORKGROUP (one workgroup, N <= 4096), IPMZ_BK_GRID
  * (every CU, a grid barrier per pivot step).  Both are bitwise the reference. */
 #define IPMZ_BK_AUTO 0
 #define IPMZ_BK_WORKGROUP 1

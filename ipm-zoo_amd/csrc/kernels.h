@@ -158,7 +158,7 @@ hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double*
 // the whole-device factor of ONE matrix (any n; one workgroup per CU, a grid
 // barrier per step): workspace bytes, launch, and its sticky error word
 // (nonzero after a barrier spin timed out -- the factor is then invalid)
-#define IPMZ_BK_GRID_MIN 768  // auto: the grid factor from this order up (single matrices)
+#define IPMZ_BK_GRID_MIN 512  // auto: the grid factor from this order up (single matrices)
 size_t bk_grid_ws_bytes(int n);
 hipError_t bk_factor_grid(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, void* ws, hipStream_t st);
 const unsigned* bk_grid_err_word(const void* ws, int n);

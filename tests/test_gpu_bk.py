@@ -115,8 +115,9 @@ def test_bk_grid_golden(ctx, N, tag):
 def _kkt_zero_block(n, m, seed):
     # [[H, B^T], [B, 0]]: the zero block forces interchanges and 2x2 pivots
     rng = np.random.default_rng(seed)
-    H = rng.uniform(-1, 1, (n, n)) / n
-    H = H + H.T + np.diag(rng.uniform(0.5, 1.5, n))
+    H = rng.uniform(-1, 1, (n, n))
+    H = H + H.T
+    H[np.arange(n), np.arange(n)] *= 0.01  # weak diagonal: interchanges and 2x2 pivots
     B = rng.uniform(-1, 1, (m, n))
     K = np.zeros((n + m, n + m))
     K[:n, :n] = H

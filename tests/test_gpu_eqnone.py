@@ -83,7 +83,7 @@ def test_batch_vs_oracle(ctx):
 @pytest.mark.parametrize("n,m,p,seed,iters", [(900, 120, 60, 5, 2), (4096, 512, 256, 7, 1)])
 def test_newton_steps_grid_factor_vs_oracle(ctx, n, m, p, seed, iters):
     # N = 1080 and 4864: the whole-device Bunch-Kaufman factor (bk.hip
-    # k_bk_grid, IPMZ_BK_GRID_MIN = 768), the second beyond one workgroup's
+    # k_bk_grid, IPMZ_BK_GRID_MIN = 512), the second beyond one workgroup's
     # former N <= 4096 limit
     o = oracle.OracleQP(oracle.gen_qp(n, m, p, seed), eq_none=True)
     g = I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_NONE)
