@@ -146,10 +146,11 @@ int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws
  * SymbolicOptimization.cpp:465-478; built at Optimizer.cpp:39-40) but never
  * evaluates it.  For the augmented K = [[H, B^T], [B, -E]] (device, lower
  * triangle, order n + mp, H SPD, E > 0 diagonal): Cholesky of H (as L D L^T,
- * D > 0), Vt = B L^{-T}, S = E + B H^{-1} B^T, Cholesky of S.  The H block is
- * overwritten by its factor, the (2,2) block by S's, B is left intact.  D:
- * device, n + mp doubles (pivots of H, then of S).  Returns > 0 (1-based
- * augmented index) when H or S has a non-positive pivot. */
+ * D > 0), L21 = B L^{-T} D^{-1}, S = E + L21 D L21^T = E + B H^{-1} B^T,
+ * Cholesky of S -- run as the x-first blocked LDL^T of K, one pipelined
+ * factor (normal.hip).  K's lower triangle is overwritten by [L_H; L21, L_S].
+ * D: device, n + mp doubles (pivots of H, then of -S).  Returns > 0 (1-based
+ * augmented index) when H or S is not positive definite. */
 int64_t ipmz_normal_workspace_bytes(ipmz_ctx* ctx, int n, int mp);
 int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes);
 /* b = [r0; r1] (device) <- [x; l]:  l = S^{-1} (B H^{-1} r0 - r1),

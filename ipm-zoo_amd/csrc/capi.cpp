@@ -389,77 +389,39 @@ int ipmz_mixed_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, void* ws
 }  // extern "C"
 
 namespace {
-// [spd info (256 B)] [ws of the H factor] [ws of the S factor] [Vt mp x ldv]
-// [W mp x ldv] [u n] [part ceil(mp/64) x n]
+// [definiteness info (256 B)] [ws of the order n + mp LDL^T]
 struct NormalWs {
   int* info = nullptr;
-  char *wsH = nullptr, *wsS = nullptr;
-  double *Vt = nullptr, *W = nullptr, *u = nullptr, *part = nullptr;
-  int64_t ldv = 0, total = 0;
+  char* wsK = nullptr;
+  int64_t total = 0;
 };
 NormalWs normal_ws(char* base, int n, int mp, const ipmz_ctx* ctx) {
-  const int nbi = ctx->nbi;
   NormalWs w;
-  int64_t off = 0;
-  auto take = [&](int64_t bytes) {
-    char* p = base ? base + off : nullptr;
-    off += round_up(bytes, 256);
-    return p;
-  };
-  w.ldv = round_up(n, 8);
-  w.info = reinterpret_cast<int*>(take(256));
-  w.wsH = take(ws_layout(n, nbo_for(ctx, n), nbi).total);
-  w.wsS = take(ws_layout(mp > 0 ? mp : 1, nbo_for(ctx, mp > 0 ? mp : 1), nbi).total);
-  w.Vt = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
-  w.W = reinterpret_cast<double*>(take((int64_t)mp * w.ldv * 8));
-  w.u = reinterpret_cast<double*>(take((int64_t)n * 8));
-  w.part = reinterpret_cast<double*>(take((int64_t)((mp + 63) / 64) * n * 8));
-  w.total = off;
+  w.info = reinterpret_cast<int*>(base);
+  w.wsK = base ? base + 256 : nullptr;
+  w.total = 256 + ws_layout(n + mp, nbo_for(ctx, n + mp), ctx->nbi).total;
   return w;
 }
 }  // namespace
 
+// The normal equations as the x-first blocked LDL^T of [[H, B^T], [B, -E]]
+// (normal.hip): Cholesky(H), the TRSM of B, the SYRK into the (2,2) block and
+// Cholesky(S) in one pipelined factor; then H's pivots > 0, S's < 0.
 static int normal_factor_impl(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, const NormalWs& w,
                               TrailTimer* timer) {
   hipStream_t st = ctx->stream;
   HIP_OK(hipMemsetAsync(w.info, 0x7f, sizeof(int), st));
-  // Cholesky of H as L D L^T (the blocked factor on the leading n x n block)
-  int rc = factor_impl(ctx, n, K, ld, D, w.wsH, timer);
+  int rc = factor_impl(ctx, n + mp, K, ld, D, w.wsK, timer);
   if (rc) return rc;
-  HIP_OK(ne_check_pos(D, n, 0, w.info, st));
-  if (mp == 0) return IPMZ_OK;
-  // Vt = B L^{-T}, S = E + Vt D^{-1} Vt^T (into the (2,2) block), Cholesky of S
-  const WsLayout lh = ws_layout(n, nbo_for(ctx, n), ctx->nbi);
-  // the TRSM steps over 128-column blocks with the solve prep's X_J = L_JJ^{-1}
-  // (built by factor_impl for nbi = 64: half the sequential steps of the
-  // factor's 64 x 64 inverses), else over the factor's own nbi blocks
-  const double* LinvH = reinterpret_cast<const double*>(w.wsH + lh.linv_off);
-  const double* XH = reinterpret_cast<const double*>(w.wsH + lh.prep_off);
-  HIP_OK(hipMemcpy2DAsync(w.Vt, w.ldv * 8, K + (int64_t)n * ld, ld * 8, (size_t)n * 8, mp, hipMemcpyDeviceToDevice,
-                          st));
-  if (ctx->nbi == 64) HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, XH, IPMZ_SOLVE_BLOCK, st));
-  else HIP_OK(ne_trsm_right(w.Vt, w.ldv, mp, n, K, ld, LinvH, ctx->nbi, st));
-  double* K22 = K + (int64_t)n * ld + n;
-  HIP_OK(ne_schur(K22, ld, mp, w.Vt, w.W, w.ldv, n, D, st));
-  if ((rc = factor_impl(ctx, mp, K22, ld, D + n, w.wsS, nullptr))) return rc;
-  HIP_OK(ne_check_pos(D + n, mp, n, w.info, st));
+  HIP_OK(ne_check_sign(D, n, 0, 1.0, w.info, st));
+  HIP_OK(ne_check_sign(D + n, mp, n, -1.0, w.info, st));
   return IPMZ_OK;
 }
 
+// b = [r0; r1] <- [x; l]: the factor's forward and backward sweeps
 static int normal_solve_impl(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D,
                              const NormalWs& w, double* b) {
-  hipStream_t st = ctx->stream;
-  HIP_OK(hipMemcpyAsync(w.u, b, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-  HIP_OK(solve_ws(K, ld, n, D, w.wsH, nbo_for(ctx, n), ctx->nbi, w.u, st));  // u = H^{-1} r0
-  if (mp == 0) {
-    HIP_OK(hipMemcpyAsync(b, w.u, (size_t)n * 8, hipMemcpyDeviceToDevice, st));
-    return IPMZ_OK;
-  }
-  const double* Bm = K + (int64_t)n * ld;
-  HIP_OK(ne_gemv(Bm, ld, mp, n, w.u, b + n, b + n, st));                                     // B u - r1
-  HIP_OK(solve_ws(K + (int64_t)n * ld + n, ld, mp, D + n, w.wsS, nbo_for(ctx, mp), ctx->nbi, b + n, st));  // l
-  HIP_OK(ne_gemvt(Bm, ld, mp, n, b + n, w.part, b, st));                                    // r0 - B^T l
-  HIP_OK(solve_ws(K, ld, n, D, w.wsH, nbo_for(ctx, n), ctx->nbi, b, st));                           // x
+  HIP_OK(solve_ws(K, ld, n + mp, D, w.wsK, nbo_for(ctx, n + mp), ctx->nbi, b, ctx->stream));
   return IPMZ_OK;
 }
 
@@ -482,11 +444,7 @@ int ipmz_normal_factor(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, doub
   HIP_OK(hipMemcpyAsync(&info, w.info, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
   HIP_OK(hipStreamSynchronize(ctx->stream));
   if (info != 0x7f7f7f7f) return info;
-  // non-finite pivots of the two LDL^T factors (their own info words)
-  const int ih = read_info(ctx, w.wsH, n);
-  if (ih) return ih;
-  const int is = mp ? read_info(ctx, w.wsS, mp) : 0;
-  return is > 0 ? n + is : is;
+  return read_info(ctx, w.wsK, n + mp);  // a non-finite pivot of the factor
 }
 
 int ipmz_normal_solve(ipmz_ctx* ctx, int n, int mp, const double* K, int64_t ld, const double* D, void* ws,
@@ -1205,11 +1163,7 @@ int qp_status(ipmz_qp* s) {
   }
   if (s->normal) {
     const NormalWs w = normal_ws(s->nws, s->n, s->m + s->p, s->ctx);
-    int rc = ws_status(st, w.wsH, s->n, nbo_for(s->ctx, s->n), s->ctx->nbi, "Newton step (normal equations, H)");
-    if (!rc && s->m + s->p)
-      rc = ws_status(st, w.wsS, s->m + s->p, nbo_for(s->ctx, s->m + s->p), s->ctx->nbi,
-                     "Newton step (normal equations, S)");
-    return rc;
+    return ws_status(st, w.wsK, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step (normal equations)");
   }
   if (s->B == 1 && !s->eqnone) return ws_status(st, s->ws, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step");
   if (s->bkws) {

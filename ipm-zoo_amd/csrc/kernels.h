@@ -83,8 +83,6 @@ hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
                        const BatchStrides* bs = nullptr);
-hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                         double* C, int64_t ldc, hipStream_t st);
 
 // trsv.hip -------------------------------------------------------------------
 // In-place b <- L^{-T} D^{-1} L^{-1} b; side: 2*nbi doubles of scratch.
@@ -136,18 +134,8 @@ hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, doubl
                        hipStream_t st);
 
 // normal.hip: normal-equations reduction (config C2) -------------------------
-hipError_t ne_check_pos(const double* D, int N, int offset, int* info, hipStream_t st);
-hipError_t ne_trsm_right(double* Vt, int64_t ldv, int rows, int n, const double* K, int64_t ld, const double* LinvH,
-                         int nb, hipStream_t st);
-hipError_t ne_schur(double* K22, int64_t ld, int mp, const double* Vt, double* W, int64_t ldv, int n,
-                    const double* DH, hipStream_t st);
-hipError_t ne_gemv(const double* Bm, int64_t ld, int rows, int cols, const double* u, const double* r1, double* t,
-                   hipStream_t st);
-hipError_t ne_gemvt(const double* Bm, int64_t ld, int rows, int cols, const double* l, double* part, double* r0,
-                    hipStream_t st);
-// C -= A B^T over the full rectangle (no triangle restriction)
-hipError_t gemm_nt_sub_rect(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                            double* C, int64_t ldc, hipStream_t st);
+hipError_t ne_check_sign(const double* D, int N, int offset, double sign, int* info, hipStream_t st);
+
 
 // bk.hip: Bunch-Kaufman factor / solve (one workgroup per matrix) -----------
 #define IPMZ_BK_NMAX 4096

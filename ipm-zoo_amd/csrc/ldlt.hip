@@ -273,41 +273,6 @@ hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const
   return gemm_nt_sub_t<double>(M, N, Kd, A, lda, B, ldb, C, ldc, row0, col0, square_lower, st, bs);
 }
 
-hipError_t gemm_nt_sub_rect(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                            double* C, int64_t ldc, hipStream_t st) {
-  GemmArgs g{};
-  g.M = M;
-  g.N = N;
-  g.Kd = Kd;
-  g.A = A;
-  g.lda = lda;
-  g.B = B;
-  g.ldb = ldb;
-  g.C = C;
-  g.ldc = ldc;
-  g.lower = 0;
-  return launch_gemm<128, 128, EPI_SUB_STRIP, 2, 4>(g, st);
-}
-
-hipError_t gemm_nt_store(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
-                         double* C, int64_t ldc, hipStream_t st) {
-  GemmArgs g{};
-  g.M = M;
-  g.N = N;
-  g.Kd = Kd;
-  g.A = A;
-  g.lda = lda;
-  g.B = B;
-  g.ldb = ldb;
-  g.C = C;
-  g.ldc = ldc;
-  g.lower = 0;
-  // in place (C == A) is safe only with one tile column per row band: N <= 128;
-  // 64-row bands double the grid of the normal equations' TRSM steps (512 rows)
-  if (M <= 4096) return launch_gemm<64, 128, EPI_STORE, 2, 4>(g, st);
-  return launch_gemm<128, 128, EPI_STORE, 2, 4>(g, st);
-}
-
 // ---------------------------------------------------------------------------
 // Factor the outer panel [k0, k0 + bo) as a kernel chain (batched factors
 // and nbi = 128): inner diag / TRSM / strip steps, all on stream st.  Writes
