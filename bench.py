@@ -214,7 +214,8 @@ def run_single(I, ctx, args, world, dist, torch, workload):
         out["phase_ms_per_step"] = {kk: ph[kk] / k for kk in ("step", "assemble", "factor", "solve", "eval")}
         if wl.get("normal"):
             fl = n ** 3 / 3.0 + n * n * (m + p) + n * (m + p) ** 2 + (m + p) ** 3 / 3.0
-            what = "normal-equations factor phase: LDL^T(H) + TRSM + SYRK + LDL^T(S)"
+            what = ("normal-equations factor phase: Cholesky(H) + TRSM + SYRK + Cholesky(S) as one pipelined "
+                    "x-first blocked LDL^T (fp64 MFMA)")
         else:
             fl = Nk ** 3 / 3.0
             what = ("blocked LDL^T factor phase (" + ("fp32 " if mixed else "fp64 ") +
