@@ -107,7 +107,7 @@ const char* ipmz_last_error(void);
  * factorization starts).  0 (default) for normal operation. */
 int ipmz_debug_inject(int mask);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512;
- * 0 = by matrix order: 384 for N >= 8192 with nbi 64, else 256), inner
+ * 0 = by matrix order: 512 for N >= 2048 with nbi 64, else 256), inner
  * diagonal block nbi (64 or 128).  Defaults 0 / 64.  Workspace sizes depend
  * on it: query them after setting the blocking. */
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);
@@ -207,6 +207,11 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
                                     With InequalityHandling::SlackedSlacks and both
                                     inequality bounds; the reference's evaluator asserts
                                     on its zero blocks (Evaluation.cpp:57-60) */
+#define IPMZ_EQ_NAIVE_SLACKS 5   /* equality NaiveSlacks: C x - v = d, C x + w = d with duals
+                                    lambda_v, lambda_w as KKT rows (SymbolicOptimization.cpp:
+                                    163-171; N = n + 2m + 2p).  With InequalityHandling::
+                                    NaiveSlacks and both inequality bounds: the rows run as
+                                    NaiveSlacks inequality rows with l = u = d */
 /* Settings::InequalityHandling (SymbolicOptimization.h:28-64) */
 #define IPMZ_INEQ_SLACKED_SLACKS 0 /* s with slacks g = s - l_A, h = u_A - s (and y, z
                                       for x): the reference default                  */

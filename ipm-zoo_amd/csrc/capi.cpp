@@ -868,7 +868,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     return fail(IPMZ_ERR_INVALID, "dimensions: n > 0, m >= 0, p >= 0, batch > 0");
   if (cfg->equality_handling != IPMZ_EQ_REGULARIZATION && cfg->equality_handling != IPMZ_EQ_NONE &&
       cfg->equality_handling != IPMZ_EQ_PENALTY && cfg->equality_handling != IPMZ_EQ_PENALTY_EXTRA_DUAL &&
-      cfg->equality_handling != IPMZ_EQ_SLACKED_SLACKS)
+      cfg->equality_handling != IPMZ_EQ_SLACKED_SLACKS && cfg->equality_handling != IPMZ_EQ_NAIVE_SLACKS)
     return fail(IPMZ_ERR_INVALID, "unknown equality handling");
   const int mk = cfg->inequality_handling == IPMZ_INEQ_NAIVE_SLACKS ? 2 * cfg->m : cfg->m;
   if (cfg->equality_handling == IPMZ_EQ_NONE && B > 1 && cfg->n + mk + cfg->p > IPMZ_BK_NMAX)
@@ -879,6 +879,9 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     return fail(IPMZ_ERR_INVALID, "unknown inequality handling");
   if (ih == IPMZ_INEQ_NAIVE_SLACKS && cfg->m > 0 && ib != IPMZ_BOUNDS_BOTH)
     return fail(IPMZ_ERR_INVALID, "InequalityHandling::NaiveSlacks: both inequality bounds");
+  if (cfg->equality_handling == IPMZ_EQ_NAIVE_SLACKS && (ih != IPMZ_INEQ_NAIVE_SLACKS || ib != IPMZ_BOUNDS_BOTH))
+    return fail(IPMZ_ERR_INVALID, "EqualityHandling::NaiveSlacks: with InequalityHandling::NaiveSlacks and both "
+                                  "inequality bounds");
   if (cfg->equality_handling == IPMZ_EQ_SLACKED_SLACKS && (ih != IPMZ_INEQ_SLACKED_SLACKS || ib != IPMZ_BOUNDS_BOTH))
     return fail(IPMZ_ERR_INVALID, "EqualityHandling::SlackedSlacks: with InequalityHandling::SlackedSlacks and both "
                                   "inequality bounds");
@@ -896,10 +899,12 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   s->n = cfg->n;
   s->m_usr = cfg->m;
   s->p_usr = cfg->p;
-  s->eqss = cfg->equality_handling == IPMZ_EQ_SLACKED_SLACKS;
+  // equality SlackedSlacks / NaiveSlacks: the p rows appended to the
+  // inequality block of the same handling with l = u = d
+  s->eqss = cfg->equality_handling == IPMZ_EQ_SLACKED_SLACKS || cfg->equality_handling == IPMZ_EQ_NAIVE_SLACKS;
   s->m = s->eqss ? cfg->m + cfg->p : cfg->m;
   s->p = s->eqss ? 0 : cfg->p;
-  s->N = cfg->n + mk + cfg->p;
+  s->N = cfg->equality_handling == IPMZ_EQ_NAIVE_SLACKS ? cfg->n + 2 * (cfg->m + cfg->p) : cfg->n + mk + cfg->p;
   s->delta = cfg->delta > 0 ? cfg->delta : 1e-4;
   s->eqnone = cfg->equality_handling == IPMZ_EQ_NONE;
   s->eqpen = cfg->equality_handling == IPMZ_EQ_PENALTY || cfg->equality_handling == IPMZ_EQ_PENALTY_EXTRA_DUAL;
@@ -1187,7 +1192,7 @@ int scalars_impl(ipmz_qp* s, double* out, int count) {
   return s->loaded ? qp_status(s) : IPMZ_OK;
 }
 
-// EqualityHandling::SlackedSlacks: the step's slots hold [lambda_g lambda_v],
+// EqualityHandling::SlackedSlacks / NaiveSlacks: the step's slots hold [lambda_g lambda_v],
 // [lambda_h lambda_w], [g v], [h w]; the reference's Newton order is
 // lambda_g, lambda_h, lambda_v, lambda_w, ..., g, h, v, w (formulations.txt).
 // perm[k] = the step-vector index of reference-order element k.
@@ -1199,7 +1204,9 @@ std::vector<int64_t> eqss_perm(const ipmz_qp* s) {
   auto run = [&](int64_t from, int64_t len) {
     for (int64_t k = 0; k < len; ++k) perm.push_back(from + k);
   };
-  int64_t off = n + 2 * mp;  // x, [lambda_A lambda_C], [s t]: same order
+  // x, [lambda_A lambda_C], [s t] (SlackedSlacks) or x alone (NaiveSlacks, no
+  // s / lambda_A): same order
+  int64_t off = s->naive ? n : n + 2 * mp;
   run(0, off);
   const int64_t LGo = off, LHo = off + mp;  // [lambda_g lambda_v], [lambda_h lambda_w]
   run(LGo, m);

@@ -113,7 +113,8 @@ enum class EqualityHandling {
   None = IPMZ_EQ_NONE,
   PenaltyFunction = IPMZ_EQ_PENALTY,
   PenaltyFunctionWithExtraDual = IPMZ_EQ_PENALTY_EXTRA_DUAL,  // the same Newton system (SymbolicOptimization.cpp:364-366)
-  SlackedSlacks = IPMZ_EQ_SLACKED_SLACKS
+  SlackedSlacks = IPMZ_EQ_SLACKED_SLACKS,
+  NaiveSlacks = IPMZ_EQ_NAIVE_SLACKS  // with InequalityHandling::NaiveSlacks
 };
 
 // Settings::Bounds and Settings::InequalityHandling (SymbolicOptimization.h:

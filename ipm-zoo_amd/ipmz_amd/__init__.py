@@ -64,6 +64,7 @@ EQ_NONE = 1            # zero (lambda_C, lambda_C) block, Bunch-Kaufman factor
 EQ_PENALTY = 2         # PenaltyFunction: -mu (lambda_C, lambda_C) block, LDL^T
 EQ_PENALTY_EXTRA_DUAL = 3  # PenaltyFunctionWithExtraDual: the same Newton system (reference-derived)
 EQ_SLACKED_SLACKS = 4  # t, v = t - d, w = d - t with duals lambda_v, lambda_w (SlackedSlacks inequalities)
+EQ_NAIVE_SLACKS = 5    # C x - v = d, C x + w = d, lambda_v / lambda_w as KKT rows (NaiveSlacks inequalities)
 INEQ_SLACKED_SLACKS = 0  # Settings::InequalityHandling (include/ipmz.h IPMZ_INEQ_*)
 INEQ_SLACKS = 1          # no g/h/y/z slacks (the reference's corrector defect reproduced)
 INEQ_NAIVE_SLACKS = 2    # no s; lambda_g, lambda_h as KKT rows (N = n + 2m + p)

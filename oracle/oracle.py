@@ -297,15 +297,21 @@ class EqSlackedOracle:
     """OracleQP over eqss_merge(qp), in the reference's variable order
     (x, lambda_A, lambda_C, s, t, lambda_g, lambda_h, lambda_v, lambda_w,
     lambda_y, lambda_z, g, h, v, w, y, z) and with t starting at 1
-    (EnvironmentBuilder.cpp:62), as capi.cpp's eqss_perm."""
+    (EnvironmentBuilder.cpp:62), as capi.cpp's eqss_perm.
 
-    def __init__(self, qp):
+    naive=True: EqualityHandling::NaiveSlacks with NaiveSlacks inequalities
+    (SymbolicOptimization.cpp:163-171 against 104-116: C x - v = d, C x + w = d
+    are the inequality rows A x - g = l, A x + h = u with l = u = d), order x,
+    lambda_g, lambda_h, lambda_v, lambda_w, lambda_y, lambda_z, g, h, v, w, y, z
+    (v, w and their duals start at 1 like g, h)."""
+
+    def __init__(self, qp, naive=False):
         n, m, p = qp["n"], qp["m"], qp["p"]
         self.qp = qp
-        self.o = OracleQP(eqss_merge(qp))
+        self.o = OracleQP(eqss_merge(qp), form=Form(naive=True) if naive else None)
         mp = m + p
-        perm = list(range(n + 2 * mp))  # x, [lambda_A lambda_C], [s t]
-        off = n + 2 * mp
+        off = n if naive else n + 2 * mp
+        perm = list(range(off))  # x (, [lambda_A lambda_C], [s t])
         for base in (off, off + 2 * mp + 2 * n):  # [lambda_g lambda_v][lambda_h lambda_w], then [g v][h w]
             perm += list(range(base, base + m)) + list(range(base + mp, base + mp + m))
             perm += list(range(base + m, base + mp)) + list(range(base + mp + m, base + 2 * mp))
@@ -314,13 +320,19 @@ class EqSlackedOracle:
         perm += list(range(len(perm), self.o.L))  # y, z
         self.perm = np.array(perm)
         assert sorted(perm) == list(range(self.o.L))
+        # KKT rows: x, [lambda_A lambda_C] already in the reference's order;
+        # NaiveSlacks: x, [lambda_g lambda_v], [lambda_h lambda_w] -> x,
+        # lambda_g, lambda_h, lambda_v, lambda_w
+        self.kperm = np.array(perm[:self.o.N]) if naive else np.arange(self.o.N)
         self.N, self.L = self.o.N, self.o.L
-        self.sizes = dict(x=n, lambda_A=m, lambda_C=p, s=m, t=p, lambda_g=m, lambda_h=m, lambda_v=p, lambda_w=p,
+        self.sizes = dict(x=n, lambda_A=0 if naive else m, lambda_C=0 if naive else p, s=0 if naive else m,
+                          t=0 if naive else p, lambda_g=m, lambda_h=m, lambda_v=p, lambda_w=p,
                           lambda_y=n, lambda_z=n, g=m, h=m, v=p, w=p, y=n, z=n)
         self.order = [k for k in self.sizes if self.sizes[k]]
-        v = self.o.vars()
-        v[n + 2 * m + p: n + 2 * mp] = 1.0  # t
-        self.o.set_vars(v)
+        if not naive:
+            v = self.o.vars()
+            v[n + 2 * m + p: n + 2 * mp] = 1.0  # t
+            self.o.set_vars(v)
 
     def vars(self):
         return self.o.vars()[self.perm]
@@ -340,7 +352,8 @@ class EqSlackedOracle:
         return self.o.iterate()
 
     def kkt(self):
-        return self.o.kkt()
+        K = self.o.kkt()
+        return K[np.ix_(self.kperm, self.kperm)]
 
     def split(self, flat):
         out, off = {}, 0

@@ -68,6 +68,7 @@ CASES = [
     ("newton", 48, 16, 7, 100, "SlackedSlacks", "Both", "Both", 8, "SlackedSlacks", "eqss"),
     ("newton", 48, 16, 7, 100, "NaiveSlacks", "Both", "Both", 0, "none", "naive"),
     ("newton", 48, 16, 7, 100, "NaiveSlacks", "Both", "Both", 8, "Regularization", "naivereg"),
+    ("newton", 48, 16, 7, 100, "NaiveSlacks", "Both", "Both", 8, "NaiveSlacks", "naiveeq"),
 ]
 
 

@@ -150,7 +150,18 @@ EQ_CASES = [
     ("naivereg", 8, dict(inequality_handling=I.INEQ_NAIVE_SLACKS),
      lambda qp: oracle.OracleQP(qp, form=oracle.Form(naive=True))),
     ("eqss", 8, dict(equality_handling=I.EQ_SLACKED_SLACKS), oracle.EqSlackedOracle),
+    ("naiveeq", 8, dict(inequality_handling=I.INEQ_NAIVE_SLACKS, equality_handling=I.EQ_NAIVE_SLACKS),
+     lambda qp: oracle.EqSlackedOracle(qp, naive=True)),
 ]
+
+
+def _kkt_ref_order(g, o):
+    # the device KKT (lower triangle, the step's row order) in the reference's
+    # row order (EqSlackedOracle.kperm: NaiveSlacks equality rows interleave)
+    K = np.tril(g.kkt())
+    K = K + np.tril(K, -1).T
+    kp = getattr(o, "kperm", np.arange(K.shape[0]))
+    return np.tril(K[np.ix_(kp, kp)])
 
 
 @pytest.mark.parametrize("tag,p,kw,mk", EQ_CASES, ids=[c[0] for c in EQ_CASES])
@@ -163,7 +174,7 @@ def test_equality_golden_trace(ctx, tag, p, kw, mk):
     g.generate(7)
     assert g.state_len == len(load(f"{fx}_it0_vars.bin")) and g.N == o.N
     assert np.array_equal(g.vars(), load(f"{fx}_it0_vars.bin"))
-    assert np.array_equal(g.kkt(), np.tril(sym_from_lower(load(f"{fx}_it0_kkt.bin"), o.N)))
+    assert np.array_equal(_kkt_ref_order(g, o), np.tril(sym_from_lower(load(f"{fx}_it0_kkt.bin"), o.N)))
     for it, ref in enumerate(rows):
         g.set_vars(load(f"{fx}_it{it}_vars.bin"))
         s0 = g.scalars()
@@ -326,3 +337,51 @@ def test_eq_slacked_slacks_batch_and_solve(ctx):
 def test_eq_slacked_slacks_rejected(ctx, kw):
     with pytest.raises(I.IpmzError):
         I.Optimizer(16, 4, 2, ctx, equality_handling=I.EQ_SLACKED_SLACKS, **kw)
+
+
+# EqualityHandling::NaiveSlacks (with NaiveSlacks inequalities) at blocked
+# sizes, in a batch, and its state order (pinned above to the reference's
+# "naiveeq" iterations at n = 48)
+@pytest.mark.parametrize("n,m,p,seed", [(300, 70, 30, 3), (200, 0, 40, 4)])
+def test_eq_naive_slacks_vs_oracle(ctx, n, m, p, seed):
+    kw = dict(inequality_handling=I.INEQ_NAIVE_SLACKS, equality_handling=I.EQ_NAIVE_SLACKS)
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, seed), naive=True)
+    g = I.Optimizer(n, m, p, ctx, **kw)
+    g.generate(seed)
+    assert g.N == n + 2 * (m + p) == o.N and g.state_len == o.L
+    assert np.array_equal(g.vars(), o.vars())
+    assert np.array_equal(_kkt_ref_order(g, o), np.tril(o.kkt()))
+    _eqss_iterations(g, o, 5, "naive")
+
+
+def test_eq_naive_slacks_state_order_batch_and_solve(ctx):
+    n, m, p = 64, 16, 8
+    kw = dict(inequality_handling=I.INEQ_NAIVE_SLACKS, equality_handling=I.EQ_NAIVE_SLACKS)
+    g = I.Optimizer(n, m, p, ctx, **kw)
+    g.generate(6)
+    o = oracle.EqSlackedOracle(oracle.gen_qp(n, m, p, 6), naive=True)
+    sp = o.split(g.vars())
+    assert np.all(sp["v"] == 1.0) and np.all(sp["lambda_w"] == 1.0)
+    v0 = g.vars()
+    v = np.arange(g.state_len, dtype=np.float64) + 0.5  # set -> get is the identity in the reference's order
+    g.set_vars(v)
+    assert np.array_equal(g.vars(), v)
+    g.set_vars(v0)
+    iters, tr = g.solve(100)
+    for it in range(100):
+        done, _ = o.iterate()
+        if done:
+            break
+    assert tr[-1]["converged"] == 1.0 and iters == it
+    assert np.abs(o.split(g.vars())["x"] - o.split(o.vars())["x"]).max() < 1e-8
+    bt = I.Batch(n, m, p, 3, ctx, **kw)
+    bt.generate(5)  # QP 1 of the batch = seed 6
+    for _ in range(3):
+        bt.step()
+    g2 = I.Optimizer(n, m, p, ctx, **kw)
+    g2.generate(6)
+    for _ in range(3):
+        g2.step()
+    assert np.abs(bt.state(1, 0) - g2.vars()).max() < 1e-12
+    with pytest.raises(I.IpmzError):  # equality NaiveSlacks rides on NaiveSlacks inequalities
+        I.Optimizer(n, m, p, ctx, equality_handling=I.EQ_NAIVE_SLACKS)
