@@ -650,6 +650,7 @@ struct ipmz_qp {
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
   char* bkws = nullptr;  // the whole-device Bunch-Kaufman factor's workspace (B == 1, N >= IPMZ_BK_GRID_MIN)
+  unsigned* pflags = nullptr;  // B > 1: the two-workgroup small factor's flags + sticky error word
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
   bool slacks = false, naive = false;
@@ -763,6 +764,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   bs.sD = s->sD;
   bs.sL = s->sL;
   bs.sW = s->sW;
+  bs.pflags = s->pflags;
   if (!info_reset) HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
   HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
                              s->ctx->stream, bs));
@@ -967,6 +969,12 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     ok = s->bLinv && s->bW && hipMalloc(&w, (size_t)(B * 4 > 256 ? B * 4 : 256)) == hipSuccess;  // one info per QP
     if (ok) s->allocs.push_back(w);
     s->binfo = static_cast<int*>(w);
+    if (ok) {  // flags of the two-workgroup small factor (B <= #CU)
+      ok = hipMalloc(&w, ((size_t)B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned)) == hipSuccess &&
+           hipMemset(w, 0, ((size_t)B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned)) == hipSuccess;
+      if (ok) s->allocs.push_back(w);
+      s->pflags = static_cast<unsigned*>(w);
+    }
   }
   if (ok && s->eqnone) {
     s->sP = round_up(N, 16);
@@ -1172,6 +1180,13 @@ int qp_status(ipmz_qp* s) {
     return ws_status(st, w.wsK, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step (normal equations)");
   }
   if (s->B == 1 && !s->eqnone) return ws_status(st, s->ws, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step");
+  if (s->pflags && small_pair_eligible(s->B, s->N)) {
+    unsigned e = 0;
+    HIP_OK(hipMemcpyAsync(&e, s->pflags + (size_t)s->B * IPMZ_PAIR_FLAGS, 4, hipMemcpyDeviceToHost, st));
+    HIP_OK(hipStreamSynchronize(st));
+    if (e) return fail(IPMZ_ERR_HIP, "Newton step: a hand-off of the two-workgroup batched factor timed out; the "
+                                     "step is invalid");
+  }
   if (s->bkws) {
     unsigned e = 0;
     HIP_OK(hipMemcpyAsync(&e, bk_grid_err_word(s->bkws, s->N), 4, hipMemcpyDeviceToHost, st));

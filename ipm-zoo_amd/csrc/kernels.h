@@ -27,7 +27,13 @@ constexpr int SOLVE_ERR_WORD = 1;
 struct BatchStrides {
   int B = 1;
   int64_t sK = 0, sD = 0, sL = 0, sW = 0;
+  // small batched factor: B * IPMZ_PAIR_FLAGS + 1 words for the two-workgroup
+  // factor (B <= #CU; W then needs 2 x N x 64 per QP), nullptr = one workgroup
+  unsigned* pflags = nullptr;
 };
+#define IPMZ_PAIR_FLAGS 32  // per QP: LW[16], DONE[16] (N <= IPMZ_SMALL_NMAX)
+// the batched factor of order N runs two workgroups per QP (given flags)
+bool small_pair_eligible(int B, int N);
 // small.hip: whole factor per workgroup (N <= IPMZ_SMALL_NMAX, nbi = 64;
 // W: N x 64 per QP)
 #define IPMZ_SMALL_NMAX 1024

@@ -19,6 +19,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "diag64.h"
+#include "sync.h"
 
 namespace ipmz {
 
@@ -45,6 +46,17 @@ __device__ __forceinline__ void tile_fetch(const double* __restrict__ src, int64
   for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
     const int rr = wave + SNW * i;
     v[i] = src[(int64_t)(rr < nrows ? rr : 0) * lds + lane];
+  }
+}
+// the same with agent-scope loads (data another workgroup of the launch wrote)
+template <int SNW>
+__device__ __forceinline__ void tile_fetch_sc(const double* __restrict__ src, int64_t lds, int nrows,
+                                              double (&v)[Cfg<SNW>::SFR]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
+    const int rr = wave + SNW * i;
+    v[i] = ld_sc1(&src[(int64_t)(rr < nrows ? rr : 0) * lds + lane]);
   }
 }
 template <int SNW>
@@ -197,9 +209,176 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_kernel(double* __restrict
   }
 }
 
+// ---------------------------------------------------------------------------
+// The same factor with TWO workgroups per QP, for batches that leave CUs
+// idle (2B <= #CU: C4's 128 QPs per GPU at 8 GPUs; N = 320, B = 128: 194 ->
+// 177 us -- the five 64-column diagonal blocks, ~15 us each, stay on one
+// chain).  Role 0 carries the
+// critical path -- the diagonal block J, the TRSM of every chunk below it and
+// the trailing tiles of column J+1 (which hold the next diagonal block and
+// the next TRSM's operands) -- and role 1, on another CU, the rest of the
+// trailing update of step J (columns J+2..), in the shadow of role 0's next
+// diagonal factor.  Hand-offs per step (sync.h protocol: write-through
+// stores, vmcnt drain, barrier, one flag store; consumers poll and read with
+// agent-scope loads):
+//   LW[J]    role 0 -> 1: L(c, J) in K and W(c, J) (parity J & 1 of the
+//            two W buffers) for every chunk c > J
+//   DONE[J]  role 1 -> 0: step J's tiles of columns >= J+2 stored (role 0
+//            needs column J+2 of them at step J+1)
+// Each element keeps the single-workgroup kernel's arithmetic (the same MFMA
+// tiles in the same order), so the factor is identical to it.
+template <int SNW>
+__global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __restrict__ K, int64_t ld, int N,
+                                                              double* __restrict__ D, double* __restrict__ Linv,
+                                                              double* __restrict__ W, int* __restrict__ info,
+                                                              int64_t sK, int64_t sD, int64_t sL, int64_t sW,
+                                                              unsigned* __restrict__ flags, unsigned* __restrict__ err) {
+  constexpr int SFR = Cfg<SNW>::SFR, SNN = Cfg<SNW>::SNN;
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
+  __shared__ unsigned sh_ok;
+  const int64_t qp = blockIdx.x >> 1;
+  const int role = blockIdx.x & 1;
+  K += qp * sK;
+  D += qp * sD;
+  Linv += qp * sL;
+  W += qp * sW;  // two N x 64 row-major buffers (parity of J): W = L D of block column J
+  unsigned* LW = flags + qp * IPMZ_PAIR_FLAGS;
+  unsigned* DONE = LW + IPMZ_PAIR_FLAGS / 2;
+  const int lane = threadIdx.x & 63;
+  const int r0 = tile_r0(), n0 = tile_n0<SNW>();
+  double* As = smem;
+  double* Bs = smem + 64 * DS;
+  const int nblk = (N + 63) / 64;
+  auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
+  auto Wj = [&](int J) { return W + (int64_t)(J & 1) * N * 64; };
+  // tiles (c, q), c >= q, for q in [qlo, qhi], in row order, -= L(c, J) W_q^T;
+  // operands of the next tile loaded while the current one computes.  All
+  // global traffic agent-scope: L / W come from role 0, tiles of column J+2
+  // go to it.
+  auto trail = [&](int J, int qlo, int qhi) {
+    if (qlo > qhi || qlo >= nblk) return;
+    const double* Wb = Wj(J);
+    double v[SFR], u[SFR];
+    int c = qlo, q = qlo;
+    tile_fetch_sc<SNW>(K + (int64_t)(64 * c) * ld + 64 * J, ld, nrows(c), v);  // L[c, J]
+    tile_fetch_sc<SNW>(Wb + (int64_t)(64 * q) * 64, 64, nrows(q), u);           // W_q
+    for (;;) {
+      const int rows = nrows(c);
+      if (q == qlo) tile_put<SNW>(As, rows, v);
+      tile_put<SNW>(Bs, nrows(q), u);
+      acc_t acc[SNN], cv[SNN];
+      const bool diag = q == c;
+      double* Ct = K + (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
+      const double* Ct0 = K + (int64_t)(64 * c) * ld + 64 * q;
+      const int64_t ld4 = 4 * ld;
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+        acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          const bool in = row < rows && (!diag || col <= row);
+          cv[n][g] = ld_sc1(in ? Ct + g * ld4 + 16 * n : Ct0);
+        }
+      }
+      __syncthreads();
+      int cn = c, qn = q + 1;
+      if (qn > cn || qn > qhi) {
+        ++cn;
+        qn = qlo;
+      }
+      const bool more = cn < nblk;
+      if (more) {
+        if (qn == qlo) tile_fetch_sc<SNW>(K + (int64_t)(64 * cn) * ld + 64 * J, ld, nrows(cn), v);
+        tile_fetch_sc<SNW>(Wb + (int64_t)(64 * qn) * 64, 64, nrows(qn), u);
+      }
+      tile_mma<SNW, true>(As, Bs, acc);
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          if (row < rows && (!diag || col <= row)) st_sc1(Ct + g * ld4 + 16 * n, cv[n][g] + acc[n][g]);
+        }
+      }
+      __syncthreads();
+      if (!more) break;
+      c = cn;
+      q = qn;
+    }
+  };
+  if (role == 1) {
+    for (int J = 0; J + 2 < nblk; ++J) {
+      if (!wait_flag(&LW[J], err, &sh_ok)) return;
+      trail(J, J + 2, nblk - 1);
+      publish(&DONE[J]);
+    }
+    return;
+  }
+  for (int J = 0; J < nblk; ++J) {
+    const int J0 = 64 * J;
+    // block J was last updated by this workgroup (column J+1 of step J-1) or
+    // before the DONE[J-2] wait of step J-1 (agent-scope loads: LSC)
+    diag64_body<false, true, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
+                                                 smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
+    if (J == nblk - 1) break;
+    __syncthreads();
+    // ---- TRSM of every chunk below, published for role 1
+    double v[SFR];
+    tile_fetch_sc<SNW>(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    const double* dsh = smem + 2 * 64 * DS;
+    double* Wb = Wj(J);
+    double rd[SNN];
+#pragma unroll
+    for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / dsh[16 * (n0 + n) + (lane & 15)];
+    for (int c = J + 1; c < nblk; ++c) {
+      const int rows = nrows(c);
+      tile_put<SNW>(As, rows, v);
+      __syncthreads();
+      if (c + 1 < nblk) tile_fetch_sc<SNW>(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
+      acc_t acc[SNN];
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
+      tile_mma<SNW, false, true>(As, Bs, acc);
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          if (row < rows) {
+            st_sc1(&Wb[(int64_t)(64 * c + row) * 64 + col], acc[n][g]);
+            st_sc1(&K[(int64_t)(64 * c + row) * ld + J0 + col], acc[n][g] * rd[n]);
+          }
+        }
+      }
+      __syncthreads();
+    }
+    publish(&LW[J]);
+    // ---- column J+1 of the trailing update (the next diagonal block and the
+    // next TRSM's operands), after role 1's step J-1 (it updated column J+1)
+    if (J >= 1 && !wait_flag(&DONE[J - 1], err, &sh_ok)) return;
+    trail(J, J + 1, J + 1);
+  }
+}
+
+// 2B workgroups must all be resident at once to help: 256 VGPRs per lane x 8
+// waves fill a CU, so one workgroup per CU -- 2B <= #CU (B = 128 at 8 GPUs)
+bool small_pair_eligible(int B, int N) { return 2 * B <= device_cus() && N > 64 && N <= IPMZ_SMALL_NMAX; }
+
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs) {
   if (N <= 0 || bs.B <= 0) return hipSuccess;
+  // a batch that leaves CUs idle: two workgroups per QP (flags zeroed here)
+  if (bs.pflags && small_pair_eligible(bs.B, N)) {
+    hipError_t e = hipMemsetAsync(bs.pflags, 0, ((size_t)bs.B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ldlt_small_pair_kernel<8>, dim3(2 * bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info,
+                       bs.sK, bs.sD, bs.sL, bs.sW, bs.pflags, bs.pflags + (size_t)bs.B * IPMZ_PAIR_FLAGS);
+    return hipGetLastError();
+  }
   // 8 waves (two per SIMD) also when the batch leaves a CU per QP: 16 waves
   // measured slower (N = 320, B = 128: 249 vs 190 us)
   hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
