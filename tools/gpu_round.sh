@@ -29,12 +29,12 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmc_fetch) step pmc_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     pmc_write) step pmc_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline ;;
     # factor-phase counters of ONE bench step (tools/pmc_factor.py), one counter group per pass
-    pmcf_fetch) step pmcf_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmcf_fetch" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
-    pmcf_write) step pmcf_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmcf_write" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_fetch) step ${PMCW:-c3}_pmcf_fetch 240 rocprofv3 --pmc FETCH_SIZE -d "$OUT/${PMCW:-c3}_pmcf_fetch" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_write) step ${PMCW:-c3}_pmcf_write 240 rocprofv3 --pmc WRITE_SIZE -d "$OUT/${PMCW:-c3}_pmcf_write" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     # (two small passes: one 4-counter pass slows every dispatch enough that the
     # panel path's cross-launch hand-offs can time out under the profiler)
-    pmcf_mops) step pmcf_mops 240 rocprofv3 --pmc SQ_INSTS_VALU_MFMA_MOPS_F64 -d "$OUT/pmcf_mops" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
-    pmcf_busy) step pmcf_busy 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d "$OUT/pmcf_busy" -o run --output-format csv -- python bench.py --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_mops) step ${PMCW:-c3}_pmcf_mops 240 rocprofv3 --pmc $([ "${PMCW:-c3}" = c5 ] && echo SQ_INSTS_VALU_MFMA_MOPS_F32 || echo SQ_INSTS_VALU_MFMA_MOPS_F64) -d "$OUT/${PMCW:-c3}_pmcf_mops" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    pmcf_busy) step ${PMCW:-c3}_pmcf_busy 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d "$OUT/${PMCW:-c3}_pmcf_busy" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;

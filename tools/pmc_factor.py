@@ -13,7 +13,8 @@ The factor phase = every launch of the factor's kernels (trailing / strip
 GEMMs, the panel chain and rows launches, the solve prep).  Corrections
 (MI355X_MICROARCH.md, HBM / PMC): FETCH_SIZE and WRITE_SIZE are KiB,
 FETCH_SIZE reports half the bytes of a 16-B/lane read on gfx950 (doubled);
-SQ_INSTS_VALU_MFMA_MOPS_F64 counts 512-flop units.
+SQ_INSTS_VALU_MFMA_MOPS_F64 / _F32 count 512-flop units (C5's fp32 factor:
+the _F32 counter in the mops pass, PMCW=c5 in tools/gpu_round.sh).
 
     python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir[,dir...]> <label> <N> > profiles/factor_traffic_c3.json
 
@@ -59,13 +60,15 @@ def main():
         fb = 2.0 * fetch[k].get("FETCH_SIZE", 0.0) * 1024
         wb = write[k].get("WRITE_SIZE", 0.0) * 1024
         mops = mfma[k].get("SQ_INSTS_VALU_MFMA_MOPS_F64", 0.0)
+        mops32 = mfma[k].get("SQ_INSTS_VALU_MFMA_MOPS_F32", 0.0)
         row = {"launches": nf.get(k, 0), "fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
-               "f64_mfma_flops": 512.0 * mops,
+               "f64_mfma_flops": 512.0 * mops, "f32_mfma_flops": 512.0 * mops32,
                "mfma_busy_cycles": mfma[k].get("SQ_VALU_MFMA_BUSY_CYCLES", 0.0),
                "grbm_gui_active": mfma[k].get("GRBM_GUI_ACTIVE", 0.0),
                "busy_cu_cycles": mfma[k].get("SQ_BUSY_CU_CYCLES", 0.0)}
         rows[k] = row
-        for f in ("fetch_bytes", "write_bytes", "hbm_bytes", "f64_mfma_flops", "mfma_busy_cycles", "busy_cu_cycles"):
+        for f in ("fetch_bytes", "write_bytes", "hbm_bytes", "f64_mfma_flops", "f32_mfma_flops", "mfma_busy_cycles",
+                  "busy_cu_cycles"):
             tot[f] += row[f]
     alg_flops = N ** 3 / 3.0
     out = {
@@ -74,8 +77,10 @@ def main():
         "factor_traffic_bytes_per_step": tot["hbm_bytes"],
         "mfma": {
             "f64_mfma_flops_per_step": tot["f64_mfma_flops"],
+            "f32_mfma_flops_per_step": tot["f32_mfma_flops"],
             "algorithmic_flops_per_step": alg_flops,
-            "executed_over_algorithmic": tot["f64_mfma_flops"] / alg_flops if alg_flops else None,
+            "executed_over_algorithmic": ((tot["f64_mfma_flops"] + tot["f32_mfma_flops"]) / alg_flops
+                                          if alg_flops else None),
             "mfma_busy_cycles": tot["mfma_busy_cycles"],
             "busy_cu_cycles": tot["busy_cu_cycles"],
             "mfma_busy_over_busy_cu": (tot["mfma_busy_cycles"] / tot["busy_cu_cycles"]
