@@ -244,8 +244,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       T* Lb = Lb0 + (int64_t)j * 64 * 64;
       if (j == 0 && !Wprev) diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
       else diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
-      if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);  // inject: the timeout tests only
-      if (j + 1 >= nb) break;
+      if (j + 1 >= nb) {
+        if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);
+        break;
+      }
       // ---- block row c = j + 1: (c, j) and (c, c) from helper c
       const int c = j + 1, r0 = k0 + 64 * c, rows = bsz(c);
       if (!wait_flag(&area[OP_READY + c], err, &sh_ok)) return;
@@ -253,6 +255,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       stage_tile<T, true>(reinterpret_cast<T*>(M), K + (int64_t)r0 * ld + j0, ld, rows, 64);
       acc_t own[4];
       load_acc<T, true, true>(own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
+      // DIAG[j] after these loads: the diagonal block's write-back drains beside
+      // them instead of on the chain (nothing this workgroup waits for needs
+      // DIAG[j]: helper c only uses blocks <= c - 2).  inject: timeout tests only
+      if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);
       T rd[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
@@ -273,7 +279,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
         for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
       store_acc<T, false, false>(lacc, Lrow, ld, rows, 64);
       store_acc<T, true, false>(acc, Wrow, ldw, rows, 64);
-      publish(&area[OP_REG + j * OP_NBMAX + c]);  // W(c, j): helpers' and the rows kernel's strips
       // own update (c, c) -= L(c, j) W(c, j)^T: L into X, W into M (both free:
       // L_jj is in K, X_jj no longer needed)
       T* Lx = reinterpret_cast<T*>(X);
@@ -282,7 +287,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       put_acc<T>(Wm, acc);
       __syncthreads();
       mma_tile<T, true>(Lx, [&](int r, int k) { return Wm[r * DS + k]; }, own);
-      __syncthreads();  // every wave done reading M and X
+      // W(c, j) for the helpers' and the rows kernel's strips: published after
+      // the update, so the stores drain beside its MFMAs (publish's barrier
+      // also ends every wave's reads of M and X)
+      publish(&area[OP_REG + j * OP_NBMAX + c]);
       // the next diagonal block, straight into diag64_body's image
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
