@@ -1018,8 +1018,13 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
                            : i < nm ? q.A + (int64_t)(ah ? i - n - m : i - n) * q.ldn : q.C + (int64_t)(i - nm) * q.ldn;
         const bool neg = q.naive && i >= n && i < n + m;
         const int lim = i < n ? i : n;  // source columns [0, lim); zeros in [n, i)
-        if (j < lim) v0[k] = neg ? -src[j] : src[j];
-        if (j + 1 < lim) v1[k] = neg ? -src[j + 1] : src[j + 1];
+        if (j + 1 < lim) {  // one 16-byte load (ldn and j even)
+          const double2 t = *reinterpret_cast<const double2*>(src + j);
+          v0[k] = neg ? -t.x : t.x;
+          v1[k] = neg ? -t.y : t.y;
+        } else if (j < lim) {
+          v0[k] = neg ? -src[j] : src[j];
+        }
       }
     }
 #pragma unroll
@@ -1027,8 +1032,8 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
       const int u = u0 + k, i = u / nch, j = (u % nch) * 128 + 2 * lane;
       if (u < units) {
         double* Kr = q.K + (int64_t)i * q.ldk;
-        if (j < i) Kr[j] = v0[k];
-        if (j + 1 < i) Kr[j + 1] = v1[k];
+        if (j + 1 < i) *reinterpret_cast<double2*>(Kr + j) = make_double2(v0[k], v1[k]);  // ldk even
+        else if (j < i) Kr[j] = v0[k];
       }
     }
   }
