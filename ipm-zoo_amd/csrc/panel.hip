@@ -68,6 +68,25 @@ __device__ __forceinline__ void mma_tile(const T* As, BF bf, typename Mfma<T>::a
   }
 }
 
+// acc[n] += A[16w.., :] B[16n.., :]^T for a LOWER-triangular B (the diagonal
+// block's inverse): k-chunks past column block n's diagonal are zero and
+// skipped (40 of 64 MFMAs per wave), the diagonal chunk masked through bf.
+// The chain's TRSM step: 4.5 -> 2.5 us per block (kbench chain clocks).
+template <typename T, typename BF>
+__device__ __forceinline__ void mma_tile_lower(const T* As, BF bf, typename Mfma<T>::acc_t (&acc)[4]) {
+  typedef Mfma<T> MF;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int arow = 16 * wave + (lane & 15);
+#pragma unroll
+  for (int s = 0; s < 16; ++s) {
+    const int k = 4 * s + (lane >> 4);
+    const T a = As[arow * DS + k];
+#pragma unroll
+    for (int n = 0; n < 4; ++n)
+      if (s < 4 * (n + 1)) acc[n] = MF::mma(a, bf(16 * n + (lane & 15), k), acc[n]);
+  }
+}
+
 // 64 x 64 tile of a row-major matrix (ld) into LDS (rows < rows, columns <
 // cols; zeros elsewhere): 16 loads in flight per thread.  SC: agent-scope
 // loads (data written earlier in this launch, possibly by another CU).
@@ -267,8 +286,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       // LDS is not meaningful: masked)
       acc_t acc[4];
       zero_acc<T>(acc);
-      mma_tile<T, false>(reinterpret_cast<const T*>(M), [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); },
-                         acc);
+      mma_tile_lower<T>(reinterpret_cast<const T*>(M), [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); },
+                        acc);
       __syncthreads();  // M and X reads done
       T* Lrow = K + (int64_t)r0 * ld + j0;
       T* Wrow = Wp + (int64_t)r0 * ldw + 64 * j;
@@ -351,7 +370,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     __syncthreads();
     acc_t acc[4];
     zero_acc<T>(acc);
-    mma_tile<T, false>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
+    mma_tile_lower<T>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);  // L_jj^{-1}: lower
     __syncthreads();
     acc_t lacc[4];
 #pragma unroll
@@ -438,7 +457,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     __syncthreads();
     acc_t acc[4];
     zero_acc<T>(acc);
-    mma_tile<T, false>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
+    mma_tile_lower<T>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);  // L_jj^{-1}: lower
     __syncthreads();
     acc_t lacc[4];
 #pragma unroll
