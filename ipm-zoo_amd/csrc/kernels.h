@@ -68,9 +68,11 @@ hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float
                        hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
                        unsigned* pctrl = nullptr);
 // ctrl words of the panel path: a shared area (sticky error word) + one
-// area per outer panel
+// area per outer panel, then two 64 x 64 (8-byte) tiles: the next panel's
+// block (0, 0) look-ahead update, pre-accumulated by the rows launch
+#define IPMZ_PANEL_PRE00_WORDS (2 * 64 * 64 * 2)
 inline int64_t panel_ctrl_words(int N, int nbo) {
-  return (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + (N + nbo - 1) / nbo);
+  return (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + (N + nbo - 1) / nbo) + IPMZ_PANEL_PRE00_WORDS;
 }
 // one outer panel [k0, k0 + bo) of the panel path (panel.hip): the chain
 // launch on st_chain, the rows launch on st_rows (flags in `area`, sticky
@@ -80,9 +82,11 @@ inline int64_t panel_ctrl_words(int N, int nbo) {
 // [kprev, kprev + boprev) (W_prev rows, ld ldw) to the panel's diagonal
 // region (and, rows_prev, the rows launch to its rows).
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
+                        const double* pre00_in, double* pre00_out,
                         int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
                         bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
+                        const float* pre00_in, float* pre00_out,
                         int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
                         bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);

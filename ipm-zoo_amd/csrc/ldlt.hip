@@ -394,10 +394,15 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   auto area = [&](int k) { return pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + k); };
   unsigned* err = pctrl ? pctrl + PANEL_ERR_WORD : nullptr;
   hipStream_t sC = (two && fused) ? st3 : st;  // rows launches
+  // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
+  // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
+  T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
+  auto slot00 = [&](int k) { return pre00 + (int64_t)(k & 1) * 64 * 64; };
   auto factor = [&](int k, bool prev) -> hipError_t {  // panel k (prev: with the look-ahead update from k - 1)
     const int k0 = k * nbo;
     if (!fused) return factor_panel(K, ld, N, D, Linv, Wb(k), k0, pw(k), nbo, nbi, info, st);
-    return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo, info, area(k), err,
+    return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo,
+                        (two && prev) ? slot00(k) : nullptr, two ? slot00(k + 1) : nullptr, info, area(k), err,
                         prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC);
   };
   hipError_t e = hipSuccess;

@@ -218,7 +218,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
                                                           T* __restrict__ D, T* __restrict__ Lb0, T* __restrict__ Wp,
                                                           int ldw, int* __restrict__ info, unsigned* __restrict__ area,
                                                           unsigned* __restrict__ err, int inject,
-                                                          const T* __restrict__ Wprev, int kprev, int boprev) {
+                                                          const T* __restrict__ Wprev, int kprev, int boprev,
+                                                          const T* __restrict__ pre00) {
   typedef Mfma<T> MF;
   typedef typename MF::acc_t acc_t;
   // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
@@ -243,9 +244,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     // ================================================================ CHAIN
     if (Wprev) {  // block (0, 0) with the previous panel's update, straight into M
       acc_t own[4];
-      zero_acc<T>(own);
-      prev_update<T>(own, Wprev + (int64_t)k0 * ldw, ldw, K + (int64_t)k0 * ld + kprev, ld, bsz(0), bsz(0), boprev,
-                     reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+      if (pre00) {
+        // accumulated by the previous panel's rows launch (the same MFMA
+        // order as prev_update), so this launch starts with the diagonal factor
+        load_acc<T, false, false>(own, pre00, 64, 64, 64);
+      } else {
+        zero_acc<T>(own);
+        prev_update<T>(own, Wprev + (int64_t)k0 * ldw, ldw, K + (int64_t)k0 * ld + kprev, ld, bsz(0), bsz(0), boprev,
+                       reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+      }
       acc_t a0[4];
       load_acc<T, false, true>(a0, K + (int64_t)k0 * ld + k0, ld, bsz(0), bsz(0));
 #pragma unroll
@@ -409,7 +416,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
                                                          const T* __restrict__ D, const T* __restrict__ Lb0,
                                                          T* __restrict__ Wp, int ldw, unsigned* __restrict__ area,
                                                          unsigned* __restrict__ err, const T* __restrict__ Wprev,
-                                                         int ldwp, int kprev, int boprev) {
+                                                         int ldwp, int kprev, int boprev, T* __restrict__ pre00) {
   typedef Mfma<T> MF;
   typedef typename MF::acc_t acc_t;
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS];
@@ -439,7 +446,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
     }
   }
-  // ---- TRSMs and strips of this chunk's rows
+  // ---- TRSMs and strips of this chunk's rows.  Chunk 0 (the next panel's
+  // first 64 rows) also accumulates that panel's block (0, 0) look-ahead
+  // update W(rows, j) L(rows, j)^T over j -- exactly the chunks prev_update
+  // would sum in the next chain launch -- and leaves it in pre00.
+  T* const p00 = blockIdx.x == 0 ? pre00 : nullptr;
+  acc_t a00[4];
+  zero_acc<T>(a00);
   bool ok = true;
   for (int j = 0; j < nb && ok; ++j) {
     const int j0 = k0 + 64 * j, bj = bsz(j);
@@ -467,6 +480,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     store_acc<T, false, false>(lacc, Krow + j0, ld, rows, bj);
     store_acc<T, false, false>(acc, Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
     put_acc<T>(As, lacc);
+    if (p00) {  // a00 += W(rows, j) L(rows, j)^T (W staged in Bs, L in As)
+      put_acc<T>(Bs, acc);
+      __syncthreads();
+      mma_tile<T, false>(Bs, [&](int r, int k) { return As[r * DS + k]; }, a00);
+      __syncthreads();  // Bs is reused by the strips
+    }
     // strips: (rows, q) -= L(rows, j) W(q, j)^T, q = j+1 .. nb-1
     for (int q = j + 1; q < nb; ++q) {
       const int q0 = k0 + 64 * q, qrows = bsz(q);
@@ -480,11 +499,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       __syncthreads();
     }
   }
+  if (p00 && ok) store_acc<T, false, false>(a00, p00, 64, 64, 64);  // consumed by a later launch
 }
 
 // ---------------------------------------------------------------------------
 template <typename T>
-static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw, int* info,
+static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw,
+                                 const T* pre00_in, T* pre00_out, int* info,
                                  unsigned* area, unsigned* err, const T* Wprev, int kprev, int boprev, bool rows_prev,
                                  hipStream_t st_chain, hipStream_t st_rows) {
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
@@ -494,24 +515,30 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   // diagonal block (0, 0) when the look-ahead update is applied here)
   const int nwork = Wprev ? nb * (nb + 1) / 2 - 1 : 0;
   hipLaunchKernelGGL(panel_chain_kernel<T>, dim3(nb + nwork), dim3(256), 0, st_chain, K, ld, N, k0, ce, D, Lb0, Wp, ldw, info,
-                     area, err, debug_inject_mask() & IPMZ_INJECT_PANEL, Wprev, kprev, boprev);
+                     area, err, debug_inject_mask() & IPMZ_INJECT_PANEL, Wprev, kprev, boprev,
+                     Wprev ? pre00_in : nullptr);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || ce >= N) return e;
   const int nch = (N - ce + 63) / 64;
   hipLaunchKernelGGL(panel_rows_kernel<T>, dim3(nch), dim3(256), 0, st_rows, K, ld, N, k0, ce, (const T*)D,
-                     (const T*)Lb0, Wp, ldw, area, err, rows_prev ? Wprev : nullptr, ldw, kprev, boprev);
+                     (const T*)Lb0, Wp, ldw, area, err, rows_prev ? Wprev : nullptr, ldw, kprev, boprev,
+                     pre00_out);
   return hipGetLastError();
 }
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
-                        int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
-                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows) {
-  return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, area, err, Wprev, kprev, boprev, rows_prev,
+                        const double* pre00_in, double* pre00_out, int* info, unsigned* area, unsigned* err,
+                        const double* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
+                        hipStream_t st_rows) {
+  return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
+                              boprev, rows_prev,
                                 st_chain, st_rows);
 }
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
-                        int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
-                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows) {
-  return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, info, area, err, Wprev, kprev, boprev, rows_prev,
+                        const float* pre00_in, float* pre00_out, int* info, unsigned* area, unsigned* err,
+                        const float* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
+                        hipStream_t st_rows) {
+  return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
+                              boprev, rows_prev,
                                st_chain, st_rows);
 }
 
