@@ -42,3 +42,11 @@ for N in [int(a) for a in sys.argv[1:]] or [1024, 4096, 11264]:
         gb = N ** 3 / 6 * 16 / 1e9
         print(f"bk {name:9s} N={N:6d}: {best * 1e3:9.2f} ms  ({gb / best:.0f} GB/s algorithmic, "
               f"{best / N * 1e6:.2f} us per pivot step)", flush=True)
+    # the solve (one workgroup, LinearSolvers.cpp:209-318) on the last factor
+    b = torch.ones(N, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    ctx.bk_solve(N, A.data_ptr(), N, piv.data_ptr(), b.data_ptr())
+    torch.cuda.synchronize()
+    ts = time.perf_counter() - t
+    print(f"bk solve     N={N:6d}: {ts * 1e3:9.2f} ms", flush=True)
