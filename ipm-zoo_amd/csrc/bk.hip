@@ -375,9 +375,10 @@ IPMZ_HOST_DEVICE Layout layout(int n, int G) {
 // of a 1x1 / 2x2 pivot at column k (lo = k + mode), with the interchange of
 // rows / columns kk = lo - 1 and kp when swap.
 struct Pass {
-  int mode, k, lo, kp;
+  int mode, k, lo, kp;  // mode 3: two 1x1 pivots k, k+1 without interchange in one pass (lo = k + 2)
   bool swap;
   double r, d11, d22, d21;
+  double r1, s01, d1;  // mode 3: 1 / a'(k+1,k+1), r a(k+1,k), a'(k+1,k+1) (a' = after step k)
   const double *ck0, *ck1, *prow, *pcol;  // staged pre-interchange columns k, k+1; row / column i_max
   double *nb0, *nb1;                      // staging out: columns lo, lo+1
   double* cpv;                            // this workgroup's (max, argmax) slot of column lo
@@ -415,6 +416,7 @@ __device__ void pass(double* __restrict__ A, int64_t ld, int n, const Pass& P, d
       const int i = g + q * G;
       rc0[q] = c0v(P, i);
       if (P.mode == 2) rc1[q] = c1v(P, i);
+      if (P.mode == 3) rc1[q] = ld_sc1(P.ck1 + i) - P.s01 * rc0[q];  // a(i,k+1) after step k
       if (P.swap && i > P.kp) rsub[q] = ld_sc1(ckS + i);  // a(i, kp) <- a(i, kk)
     }
   }
@@ -426,9 +428,17 @@ __device__ void pass(double* __restrict__ A, int64_t ld, int n, const Pass& P, d
     if (tid == (k & (T - 1))) {
       if (P.mode == 1 && P.swap && k % G == g) A[(int64_t)k * ld + k] = ld_sc1(P.prow + P.kp);
       if (P.mode == 2 && P.swap && (k + 1) % G == g) A[(int64_t)(k + 1) * ld + k] = ld_sc1(P.prow + k);
+      if (P.mode == 3 && (k + 1) % G == g) A[(int64_t)(k + 1) * ld + k] = ld_sc1(P.ck0 + k + 1) * P.r;
       for (int q = q_lo; q < nq; ++q) {
         const int i = g + q * G;
-        A[(int64_t)i * ld + k] = P.mode == 1 ? rc0[q] * P.r : P.d21 * (P.d11 * rc0[q] - rc1[q]);
+        A[(int64_t)i * ld + k] = P.mode != 2 ? rc0[q] * P.r : P.d21 * (P.d11 * rc0[q] - rc1[q]);
+      }
+    }
+    if (P.mode == 3 && tid == ((k + 1) & (T - 1))) {  // step k+1's pivot and L column
+      if ((k + 1) % G == g) A[(int64_t)(k + 1) * ld + k + 1] = P.d1;
+      for (int q = q_lo; q < nq; ++q) {
+        const int i = g + q * G;
+        A[(int64_t)i * ld + k + 1] = rc1[q] * P.r1;
       }
     }
     if (P.mode == 2 && tid == ((k + 1) & (T - 1))) {
@@ -447,6 +457,10 @@ __device__ void pass(double* __restrict__ A, int64_t ld, int n, const Pass& P, d
     double w0 = 0.0, w1 = 0.0, subj = 0.0;
     if (P.mode == 1) {
       w0 = P.r * c0v(P, j);
+    } else if (P.mode == 3) {
+      const double a0 = ld_sc1(P.ck0 + j);
+      w0 = P.r * a0;
+      w1 = P.r1 * (ld_sc1(P.ck1 + j) - P.s01 * a0);  // r1 a'(j,k+1)
     } else if (P.mode == 2) {
       const double a0 = c0v(P, j), a1 = c1v(P, j);
       w0 = P.d21 * (P.d11 * a0 - a1);
@@ -473,7 +487,10 @@ __device__ void pass(double* __restrict__ A, int64_t ld, int n, const Pass& P, d
           else if (i > P.kp && j == P.kp) x = rsub[q + u];
         }
         if (P.mode == 1) x = x - w0 * rc0[q + u];  // a(i,j) -= (r a(j,k)) a(i,k)
-        else if (P.mode == 2) x = x - (rc0[q + u] * w0 + rc1[q + u] * w1);
+        else if (P.mode == 3) {                     // step k, then step k+1 on the updated values
+          x = x - w0 * rc0[q + u];
+          x = x - w1 * rc1[q + u];
+        } else if (P.mode == 2) x = x - (rc0[q + u] * w0 + rc1[q + u] * w1);
         if (P.mode) A[(int64_t)i * ld + j] = x;
         if (stage0) {
           st_sc1(P.nb0 + i, x);
@@ -639,9 +656,51 @@ __global__ __launch_bounds__(bkg::T) void k_bk_grid(double* __restrict__ A, int6
         step = 2;
       }
     }
+    // ---- pivot k+1 from the staged columns: when step k is a 1x1 pivot
+    // without interchange, column k+1 after step k is ck1 - (r a(k+1,k)) ck0
+    // (the reference's own update expression), so its column search and
+    // pivot test need no pass; if it is a 1x1 pivot without interchange too,
+    // both updates run in ONE pass (each element updated by step k, then by
+    // step k+1 -- the reference's order), halving the trailing traffic.
+    bool pair = false;
+    double r0 = 0.0, s01 = 0.0, d1 = 0.0;
+    if (!zero_col && step == 1 && kp == k && k + 1 < n) {
+      r0 = 1.0 / ld_sc1(ck0 + k);
+      s01 = r0 * ld_sc1(ck0 + k + 1);
+      double v = 0.0, cmax1 = 0.0;
+      int ix = 0x7fffffff, imax1 = 0;
+      for (int i = k + 2 + tid; i < n; i += T) {
+        const double t = fabs(ld_sc1(ck1 + i) - s01 * ld_sc1(ck0 + i));
+        if (t > v) {
+          v = t;
+          ix = i;
+        }
+      }
+      block_argmax(v, ix, sv, si, cmax1, imax1);
+      d1 = ld_sc1(ck1 + k + 1) - s01 * ld_sc1(ck0 + k + 1);
+      const double akk1 = fabs(d1);
+      pair = !(akk1 == 0.0 && cmax1 == 0.0) && akk1 >= alpha * cmax1;
+    }
     if (g == 0 && tid == 0) {
       if (step == 1) ipiv[k] = kp;
       else ipiv[k] = ipiv[k + 1] = -kp;
+      if (pair) ipiv[k + 1] = k + 1;
+    }
+    if (pair) {
+      Pass P{};
+      P.mode = 3;
+      P.k = k;
+      P.lo = k + 2;
+      P.kp = k;
+      P.ck0 = ck0;
+      P.ck1 = ck1;
+      P.r = r0;
+      P.s01 = s01;
+      P.d1 = d1;
+      P.r1 = 1.0 / d1;
+      ok = run(P);
+      k += 2;
+      continue;
     }
     if (zero_col) {  // no interchange, no update: stage the next column
       if (k + 1 < n) ok = stage(k + 1);
