@@ -226,6 +226,10 @@ __global__ __launch_bounds__(BKT) void k_bk_factor(double* __restrict__ Ab, int6
   if (tid == 0) infob[blockIdx.x] = info;
 }
 
+// TRANS: the factor's lower triangle as its transpose LT (row j of LT =
+// column j of L, contiguous; ld = the row stride of LT): every column access of
+// the sweeps is then one coalesced row instead of a cache line per element
+template <bool TRANS>
 __global__ __launch_bounds__(BKT) void k_bk_solve(const double* __restrict__ Lb, int64_t ld, int n, int64_t sA,
                                                   const int* __restrict__ ipivb, int64_t sP, double* __restrict__ bb,
                                                   int64_t sb) {
@@ -234,7 +238,7 @@ __global__ __launch_bounds__(BKT) void k_bk_solve(const double* __restrict__ Lb,
   const int* ipiv = ipivb + blockIdx.x * sP;
   double* b = bb + blockIdx.x * sb;
   const int tid = threadIdx.x;
-  auto l = [&](int i, int j) { return L[(int64_t)i * ld + j]; };
+  auto l = [&](int i, int j) { return TRANS ? L[(int64_t)j * ld + i] : L[(int64_t)i * ld + j]; };
   auto swapb = [&](int p, int q) {
     if (tid == 0) {
       const double t = b[p];
@@ -765,7 +769,37 @@ hipError_t bk_factor(double* A, int64_t ld, int n, int* ipiv, int* info, int fix
 hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double* b, int batch, int64_t sA, int64_t sP,
                     int64_t sb, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bk_solve, dim3(batch), dim3(BKT), 0, st, F, ld, n, sA, ipiv, sP, b, sb);
+  hipLaunchKernelGGL(k_bk_solve<false>, dim3(batch), dim3(BKT), 0, st, F, ld, n, sA, ipiv, sP, b, sb);
+  return hipGetLastError();
+}
+
+// LT[j][i] = F[i][j], i >= j (64 x 64 tiles through LDS: coalesced both ways)
+__global__ __launch_bounds__(256) void k_bk_transpose(const double* __restrict__ F, int64_t ld, int n,
+                                                      double* __restrict__ LT, int64_t ldt) {
+  __shared__ double t[64][65];
+  const int bi = blockIdx.y, bj = blockIdx.x;  // source tile rows 64 bi.., columns 64 bj..
+  if (bj > bi) return;
+  const int c = threadIdx.x & 63;
+  for (int r = threadIdx.x >> 6; r < 64; r += 4) {
+    const int i = 64 * bi + r, j = 64 * bj + c;
+    t[r][c] = (i < n && j < n) ? F[(int64_t)i * ld + j] : 0.0;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x >> 6; r < 64; r += 4) {
+    const int j = 64 * bj + r, i = 64 * bi + c;  // LT row j, column i
+    if (j < n && i < n && i >= j) LT[(int64_t)j * ldt + i] = t[c][r];
+  }
+}
+
+hipError_t bk_transpose(const double* F, int64_t ld, int n, double* LT, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const int nb = (n + 63) / 64;
+  hipLaunchKernelGGL(k_bk_transpose, dim3(nb, nb), dim3(256), 0, st, F, ld, n, LT, (int64_t)n);
+  return hipGetLastError();
+}
+hipError_t bk_solve_lt(const double* LT, int n, const int* ipiv, double* b, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(k_bk_solve<true>, dim3(1), dim3(BKT), 0, st, LT, (int64_t)n, n, 0, ipiv, 0, b, 0);
   return hipGetLastError();
 }
 

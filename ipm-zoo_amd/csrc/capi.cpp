@@ -492,7 +492,17 @@ int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* 
   if (N == 0) return IPMZ_OK;  // LinearSolvers.cpp:212-214
   if (!F || !ipiv || !b) return fail(IPMZ_ERR_INVALID, "null pointer");
   HIP_OK(hipSetDevice(ctx->device));
-  HIP_OK(bk_solve(F, ld, N, ipiv, b, 1, 0, 0, 0, ctx->stream));
+  if (N < IPMZ_BK_GRID_MIN) {
+    HIP_OK(bk_solve(F, ld, N, ipiv, b, 1, 0, 0, 0, ctx->stream));
+    return IPMZ_OK;
+  }
+  // large N: through a transposed copy (coalesced column sweeps)
+  double* lt = nullptr;
+  HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&lt), (size_t)N * N * sizeof(double), ctx->stream));
+  hipError_t e = bk_transpose(F, ld, N, lt, ctx->stream);
+  if (e == hipSuccess) e = bk_solve_lt(lt, N, ipiv, b, ctx->stream);
+  hipFreeAsync(lt, ctx->stream);
+  HIP_OK(e);
   return IPMZ_OK;
 }
 
@@ -650,6 +660,7 @@ struct ipmz_qp {
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
   char* bkws = nullptr;  // the whole-device Bunch-Kaufman factor's workspace (B == 1, N >= IPMZ_BK_GRID_MIN)
+  double* bklt = nullptr;  // its factor transposed (N x N), for coalesced solves
   unsigned* pflags = nullptr;  // B > 1: the two-workgroup small factor's flags + sticky error word
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
@@ -725,7 +736,9 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
 QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
 
 int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
-  if (s->eqnone) {  // overwriting_solve_bunch_kaufman
+  if (s->eqnone && s->bklt) {  // overwriting_solve_bunch_kaufman on the transposed factor
+    HIP_OK(bk_solve_lt(s->bklt, s->N, s->ipiv, q0(s).b, st));
+  } else if (s->eqnone) {  // overwriting_solve_bunch_kaufman
     HIP_OK(bk_solve(s->K, s->ldk, s->N, s->ipiv, q0(s).b, s->B, s->sK, s->sP, s->sb, st));
   } else if (s->normal) {
     return normal_solve_impl(s->ctx, s->n, s->m + s->p, s->K, s->ldk, s->D,
@@ -748,6 +761,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   if (s->eqnone) {  // zero diagonal block: symmetric_indefinite_factorization (reference kp behaviour)
     if (s->bkws) {
       HIP_OK(bk_factor_grid(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->bkws, s->ctx->stream));
+      HIP_OK(bk_transpose(s->K, s->ldk, s->N, s->bklt, s->ctx->stream));
       return IPMZ_OK;
     }
     HIP_OK(bk_factor(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->B, s->sK, s->sP, s->ctx->stream));
@@ -991,6 +1005,9 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
       ok = hipMalloc(&w, bk_grid_ws_bytes(N)) == hipSuccess;
       if (ok) s->allocs.push_back(w);
       s->bkws = static_cast<char*>(w);
+      if (ok) ok = hipMalloc(&w, (size_t)N * N * sizeof(double)) == hipSuccess;
+      if (ok) s->allocs.push_back(w);
+      s->bklt = static_cast<double*>(w);
     }
   }
   if (!ok) {

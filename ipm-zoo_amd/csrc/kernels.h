@@ -160,6 +160,11 @@ hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double*
 size_t bk_grid_ws_bytes(int n);
 hipError_t bk_factor_grid(double* A, int64_t ld, int n, int* ipiv, int* info, int fix_kp, void* ws, hipStream_t st);
 const unsigned* bk_grid_err_word(const void* ws, int n);
+// one system's solve through a transposed copy of the factor's lower
+// triangle (LT: n x n doubles, row j = column j of L; bk_transpose once per
+// factor): coalesced sweeps, the same arithmetic as bk_solve
+hipError_t bk_transpose(const double* F, int64_t ld, int n, double* LT, hipStream_t st);
+hipError_t bk_solve_lt(const double* LT, int n, const int* ipiv, double* b, hipStream_t st);
 
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };
