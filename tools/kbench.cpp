@@ -130,15 +130,15 @@ int main(int argc, char** argv) {
   if (mode == "gvar") {  // trailing-GEMM tile variants: kbench N gvar v1 v2 ...
     for (int a = 3; a < argc; ++a) {
       const int var = std::atoi(argv[a]);
-      if (var >= 20) {  // strip: M rows x 384 columns, rank 384
-        for (int M : {3072, 6144, 8192, 10496}) {
-          CK(ipmz::gemm_nt_sub_variant(var, M, 384, 384, W, 384, K, ld, K + 384 * ld + 384, ld, st));
+      if (var >= 20) {  // strip: M rows x 512 columns, rank 512 (the look-ahead strips at nbo = 512)
+        for (int M : {3072, 6144, 8192, 10240}) {
+          CK(ipmz::gemm_nt_sub_variant(var, M, 512, 512, W, 512, K, ld, K + 512 * ld + 512, ld, st));
           t.start(st);
           for (int r = 0; r < 10; ++r)
-            CK(ipmz::gemm_nt_sub_variant(var, M, 384, 384, W, 384, K, ld, K + 384 * ld + 384, ld, st));
+            CK(ipmz::gemm_nt_sub_variant(var, M, 512, 512, W, 512, K, ld, K + 512 * ld + 512, ld, st));
           const float us = t.stop(st) / 10 * 1e3;
-          std::printf("gvar %2d strip M=%5d x 384 rank=384: %.1f us %.2f TFLOP/s\n", var, M, us,
-                      2.0 * M * 384 * 384 / us / 1e6);
+          std::printf("gvar %2d strip M=%5d x 512 rank=512: %.1f us %.2f TFLOP/s\n", var, M, us,
+                      2.0 * M * 512 * 512 / us / 1e6);
         }
         continue;
       }
@@ -152,6 +152,18 @@ int main(int argc, char** argv) {
           std::printf("gvar %2d R=%5d rank=%d: %.3f ms %.2f TFLOP/s\n", var, R, rank, ms,
                       (double)R * (R + 1) * rank / ms / 1e9);
         }
+    }
+    return 0;
+  }
+  if (mode == "sustain") {  // the trailing update back to back: clock / power drift over ~60 ms
+    const int rank = 512, R = N - 3 * rank;
+    for (int g = 0; g < 8; ++g) {
+      t.start(st);
+      for (int r = 0; r < 8; ++r)
+        CK(ipmz::gemm_nt_sub(R, R, rank, W, rank, K, ld, K + (int64_t)rank * ld + rank, ld, 0, 0, true, st));
+      const float ms = t.stop(st) / 8;
+      std::printf("sustain group %d R=%d rank=%d: %.3f ms %.2f TFLOP/s\n", g, R, rank, ms,
+                  (double)R * (R + 1) * rank / ms / 1e9);
     }
     return 0;
   }
@@ -170,7 +182,9 @@ int main(int argc, char** argv) {
   // factor: the look-ahead factor (panel path on a high-priority stream,
   // trailing updates on a low-priority one) and the persistent solve.
   // (Measured and dropped: CU masks reserving 8 / 16 / 32 CUs for the panel
-  // streams, a persistent trailing-GEMM grid of 248-512 workgroups -- no gain.)
+  // streams, a persistent trailing-GEMM grid of 248-512 workgroups -- no gain;
+  // the next-but-one panel's column update on a fourth stream beside the
+  // trailing update: 12.22 -> 12.11 ms here, C3 72 -> 66 steps/s in the graph.)
   std::vector<hipEvent_t> ev(3 * (N / 64 + 2) + 8);
   for (size_t i = 0; i < ev.size(); ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
   int lo = 0, hi = 0;
