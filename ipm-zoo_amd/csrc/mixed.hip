@@ -128,19 +128,36 @@ __global__ __launch_bounds__(MNT) void k_mx_symv(const double* __restrict__ K, i
 }
 
 // r = b - K x ; r32 = fp32(S r) ; per-block max |r|, max |b| partials
+// one workgroup per 64 columns j (lane = j): the column partials colp[I][j],
+// I >= j / 64, split over the 4 waves in contiguous I ranges (the 64 columns
+// share the range), summed through LDS with the row sums
 __global__ __launch_bounds__(MNT) void k_mx_resid(int N, const double* __restrict__ b, const double* __restrict__ s,
                                                   const double* __restrict__ colp, const double* __restrict__ rowp,
                                                   int nblk, float* __restrict__ r32, double* __restrict__ part,
                                                   const unsigned* __restrict__ state) {
   if (state[ST_DONE]) return;
-  __shared__ double sh[2][4];
-  const int j = blockIdx.x * MNT + threadIdx.x;
+  __shared__ double sh[4][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int jb = blockIdx.x, j = 64 * jb + lane;
+  const int cnt = nblk - jb, I0 = jb + cnt * wave / 4, I1 = jb + cnt * (wave + 1) / 4;
+  double a0 = 0.0, a1 = 0.0;
+  if (j < N) {
+    int I = I0;
+    for (; I + 1 < I1; I += 2) {
+      a0 += colp[(int64_t)I * N + j];
+      a1 += colp[(int64_t)(I + 1) * N + j];
+    }
+    if (I < I1) a0 += colp[(int64_t)I * N + j];
+  }
+  sh[wave][lane] = a0 + a1;
+  __syncthreads();
+  if (wave) return;
   double rr = 0.0, bb = 0.0;
   if (j < N) {
     double kx = 0.0;
 #pragma unroll
     for (int h = 0; h < NSPLIT; ++h) kx += rowp[(int64_t)h * N + j];
-    for (int I = j / 64; I < nblk; ++I) kx += colp[(int64_t)I * N + j];
+    kx += (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
     const double r = b[j] - kx;
     r32[j] = (float)(s[j] * r);
     rr = fabs(r);
@@ -148,15 +165,9 @@ __global__ __launch_bounds__(MNT) void k_mx_resid(int N, const double* __restric
   }
   rr = wave_max(rr);
   bb = wave_max(bb);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   if (lane == 0) {
-    sh[0][wave] = rr;
-    sh[1][wave] = bb;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = fmax(fmax(sh[0][0], sh[0][1]), fmax(sh[0][2], sh[0][3]));
-    part[2 * blockIdx.x + 1] = fmax(fmax(sh[1][0], sh[1][1]), fmax(sh[1][2], sh[1][3]));
+    part[2 * blockIdx.x] = rr;
+    part[2 * blockIdx.x + 1] = bb;
   }
 }
 
@@ -220,7 +231,7 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
   w.x = reinterpret_cast<double*>(take((int64_t)N * 8));
   w.colp = reinterpret_cast<double*>(take(nblk * N * 8));
   w.rowp = reinterpret_cast<double*>(take((int64_t)NSPLIT * N * 8));
-  w.part = reinterpret_cast<double*>(take(2 * ((N + MNT - 1) / MNT) * 8));
+  w.part = reinterpret_cast<double*>(take(2 * ((N + 63) / 64) * 8));
   w.stat = reinterpret_cast<double*>(take(64));
   return off;
 }
@@ -254,8 +265,9 @@ hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, doubl
     hipLaunchKernelGGL(k_mx_accum, gv, bt, 0, st, N, w.s, w.r32, w.x, w.state);
     hipLaunchKernelGGL(k_mx_symv, dim3((nblk + 1) / 2, NSPLIT), bt, 0, st, K, ld, N, w.x, w.colp, w.rowp, nblk,
                        w.state);
-    hipLaunchKernelGGL(k_mx_resid, gv, bt, 0, st, N, b, w.s, w.colp, w.rowp, nblk, w.r32, w.part, w.state);
-    hipLaunchKernelGGL(k_mx_check, dim3(1), dim3(64), 0, st, (int)gv.x, w.part, tol, w.state, w.stat);
+    hipLaunchKernelGGL(k_mx_resid, dim3((N + 63) / 64), bt, 0, st, N, b, w.s, w.colp, w.rowp, nblk, w.r32, w.part,
+                       w.state);
+    hipLaunchKernelGGL(k_mx_check, dim3(1), dim3(64), 0, st, (N + 63) / 64, w.part, tol, w.state, w.stat);
   }
   hipLaunchKernelGGL(k_mx_finish, gv, bt, 0, st, N, w.x, b);
   return hipGetLastError();
