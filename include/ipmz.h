@@ -175,6 +175,10 @@ int ipmz_bk_factor(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int f
 #define IPMZ_BK_WORKGROUP 1
 #define IPMZ_BK_GRID 2
 int ipmz_bk_factor_ex(ipmz_ctx* ctx, int N, double* A, int64_t ld, int* ipiv, int fix_kp, int algo);
+/* b <- A^{-1} b from ipmz_bk_factor's F and ipiv, in the reference's order
+ * (overwriting_solve_bunch_kaufman, LinearSolvers.cpp:209-318).  From
+ * N = 512 it reads a transposed copy of F made on the context's stream
+ * (N * N doubles, stream-ordered allocation freed after the solve). */
 int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* ipiv, double* b);
 /* Host signatures of the reference (value semantics, reference pivoting
  * including its kp = 0 defect): F = A with the lower triangle factored. */
