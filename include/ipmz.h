@@ -104,7 +104,9 @@ const char* ipmz_last_error(void);
  * their consumers hit the 0.5 s spin limit -- the path by which a stuck
  * hand-off surfaces as IPMZ_ERR_HIP from ipmz_ldlt_factor, ipmz_ctx_sync,
  * ipmz_qp_scalars, ipmz_qp_solve (sticky error words, cleared when a
- * factorization starts).  0 (default) for normal operation. */
+ * factorization starts).  Bit 4 is not a fault: IPMZ_STEP_GRAPH then
+ * captures steps whose factor forks onto the look-ahead streams as well.
+ * 0 (default) for normal operation. */
 int ipmz_debug_inject(int mask);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512;
  * 0 = by matrix order: 512 for N >= 2048 with nbi 64, else 256), inner
@@ -326,6 +328,16 @@ int ipmz_batch_copy_scalars(ipmz_qp* qp, double* dst_device);
 int ipmz_batch_summary(ipmz_qp* qp, double* dst_device);
 /* Step until every QP converged (converged QPs keep their iterate). */
 int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
+/* Which kernel factors a batch of small systems (N <= 1024; same LDL^T,
+ * same MFMA tiles in the same order, so both give the same factor):
+ * IPMZ_BATCH_FACTOR_AUTO (default: two workgroups per QP when 2 * batch <=
+ * #CU, else one), IPMZ_BATCH_FACTOR_ONE (one workgroup per QP),
+ * IPMZ_BATCH_FACTOR_PAIR (two per QP; IPMZ_ERR_INVALID unless 2 * batch <=
+ * #CU, since both workgroups of a QP must be resident together). */
+#define IPMZ_BATCH_FACTOR_AUTO 0
+#define IPMZ_BATCH_FACTOR_ONE 1
+#define IPMZ_BATCH_FACTOR_PAIR 2
+int ipmz_batch_set_factor_kernel(ipmz_qp* qp, int kernel);
 
 /* Phase timing (HIP events on the context stream; eager launches only).
  * ms: host array of IPMZ_PH_COUNT floats, cumulative since enable. */

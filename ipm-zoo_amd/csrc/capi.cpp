@@ -252,7 +252,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
     HIP_OK(prep());
     return IPMZ_OK;
   }
-  const int nev = 3 * npan + 4;
+  const int nev = 4 * npan + 4;
   int rc = ensure_events(ctx, (size_t)nev);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
@@ -333,7 +333,7 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
     HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
     return IPMZ_OK;
   }
-  const int nev = 3 * npan + 4;
+  const int nev = 4 * npan + 4;
   int rc = ensure_events(ctx, (size_t)nev);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
@@ -662,6 +662,7 @@ struct ipmz_qp {
   char* bkws = nullptr;  // the whole-device Bunch-Kaufman factor's workspace (B == 1, N >= IPMZ_BK_GRID_MIN)
   double* bklt = nullptr;  // its factor transposed (N x N), for coalesced solves
   unsigned* pflags = nullptr;  // B > 1: the two-workgroup small factor's flags + sticky error word
+  int small_kernel = IPMZ_BATCH_FACTOR_AUTO;  // ipmz_batch_set_factor_kernel
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
   // InequalityHandling / Bounds (which Newton slots exist)
   bool slacks = false, naive = false;
@@ -778,7 +779,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   bs.sD = s->sD;
   bs.sL = s->sL;
   bs.sW = s->sW;
-  bs.pflags = s->pflags;
+  bs.pflags = s->small_kernel == IPMZ_BATCH_FACTOR_ONE ? nullptr : s->pflags;
   if (!info_reset) HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
   HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
                              s->ctx->stream, bs));
@@ -1125,10 +1126,11 @@ int load_one(ipmz_qp* s, int i, const double* Q, const double* c, const double* 
 // the first capture, N >= 3 outer panels), and a multi-millisecond step hides
 // its launch latency anyway.
 bool step_forks(const ipmz_qp* s) {
-  auto npan = [&](int N) { return (N + nbo_for(s->ctx, N) - 1) / nbo_for(s->ctx, N); };
   if (s->eqnone || s->B > 1) return false;
-  if (s->normal) return npan(s->n) >= 3 || npan(s->m + s->p) >= 3;
-  return npan(s->N) >= 3;
+  if (debug_inject_mask() & IPMZ_INJECT_GRAPH_FORKS) return false;
+  // the augmented factor and the normal equations' pipelined factor are both
+  // one factor_impl of order N (= n + m + p): it forks from 3 outer panels
+  return (s->N + nbo_for(s->ctx, s->N) - 1) / nbo_for(s->ctx, s->N) >= 3;
 }
 
 int step_impl(ipmz_qp* s, int flags) {
@@ -1574,6 +1576,21 @@ int ipmz_batch_solve(ipmz_qp* s, int max_iter, int* iterations, int* converged_c
   }
   if (iterations) *iterations = it;
   if (converged_count) *converged_count = nconv;
+  return IPMZ_OK;
+}
+int ipmz_batch_set_factor_kernel(ipmz_qp* s, int kernel) {
+  if (!s || kernel < IPMZ_BATCH_FACTOR_AUTO || kernel > IPMZ_BATCH_FACTOR_PAIR)
+    return fail(IPMZ_ERR_INVALID, "ipmz_batch_set_factor_kernel: bad arguments");
+  if (kernel == IPMZ_BATCH_FACTOR_PAIR && !(s->pflags && small_pair_eligible(s->B, s->N)))
+    return fail(IPMZ_ERR_INVALID, "ipmz_batch_set_factor_kernel: two workgroups per QP need a batch of small systems "
+                                  "(N <= 1024) with 2 * batch <= #CU");
+  if (s->gexec) {  // the captured step has the other kernel baked in
+    hipGraphExecDestroy(s->gexec);
+    hipGraphDestroy(s->graph);
+    s->gexec = nullptr;
+    s->graph = nullptr;
+  }
+  s->small_kernel = kernel;
   return IPMZ_OK;
 }
 

@@ -13,7 +13,10 @@ namespace ipmz {
 // Fault injection for the tests of the spin-timeout path (ipmz_debug_inject):
 // a persistent kernel launched while its bit is set drops its first
 // hand-off, so every consumer times out and raises the sticky error word.
-enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2 };
+// IPMZ_INJECT_GRAPH_FORKS: not a fault -- IPMZ_STEP_GRAPH captures steps whose
+// factor forks onto the look-ahead streams too (the capture experiment of
+// tests/test_gpu_graph.py) instead of enqueuing them eagerly.
+enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4 };
 int debug_inject_mask();
 void set_debug_inject_mask(int mask);
 // error words the persistent kernels raise on a spin timeout (sync.h): the
@@ -54,7 +57,7 @@ struct TrailTimer {  // HIP-event pairs around every dominant trailing-update la
   double flops = 0.0;
   hipEvent_t* next() { return used < cap ? pairs[used++] : nullptr; }
 };
-// Look-ahead when st2 (and, for the panel path, st3) and ev (>= 3 *
+// Look-ahead when st2 (and, for the panel path, st3) and ev (>= 4 *
 // ceil(N/nbo) + 2 events) are given; W must then hold 3 * N * nbo doubles
 // (else N * nbo).  pctrl: panel_ctrl_words(N, nbo) zeroed words for the
 // panel path of panel.hip (nbi == 64); nullptr selects the diag / TRSM /

@@ -361,13 +361,16 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 //
 // Panel path of panel.hip (single QP, nbi = 64), THREE streams:
 //   A (st, high priority): [wait N_{k-1}] the chain launch of P_{k+1}
-//      (diagonal region, first updated with P_k; the factor's critical path
-//      on ~nb CUs)
-//   C (st3, high priority): [wait N_{k-1}] the look-ahead update of P_{k+1}'s
-//      rows below its region with P_k (strip GEMM), then the rows launch of
-//      P_{k+1}: their TRSMs / strips, pipelined behind the chain by flags ->
-//      event C_{k+1};
+//      (normally the diagonal-region roles, first updated with P_k; the
+//      factor's critical path on ~nb CUs) -> event A_{k+1}
+//   C (st3, high priority): [wait N_{k-1}, A_k] the look-ahead update of
+//      P_{k+1}'s rows below its region with P_k (strip GEMM), then the rows
+//      launch of P_{k+1}: their TRSMs / strips, pipelined behind the chain by
+//      flags -> event C_{k+1};
 //      A waits for it -> event P_{k+1} (the panel is complete)
+//   The two launches of a panel share one ticket counter (panel.hip), so any
+//   role may run in either launch: C waits for A_k as well before it touches
+//   rows panel k's roles wrote.
 //   B (st2, low priority): [wait P_k] update P_{k+2} with P_k -> event N_k;
 //      the trailing update beyond P_{k+2} with P_k (the big GEMM, overlapping
 //      the next panels)
@@ -387,7 +390,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
   const int npan = (N + nbo - 1) / nbo;
   const bool fused = pctrl != nullptr && nbi == 64;
-  const bool two = st2 != nullptr && ev != nullptr && nev >= 3 * npan + 2 && (!fused || st3 != nullptr);
+  const bool two = st2 != nullptr && ev != nullptr && nev >= 4 * npan + 2 && (!fused || st3 != nullptr);
   const int64_t wsz = (int64_t)N * nbo;
   auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };  // T*
   auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
@@ -425,9 +428,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   hipEvent_t* evP = ev;             // panel k complete (A)
   hipEvent_t* evN = ev + npan;      // P_{k+2} updated with P_k (B)
   hipEvent_t* evC = ev + 2 * npan;  // rows launch of panel k done (C)
-  hipEvent_t evJoin = ev[3 * npan];
+  hipEvent_t* evA = ev + 3 * npan;  // chain launch of panel k done (A)
+  hipEvent_t evJoin = ev[4 * npan];
   if ((e = factor(0, false)) != hipSuccess) return e;
   if (fused) {
+    if ((e = hipEventRecord(evA[0], st)) != hipSuccess) return e;
     if ((e = hipEventRecord(evC[0], sC)) != hipSuccess) return e;
     if ((e = hipStreamWaitEvent(st, evC[0], 0)) != hipSuccess) return e;
   }
@@ -460,13 +465,16 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
       // region as a strip GEMM on C (beside the chain launch, which updates
-      // the region itself)
+      // the region itself); panel k's rows roles may have run in its chain
+      // launch, so C also waits for that launch
+      if ((e = hipStreamWaitEvent(sC, evA[k], 0)) != hipSuccess) return e;
       if (p2 < N) {
         if ((e = gemm_nt_sub_t<T>(N - p2, p2 - p1, bo, Wb(k) + (int64_t)p2 * nbo, nbo, K + (int64_t)p1 * ld + k0, ld,
                                   K + (int64_t)p2 * ld + p1, ld, p2, p1, false, sC, nullptr)) != hipSuccess)
           return e;
       }
       if ((e = factor(k + 1, true)) != hipSuccess) return e;
+      if ((e = hipEventRecord(evA[k + 1], st)) != hipSuccess) return e;
       if ((e = hipEventRecord(evC[k + 1], sC)) != hipSuccess) return e;
       if ((e = hipStreamWaitEvent(st, evC[k + 1], 0)) != hipSuccess) return e;
     } else {

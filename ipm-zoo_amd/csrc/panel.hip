@@ -1,30 +1,29 @@
 // The panel path of the blocked LDL^T: for one outer panel (columns
 // [k0, c1), nb <= 8 inner blocks of 64), the column loop of
 // LinearSolvers::ldlt_decomposition (LinearSolvers.cpp:20-40) restricted to
-// those columns, as TWO concurrent launches that hand off by flags:
+// those columns, as roles that hand off by flags.  ONE kernel (panel_kernel,
+// 66.5 KB of LDS) is launched twice -- on the chain stream and on the rows
+// stream, after the look-ahead strip update of the rows below -- and every
+// workgroup takes its role from a ticket counter the two launches share
+// (see panel_kernel for why that cannot deadlock):
 //
-//   panel_chain_kernel (nb workgroups, 66.5 KB of LDS, s_setprio 3): the
-//   panel's diagonal region, first updated with the previous panel (each
-//   workgroup its own row of blocks).
+//   chain roles (the panel's diagonal region, first updated with the previous
+//   panel; s_setprio 3):
 //     ticket 0 = the CHAIN: for every inner block j, factor the 64 x 64
 //       diagonal block (diag64_body), publish DIAG[j], then -- still in its
 //       own LDS, no hand-off -- the TRSM of the next region block (j+1, j)
 //       and that block's own diagonal update; the result IS the next diagonal
 //       block.  The whole critical path of the panel lives on one CU.
-//     tickets >= nb = TILE WORKERS: one region block (c, q), c >= 1, each,
+//     tickets nb.. = TILE WORKERS: one region block (c, q), c >= 1, each,
 //       updated with the previous panel (flag TILE[c][q]); the chain updates
 //       block (0, 0) itself, straight into its LDS image.
-//     ticket c = region HELPER c (rows of block c): the TRSMs of its blocks
-//       j <= c - 2 and their strip updates, then READY[c]: its blocks
+//     ticket c < nb = region HELPER c (rows of block c): the TRSMs of its
+//       blocks j <= c - 2 and their strip updates, then READY[c]: its blocks
 //       (c, c-1) and (c, c) carry every contribution but block c-1's, which
 //       the chain applies itself.
-//   panel_rows_kernel (one 256-thread workgroup per 64 rows below the region,
-//   66.5 KB): optionally (rows_prev) first the look-ahead update of its rows
-//   with the PREVIOUS panel (A[rows, panel] -= W_prev[rows] L_prev[panel
-//   rows]^T; the fused factor runs that update as a strip GEMM on its own
-//   stream instead), then for every j: TRSM with L_jj^{-1} (waits DIAG[j]),
-//   L = T / D, W = T, and the strip pieces A[rows, q] -= L W[q, j]^T (waits
-//   REG[j][q]).
+//   rows roles (one per 64 rows below the region): for every j: TRSM with
+//     L_jj^{-1} (waits DIAG[j]), L = T / D, W = T, and the strip pieces
+//     A[rows, q] -= L W[q, j]^T (waits REG[j][q]).
 //
 // Flags: one area of IPMZ_PANEL_CTRL_WORDS words per outer panel (zeroed by
 // one memset when the factorization starts); the sticky error word is shared.
@@ -207,33 +206,72 @@ __device__ __forceinline__ void zero_acc(typename Mfma<T>::acc_t (&acc)[4]) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
+// One outer panel as ONE kernel launched twice (on the chain stream and on the
+// rows stream), every workgroup of both launches taking its role from one
+// ticket counter (area[OP_TICKET]) shared by the two launches:
+//   tickets [0, nchain)           the chain roles: 0 = the CHAIN, 1 .. nb-1 =
+//                                 region HELPERS, nb .. = TILE WORKERS
+//   tickets [nchain, nchain+nch)  the ROWS roles, one per 64 rows below the
+//                                 diagonal region
+//   later tickets                 nothing (the rows launch has max(nch, nchain)
+//                                 workgroups)
+// Every role waits only for roles with LOWER tickets, except inside the chain
+// roles (chain <-> helpers <-> tile workers), which are all in the first
+// nchain tickets -- and each launch has at least nchain workgroups, so
+// whichever launch is dispatched first holds all of them.  No launch ever
+// waits for a launch that has not started: the panel completes even when the
+// two launches run one after the other in either order (rocprofv3 --pmc
+// serializes dispatches; a device shared with other work may too).  A rows
+// role needs the look-ahead strip update of its rows, which runs before the
+// rows launch on the rows stream: a workgroup of the chain launch only gets a
+// rows ticket after a workgroup of the rows launch took an earlier one (the
+// chain launch has exactly nchain workgroups), i.e. after the strip update
+// finished.
+//
 // T = float: the fp32 factor of the mixed-precision path (f32 MFMA TRSMs and
 // strip pieces; the 64 x 64 diagonal blocks are factored in fp64 and stored
 // in fp32).
 // amdgpu_waves_per_eu(2): <= 256 registers per lane (VGPR + AGPR), so a
 // panel workgroup fits beside a trailing-GEMM workgroup (64 per lane at 4
 // waves per SIMD) -- with more it waits for a CU with no GEMM at all
+namespace {
 template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_chain_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
-                                                          T* __restrict__ D, T* __restrict__ Lb0, T* __restrict__ Wp,
-                                                          int ldw, int* __restrict__ info, unsigned* __restrict__ area,
-                                                          unsigned* __restrict__ err, int inject,
-                                                          const T* __restrict__ Wprev, int kprev, int boprev,
-                                                          const T* __restrict__ pre00) {
+struct PanelArgs {
+  T* K;
+  int64_t ld;
+  int N, k0, c1;
+  T* D;
+  T* Lb0;
+  T* Wp;
+  int ldw;
+  int* info;
+  unsigned* area;
+  unsigned* err;
+  int inject;
+  const T* Wprev;  // previous panel's W (nullptr: no look-ahead update in this launch pair)
+  int kprev, boprev;
+  const T* pre00_in;  // this panel's block (0, 0) update, accumulated by the previous rows role 0
+  T* pre00_out;       // the next panel's, accumulated by rows role 0
+  int nchain;         // chain-role tickets
+  int nrows;          // rows-role tickets
+};
+
+// ---- the chain roles (tickets < nchain)
+template <typename T>
+__device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double* smem, unsigned* sh_ok) {
   typedef Mfma<T> MF;
   typedef typename MF::acc_t acc_t;
-  // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
-  // trailing-GEMM workgroup leaves free, so it is never starved of a CU);
-  // s_setprio 3: its waves win issue arbitration (matrix pipe included)
-  // against the GEMM waves that share the CU
-  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
-  __shared__ unsigned sh_ticket, sh_ok;
-  __builtin_amdgcn_s_setprio(3);
+  T* const K = a.K;
+  const int64_t ld = a.ld;
+  const int k0 = a.k0, ldw = a.ldw;
+  T* const D = a.D;
+  T* const Lb0 = a.Lb0;
+  T* const Wp = a.Wp;
+  unsigned* const area = a.area;
+  unsigned* const err = a.err;
+  const T* const Wprev = a.Wprev;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) sh_ticket = atomicAdd(&area[OP_TICKET], 1u);
-  __syncthreads();
-  const int t = (int)sh_ticket;
-  const int ce = c1 < N ? c1 : N;
+  const int ce = a.c1 < a.N ? a.c1 : a.N;
   const int nb = (ce - k0 + 63) / 64;
   double* M = smem;
   double* X = smem + 64 * DS;
@@ -244,14 +282,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     // ================================================================ CHAIN
     if (Wprev) {  // block (0, 0) with the previous panel's update, straight into M
       acc_t own[4];
-      if (pre00) {
-        // accumulated by the previous panel's rows launch (the same MFMA
-        // order as prev_update), so this launch starts with the diagonal factor
-        load_acc<T, false, false>(own, pre00, 64, 64, 64);
+      if (a.pre00_in) {
+        // accumulated by the previous panel's rows role 0 (the same MFMA
+        // order as prev_update), so this role starts with the diagonal factor
+        load_acc<T, false, false>(own, a.pre00_in, 64, 64, 64);
       } else {
         zero_acc<T>(own);
-        prev_update<T>(own, Wprev + (int64_t)k0 * ldw, ldw, K + (int64_t)k0 * ld + kprev, ld, bsz(0), bsz(0), boprev,
-                       reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+        prev_update<T>(own, Wprev + (int64_t)k0 * ldw, ldw, K + (int64_t)k0 * ld + a.kprev, ld, bsz(0), bsz(0),
+                       a.boprev, reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
       }
       acc_t a0[4];
       load_acc<T, false, true>(a0, K + (int64_t)k0 * ld + k0, ld, bsz(0), bsz(0));
@@ -268,15 +306,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     for (int j = 0; j < nb; ++j) {
       const int j0 = k0 + 64 * j, bj = bsz(j);
       T* Lb = Lb0 + (int64_t)j * 64 * 64;
-      if (j == 0 && !Wprev) diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
-      else diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, info, M, X, dsh, nullptr);
+      if (j == 0 && !Wprev) diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr);
+      else diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr);
       if (j + 1 >= nb) {
-        if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);
+        if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
         break;
       }
       // ---- block row c = j + 1: (c, j) and (c, c) from helper c
       const int c = j + 1, r0 = k0 + 64 * c, rows = bsz(c);
-      if (!wait_flag(&area[OP_READY + c], err, &sh_ok)) return;
+      if (!wait_flag(&area[OP_READY + c], err, sh_ok)) return;
       // A(c, j) into M (free: L_jj is in K), the own block (c, c) into registers
       stage_tile<T, true>(reinterpret_cast<T*>(M), K + (int64_t)r0 * ld + j0, ld, rows, 64);
       acc_t own[4];
@@ -284,7 +322,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       // DIAG[j] after these loads: the diagonal block's write-back drains beside
       // them instead of on the chain (nothing this workgroup waits for needs
       // DIAG[j]: helper c only uses blocks <= c - 2).  inject: timeout tests only
-      if (!(inject && j == 0)) publish(&area[OP_DIAG + j]);
+      if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
       T rd[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
@@ -313,7 +351,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       put_acc<T>(Wm, acc);
       __syncthreads();
       mma_tile<T, true>(Lx, [&](int r, int k) { return Wm[r * DS + k]; }, own);
-      // W(c, j) for the helpers' and the rows kernel's strips: published after
+      // W(c, j) for the helpers' and the rows roles' strips: published after
       // the update, so the stores drain beside its MFMAs (publish's barrier
       // also ends every wave's reads of M and X)
       publish(&area[OP_REG + j * OP_NBMAX + c]);
@@ -343,7 +381,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     const int q = w, r0 = k0 + 64 * c, q0 = k0 + 64 * q, rows = bsz(c), qrows = bsz(q);
     acc_t upd[4], tile[4];
     zero_acc<T>(upd);
-    prev_update<T>(upd, Wprev + (int64_t)r0 * ldw, ldw, K + (int64_t)q0 * ld + kprev, ld, rows, qrows, boprev,
+    prev_update<T>(upd, Wprev + (int64_t)r0 * ldw, ldw, K + (int64_t)q0 * ld + a.kprev, ld, rows, qrows, a.boprev,
                    reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
     if (q == c) load_acc<T, false, true>(tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
     else load_acc<T, false, false>(tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
@@ -362,14 +400,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   T* Bs = reinterpret_cast<T*>(X);  // L_jj^{-1}, then W pieces
   if (Wprev) {  // this row of region blocks, updated with the previous panel by the tile workers
     for (int q = 0; q <= c; ++q)
-      if (!wait_flag(&area[OP_TILE + c * OP_NBMAX + q], err, &sh_ok)) return;
+      if (!wait_flag(&area[OP_TILE + c * OP_NBMAX + q], err, sh_ok)) return;
   }
   for (int j = 0; j + 2 <= c; ++j) {
     const int j0 = k0 + 64 * j;
     T* Lb = Lb0 + (int64_t)j * 64 * 64;
     if (j || Wprev) stage_tile<T, true>(As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
     else stage_tile<T, false>(As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
-    if (!wait_flag(&area[OP_DIAG + j], err, &sh_ok)) return;
+    if (!wait_flag(&area[OP_DIAG + j], err, sh_ok)) return;
     stage_tile<T, true>(Bs, Lb, 64, 64, 64);
     T rd[4];
 #pragma unroll
@@ -394,7 +432,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       if (q == c) {
         put_acc<T>(Bs, acc);
       } else {
-        if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], err, &sh_ok)) return;
+        if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], err, sh_ok)) return;
         stage_tile<T, true>(Bs, Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, 64);
       }
       acc_t tile[4];
@@ -410,35 +448,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   publish(&area[OP_READY + c]);
 }
 
-// ---------------------------------------------------------------------------
+// ---- a rows role (ticket nchain + r): the 64 rows from ce + 64 r.  Every
+// operand another role of this panel produced (and the strip update of these
+// rows, a previous kernel) is read with agent-scope loads, so the role may run
+// in either launch.  rows_prev (the kernel-chain fallback of a single-stream
+// factor): first the look-ahead update of these rows with the PREVIOUS panel,
+// A[rows, panel] -= W_prev[rows] L_prev[panel rows]^T.
 template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_rows_kernel(T* __restrict__ K, int64_t ld, int N, int k0, int c1,
-                                                         const T* __restrict__ D, const T* __restrict__ Lb0,
-                                                         T* __restrict__ Wp, int ldw, unsigned* __restrict__ area,
-                                                         unsigned* __restrict__ err, const T* __restrict__ Wprev,
-                                                         int ldwp, int kprev, int boprev, T* __restrict__ pre00) {
-  typedef Mfma<T> MF;
-  typedef typename MF::acc_t acc_t;
-  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS];
-  __shared__ unsigned sh_ok;
+__device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool rows_prev, double* smem,
+                                          unsigned* sh_ok) {
+  typedef typename Mfma<T>::acc_t acc_t;
+  T* const K = a.K;
+  const int64_t ld = a.ld;
+  const int k0 = a.k0, N = a.N, ldw = a.ldw;
   const int lane = threadIdx.x & 63;
-  const int ce = c1 < N ? c1 : N;
+  const int ce = a.c1 < N ? a.c1 : N;
   const int nb = (ce - k0 + 63) / 64;
-  const int row0 = ce + 64 * blockIdx.x;
+  const int row0 = ce + 64 * r;
   const int rows = N - row0 < 64 ? N - row0 : 64;
   auto bsz = [&](int j) { return ce - (k0 + 64 * j) < 64 ? ce - (k0 + 64 * j) : 64; };
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
   T* Krow = K + (int64_t)row0 * ld;
-  // ---- look-ahead update with the previous panel (written by earlier launches)
-  if (Wprev) {
+  if (rows_prev) {
     for (int q = 0; q < nb; ++q) {
       const int q0 = k0 + 64 * q, qrows = bsz(q);
       acc_t acc[4], tile[4];
       zero_acc<T>(acc);
-      prev_update<T>(acc, Wprev + (int64_t)row0 * ldwp, ldwp, K + (int64_t)q0 * ld + kprev, ld, rows, qrows, boprev,
-                     As, Bs);
-      load_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
+      prev_update<T>(acc, a.Wprev + (int64_t)row0 * ldw, ldw, K + (int64_t)q0 * ld + a.kprev, ld, rows, qrows,
+                     a.boprev, As, Bs);
+      load_acc<T, true, false>(tile, Krow + q0, ld, rows, qrows);
 #pragma unroll
       for (int n = 0; n < 4; ++n)
 #pragma unroll
@@ -446,31 +485,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
       store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
     }
   }
-  // ---- TRSMs and strips of this chunk's rows.  Chunk 0 (the next panel's
+  // ---- TRSMs and strips of this chunk's rows.  Role 0 (the next panel's
   // first 64 rows) also accumulates that panel's block (0, 0) look-ahead
   // update W(rows, j) L(rows, j)^T over j -- exactly the chunks prev_update
-  // would sum in the next chain launch -- and leaves it in pre00.
-  T* const p00 = blockIdx.x == 0 ? pre00 : nullptr;
+  // would sum in the next chain role -- and leaves it in pre00_out.
+  T* const p00 = r == 0 ? a.pre00_out : nullptr;
   acc_t a00[4];
   zero_acc<T>(a00);
   bool ok = true;
   for (int j = 0; j < nb && ok; ++j) {
     const int j0 = k0 + 64 * j, bj = bsz(j);
-    const T* Lb = Lb0 + (int64_t)j * 64 * 64;
+    const T* Lb = a.Lb0 + (int64_t)j * 64 * 64;
     __syncthreads();  // previous block's strip finished reading As / Bs
     stage_tile<T, true>(As, Krow + j0, ld, rows, bj);
-    if (!(ok = wait_flag(&area[OP_DIAG + j], err, &sh_ok))) break;
+    if (!(ok = wait_flag(&a.area[OP_DIAG + j], a.err, sh_ok))) break;
     stage_tile<T, true>(Bs, Lb, 64, 64, 64);
     T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int col = 16 * n + (lane & 15);
-      rd[n] = col < bj ? T(1) / ld_sc1(&D[j0 + col]) : T(0);
+      rd[n] = col < bj ? T(1) / ld_sc1(&a.D[j0 + col]) : T(0);
     }
     __syncthreads();
     acc_t acc[4];
     zero_acc<T>(acc);
-    mma_tile_lower<T>(As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);  // L_jj^{-1}: lower
+    mma_tile_lower<T>(As, [&](int rr, int k) { return Bs[rr * DS + k]; }, acc);  // L_jj^{-1}: lower
     __syncthreads();
     acc_t lacc[4];
 #pragma unroll
@@ -478,28 +517,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 #pragma unroll
       for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
     store_acc<T, false, false>(lacc, Krow + j0, ld, rows, bj);
-    store_acc<T, false, false>(acc, Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
+    store_acc<T, false, false>(acc, a.Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
     put_acc<T>(As, lacc);
     if (p00) {  // a00 += W(rows, j) L(rows, j)^T (W staged in Bs, L in As)
       put_acc<T>(Bs, acc);
       __syncthreads();
-      mma_tile<T, false>(Bs, [&](int r, int k) { return As[r * DS + k]; }, a00);
+      mma_tile<T, false>(Bs, [&](int rr, int k) { return As[rr * DS + k]; }, a00);
       __syncthreads();  // Bs is reused by the strips
     }
     // strips: (rows, q) -= L(rows, j) W(q, j)^T, q = j+1 .. nb-1
     for (int q = j + 1; q < nb; ++q) {
       const int q0 = k0 + 64 * q, qrows = bsz(q);
-      if (!(ok = wait_flag(&area[OP_REG + j * OP_NBMAX + q], err, &sh_ok))) break;  // (its barrier also frees Bs)
-      stage_tile<T, true>(Bs, Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, bj);
+      if (!(ok = wait_flag(&a.area[OP_REG + j * OP_NBMAX + q], a.err, sh_ok))) break;  // (its barrier also frees Bs)
+      stage_tile<T, true>(Bs, a.Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, bj);
       acc_t tile[4];
       load_acc<T, true, false>(tile, Krow + q0, ld, rows, qrows);
       __syncthreads();
-      mma_tile<T, true>(As, [&](int r, int k) { return Bs[r * DS + k]; }, tile);
+      mma_tile<T, true>(As, [&](int rr, int k) { return Bs[rr * DS + k]; }, tile);
       store_acc<T, false, false>(tile, Krow + q0, ld, rows, qrows);
       __syncthreads();
     }
   }
   if (p00 && ok) store_acc<T, false, false>(a00, p00, 64, 64, 64);  // consumed by a later launch
+}
+}  // namespace
+
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_kernel(PanelArgs<T> a,
+                                                                                           int rows_prev) {
+  // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
+  // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
+  __shared__ unsigned sh_ticket, sh_ok;
+  if (threadIdx.x == 0) sh_ticket = atomicAdd(&a.area[OP_TICKET], 1u);
+  __syncthreads();
+  const int t = (int)sh_ticket;
+  if (t < a.nchain) {
+    // s_setprio 3: the chain roles' waves win issue arbitration (matrix pipe
+    // included) against the GEMM waves that share the CU
+    __builtin_amdgcn_s_setprio(3);
+    chain_roles<T>(a, t, smem, &sh_ok);
+  } else if (t < a.nchain + a.nrows) {
+    rows_role<T>(a, t - a.nchain, rows_prev != 0, smem, &sh_ok);
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -511,18 +571,36 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
   const int ce = k0 + bo;
   const int nb = (bo + 63) / 64;
+  PanelArgs<T> a;
+  a.K = K;
+  a.ld = ld;
+  a.N = N;
+  a.k0 = k0;
+  a.c1 = ce;
+  a.D = D;
+  a.Lb0 = Lb0;
+  a.Wp = Wp;
+  a.ldw = ldw;
+  a.info = info;
+  a.area = area;
+  a.err = err;
+  a.inject = debug_inject_mask() & IPMZ_INJECT_PANEL;
+  a.Wprev = Wprev;
+  a.kprev = kprev;
+  a.boprev = boprev;
+  a.pre00_in = Wprev ? pre00_in : nullptr;
+  a.pre00_out = pre00_out;
   // chain + nb - 1 helpers (+ one tile worker per region block below the
   // diagonal block (0, 0) when the look-ahead update is applied here)
-  const int nwork = Wprev ? nb * (nb + 1) / 2 - 1 : 0;
-  hipLaunchKernelGGL(panel_chain_kernel<T>, dim3(nb + nwork), dim3(256), 0, st_chain, K, ld, N, k0, ce, D, Lb0, Wp, ldw, info,
-                     area, err, debug_inject_mask() & IPMZ_INJECT_PANEL, Wprev, kprev, boprev,
-                     Wprev ? pre00_in : nullptr);
+  a.nchain = nb + (Wprev ? nb * (nb + 1) / 2 - 1 : 0);
+  a.nrows = ce < N ? (N - ce + 63) / 64 : 0;
+  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, rows_prev ? 1 : 0);
   hipError_t e = hipGetLastError();
-  if (e != hipSuccess || ce >= N) return e;
-  const int nch = (N - ce + 63) / 64;
-  hipLaunchKernelGGL(panel_rows_kernel<T>, dim3(nch), dim3(256), 0, st_rows, K, ld, N, k0, ce, (const T*)D,
-                     (const T*)Lb0, Wp, ldw, area, err, rows_prev ? Wprev : nullptr, ldw, kprev, boprev,
-                     pre00_out);
+  if (e != hipSuccess || a.nrows == 0) return e;
+  // the rows launch: at least nchain workgroups, so either launch alone can
+  // hold every chain role
+  const int g = a.nrows > a.nchain ? a.nrows : a.nchain;
+  hipLaunchKernelGGL(panel_kernel<T>, dim3(g), dim3(256), 0, st_rows, a, rows_prev ? 1 : 0);
   return hipGetLastError();
 }
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
@@ -530,16 +608,14 @@ hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D,
                         const double* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
                         hipStream_t st_rows) {
   return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                              boprev, rows_prev,
-                                st_chain, st_rows);
+                                boprev, rows_prev, st_chain, st_rows);
 }
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                         const float* pre00_in, float* pre00_out, int* info, unsigned* area, unsigned* err,
                         const float* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
                         hipStream_t st_rows) {
   return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                              boprev, rows_prev,
-                               st_chain, st_rows);
+                               boprev, rows_prev, st_chain, st_rows);
 }
 
 }  // namespace ipmz

@@ -45,7 +45,7 @@ EXPORTS = [
     "ipmz_mixed_workspace_bytes", "ipmz_mixed_factor", "ipmz_mixed_solve", "ipmz_qp_set_mixed_precision",
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
     "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_factor_ex", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
-    "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject", "ipmz_batch_summary",
+    "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject", "ipmz_batch_summary", "ipmz_batch_set_factor_kernel",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
@@ -148,6 +148,7 @@ def _load():
         "ipmz_overwriting_solve_bunch_kaufman": ([_VP, _I, _P, ctypes.POINTER(ctypes.c_int), _P], _I),
         "ipmz_debug_inject": ([_I], _I),
         "ipmz_batch_summary": ([_VP, _VP], _I),
+        "ipmz_batch_set_factor_kernel": ([_VP, _I], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -178,6 +179,7 @@ class Context:
         _check(lib.ipmz_ctx_create(ctypes.byref(h), device), "ipmz_ctx_create")
         self.h = h
         self.device = device
+        self.stream = None  # None: the context's own (non-blocking) stream
         if stream is not None:
             self.set_stream(stream)
         if nbo or nbi:  # nbo 0 / None: by matrix order (libipmz's default)
@@ -190,6 +192,12 @@ class Context:
             _check(lib.ipmz_ctx_reset_stream(self.h), "ipmz_ctx_reset_stream")
         else:
             _check(lib.ipmz_ctx_set_stream(self.h, _VP(stream)), "ipmz_ctx_set_stream")
+        self.stream = stream
+
+    def on_stream(self, stream):
+        """True when work enqueued on this context is ordered before later
+        work on the HIP stream handle `stream` (the same stream)."""
+        return self.stream is not None and int(self.stream) == int(stream)
 
     def set_blocking(self, nbo, nbi):
         _check(lib.ipmz_ctx_set_blocking(self.h, nbo, nbi), "ipmz_ctx_set_blocking")
@@ -273,7 +281,7 @@ def debug_inject(mask):
     _check(lib.ipmz_debug_inject(int(mask)), "ipmz_debug_inject")
 
 
-INJECT_SOLVE, INJECT_PANEL = 1, 2
+INJECT_SOLVE, INJECT_PANEL, INJECT_GRAPH_FORKS = 1, 2, 4
 
 _default_ctx = None
 
@@ -526,9 +534,23 @@ class Batch(Optimizer):
         _check(lib.ipmz_batch_summary(self.h, _VP(dst_ptr)), "ipmz_batch_summary")
 
     def summary_into(self, t):
-        """Device tensor t (>= 3 float64): the summary, enqueued on the ctx
-        stream (the stepper protocol of ipmz_amd.dist.solve_sharded)."""
+        """Device tensor t (>= 3 float64): the summary (the stepper protocol
+        of ipmz_amd.dist.solve_sharded).  It is ordered before anything later
+        on torch's current stream: enqueued there when the context runs on
+        that stream, otherwise the context's stream is synchronized after it,
+        so an all-reduce or .tolist() on torch's stream never reads a stale
+        buffer."""
         self.summary(t.data_ptr())
+        import torch
+        if not self.ctx.on_stream(torch.cuda.current_stream(t.device).cuda_stream):
+            self.ctx.sync()
+
+    FACTOR_AUTO, FACTOR_ONE, FACTOR_PAIR = 0, 1, 2  # include/ipmz.h IPMZ_BATCH_FACTOR_*
+
+    def set_factor_kernel(self, kernel):
+        """FACTOR_AUTO, FACTOR_ONE (one workgroup per QP) or FACTOR_PAIR (two
+        per QP; needs 2 * batch <= #CU): the small batched LDL^T kernel."""
+        _check(lib.ipmz_batch_set_factor_kernel(self.h, int(kernel)), "ipmz_batch_set_factor_kernel")
 
     def batch_scalars(self):
         out = np.zeros(self.batch * SC_COUNT)

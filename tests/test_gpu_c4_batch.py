@@ -1,0 +1,120 @@
+"""Config C4 on the path bench.py times: a batch of 1024 QPs (n = 256, m = 64,
+KKT N = 320), where every batch > #CU / 2 runs the one-workgroup-per-QP factor
+(ldlt_small_kernel<8>, small.hip) and the 8-wave one-workgroup solve
+(trsv_small_kernel<8>, trsv.hip) -- the kernels of the `batched` bench line.
+
+Each QP is one Optimizer::solve_quasi_definite_ body
+(/root/reference/src/NumericalOptimization/Optimizer.cpp:127-219) on its own
+data; the reference has no batches, so parity is per QP:
+  * a strided sample of 33 QPs against their own oracle runs, every
+    iteration from the oracle's iterate: ||dx_gpu - dx_cpu||_inf < 1e-10 for
+    the affine and the corrector direction, every block within 1e-9
+    relative, alpha within 1e-9;
+  * QP 0 against the reference's C4-size golden vectors (c4_it*);
+  * every QP's alpha_aff, mu_aff, sigma, alpha and directions against runs of
+    the same seeds in batches of 128 (two workgroups per QP,
+    ldlt_small_pair_kernel, and the 16-wave solve) within 1e-9;
+  * the two small-factor kernels forced on the same batch agree bitwise.
+"""
+import numpy as np
+import pytest
+
+import oracle
+from golden_io import load, trace
+
+pytestmark = pytest.mark.gpu
+I = pytest.importorskip("ipmz_amd")
+DX_TOL = 1e-10
+N_, M_, B_ = 256, 64, 1024
+
+
+@pytest.fixture(scope="module")
+def ctx():
+    return I.Context(0)
+
+
+def test_c4_batch1024_vs_oracle_and_golden(ctx):
+    bt = I.Batch(N_, M_, 0, B_, ctx)
+    bt.generate(0)
+    sample = list(range(0, B_, 32)) + [B_ - 1]
+    orcs = {i: oracle.OracleQP(oracle.gen_qp(N_, M_, 0, i)) for i in sample}
+    for i, o in orcs.items():
+        assert np.array_equal(bt.state(i, 0), o.vars()), i  # generator + initial iterate: bitwise
+    names, rows, _ = trace("c4")
+    for it in range(len(rows)):
+        # QP 0 follows the reference's own iterates (golden), the others their oracle's
+        bt.set_state(0, load(f"c4_it{it}_vars.bin"))
+        recs = {i: o.iterate()[1] for i, o in orcs.items() if i != 0}
+        bt.step()
+        sc = bt.batch_scalars()
+        for which, tag in ((1, "daff"), (2, "d")):
+            ref = load(f"c4_it{it}_{tag}.bin")
+            got = bt.state(0, which)
+            assert np.abs(got[:N_] - ref[:N_]).max() < DX_TOL, (it, tag)
+            assert np.abs(got - ref).max() < 1e-9 * max(1.0, np.abs(ref).max()), (it, tag)
+        for i, o in orcs.items():
+            if i == 0:
+                continue
+            for which, ref in ((1, o.daff()), (2, o.dir())):
+                got = bt.state(i, which)
+                assert np.abs(got - ref).max() < 1e-9 * max(1.0, np.abs(ref).max()), (it, i, which)
+                assert np.abs(got[:N_] - ref[:N_]).max() < DX_TOL, (it, i, which)
+            for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+                assert abs(sc[i, I.SC[k]] - recs[i][k]) <= 1e-9 * max(1.0, abs(recs[i][k])), (it, i, k)
+            bt.set_state(i, o.vars())
+
+
+def _run(ctx, B, seed0, steps, kernel=None):
+    bt = I.Batch(N_, M_, 0, B, ctx)
+    if kernel is not None:
+        bt.set_factor_kernel(kernel)
+    bt.generate(seed0)
+    out = []
+    for _ in range(steps):
+        bt.step()
+        out.append((bt.batch_scalars(), [(bt.state(i, 1), bt.state(i, 2)) for i in range(B)]))
+    bt.close()
+    return out
+
+
+def test_c4_batch1024_matches_pair_kernel_runs(ctx):
+    """All 1024 QPs (one workgroup per QP) vs the same seeds in eight batches
+    of 128 (two workgroups per QP -- the 8-GPU shard's kernel)."""
+    steps = 3
+    big = _run(ctx, B_, 0, steps)
+    for c in range(B_ // 128):
+        part = _run(ctx, 128, 128 * c, steps)
+        for it in range(steps):
+            scb, dirs_b = big[it]
+            scp, dirs_p = part[it]
+            for j in range(128):
+                i = 128 * c + j
+                for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+                    a, b = scb[i, I.SC[k]], scp[j, I.SC[k]]
+                    assert abs(a - b) <= 1e-9 * max(1.0, abs(b)), (it, i, k, a, b)
+                for w in range(2):
+                    g, r = dirs_b[i][w], dirs_p[j][w]
+                    assert np.abs(g[:N_] - r[:N_]).max() < DX_TOL, (it, i, w)
+                    assert np.abs(g - r).max() < 1e-9 * max(1.0, np.abs(r).max()), (it, i, w)
+
+
+def test_c4_small_factor_kernels_agree_bitwise(ctx):
+    """B = 128: the one-workgroup factor and the two-workgroup factor forced on
+    the same batch (same MFMA tiles in the same order) give the same steps."""
+    one = _run(ctx, 128, 500, 3, I.Batch.FACTOR_ONE)
+    pair = _run(ctx, 128, 500, 3, I.Batch.FACTOR_PAIR)
+    auto = _run(ctx, 128, 500, 1)
+    for it in range(3):
+        assert np.array_equal(one[it][0], pair[it][0]), it
+        for i in range(128):
+            for w in range(2):
+                assert np.array_equal(one[it][1][i][w], pair[it][1][i][w]), (it, i, w)
+    assert np.array_equal(auto[0][0], pair[0][0])
+
+
+def test_c4_pair_kernel_rejected_when_not_coresident(ctx):
+    bt = I.Batch(N_, M_, 0, B_, ctx)
+    with pytest.raises(I.IpmzError, match="2 \\* batch <= #CU"):
+        bt.set_factor_kernel(I.Batch.FACTOR_PAIR)
+    bt.set_factor_kernel(I.Batch.FACTOR_ONE)
+    bt.close()

@@ -72,3 +72,22 @@ def test_sharded_batch_solve_two_ranks_one_gpu():
     got = np.array(v0 + v1)
     exp = np.array([ref.state(i) for i in range(BATCH)])
     assert np.array_equal(got, exp)
+
+
+def test_solve_sharded_batch_on_own_stream():
+    """A Batch passed straight to solve_sharded while its context runs on its
+    own (non-blocking) stream: the summary must be ordered before torch's
+    stream reads it (a stale zero buffer would stop the loop at iteration 0)."""
+    import ipmz_amd as I
+    from ipmz_amd.dist import solve_sharded
+
+    ctx = I.Context(0)  # the context's own stream, not torch's
+    b = I.Batch(N, M, 0, BATCH, ctx)
+    b.generate(0)
+    it, s = solve_sharded(b, 80, device="cuda")
+    ref = I.Batch(N, M, 0, BATCH, I.Context(0))
+    ref.generate(0)
+    it_ref, nconv = ref.solve_all(80)
+    assert nconv == BATCH and s[2] == 0.0 and it == it_ref > 0
+    for i in range(BATCH):
+        assert np.array_equal(b.state(i), ref.state(i)), i

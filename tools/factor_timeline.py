@@ -14,7 +14,7 @@ from collections import defaultdict
 
 def short(name):
     n = name.split("(")[0]
-    for key, s in (("outer_panel", "panel"), ("panel_chain", "chain"), ("panel_rows", "rows"), ("0, 4, 4", "trail128"), ("0, 2, 2", "trail64"),
+    for key, s in (("outer_panel", "panel"), ("panel_kernel", "panel"), ("panel_chain", "chain"), ("panel_rows", "rows"), ("0, 4, 4", "trail128"), ("0, 2, 2", "trail64"),
                    ("3, 2, 4", "strip"), ("3, 2, 2", "strip64"), ("3, 4, 4", "strip16w"), ("1, 4, 2", "trsm"),
                    ("panel_trsm", "ptrsm"), ("trsv", "solve"), ("fillBuffer", "memset")):
         if key in n:
@@ -71,7 +71,7 @@ def main():
         for r in fac:
             print(f"{(r[0] - t0) / 1e3:9.1f} {(r[1] - r[0]) / 1e3:8.1f} q{r[3]} {r[4]:8d} {short(r[2])}")
         return
-    panels = [r for r in fac if "outer_panel" in r[2] or "panel_chain" in r[2] or "panel_rows" in r[2]]
+    panels = [r for r in fac if "outer_panel" in r[2] or "panel_kernel" in r[2] or "panel_chain" in r[2] or "panel_rows" in r[2]]
     print(f"{'start':>8} {'dur':>7} {'gap':>6}  concurrent (other queue)")
     prev_end = t0
     for p in panels:

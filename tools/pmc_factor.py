@@ -27,7 +27,7 @@ import json
 import sys
 from collections import defaultdict
 
-FACTOR_KERNELS = ("gemm_nt_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel")
+FACTOR_KERNELS = ("gemm_nt_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel")
 
 
 def load(d):
