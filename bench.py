@@ -123,29 +123,40 @@ def run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch):
     for _ in range(args.warmup):
         one_step()
     elapsed = timed(world, dist, torch, args.steps, one_step)
+    graph = qp.last_step_graph()
     # instrumented pass (per-phase HIP events, eager launches)
-    qp.set_timing(True)
-    for _ in range(args.steps):
-        one_step(I.STEP_RESTART_IF_CONVERGED)
-    torch.cuda.synchronize()
-    ph = qp.phase_times()
     N = wl["n"] + wl["m"] + wl["p"]
-    factor_ms = ph["factor"] / args.steps
-    fac = B * (N ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
+    ph, fac = None, None
+    if not args.no_instrumented:
+        qp.set_timing(True)
+        for _ in range(args.steps):
+            one_step(I.STEP_RESTART_IF_CONVERGED)
+        torch.cuda.synchronize()
+        ph = qp.phase_times()
+        factor_ms = ph["factor"] / args.steps
+        fac = B * (N ** 3 / 3.0) / (factor_ms * 1e-3) / 1e12
     out = {
         "metric": f"QP Newton steps/sec, batch of {nbatch} dense QPs n={wl['n']} (C4), 1/2/4/8 MI355X",
         "value": args.steps * nbatch / elapsed, "unit": "QP-steps/s", "n_gpus": world,
         "ms_per_step": 1e3 * elapsed / args.steps, "scaling": "strong", "higher_is_better": True,
         "config": {"workload": "c4", "n": wl["n"], "m": wl["m"], "kkt_N": N, "global_batch": nbatch,
                    "qps_on_rank0": B, "parallelism": f"batch sharded over {world} rank(s); one all-reduce (MAX) "
-                                                     "of {max res, max mu, unconverged} per step"},
-        "phase_ms_per_step": {k: ph[k] / args.steps for k in ("step", "assemble", "factor", "solve", "eval")},
+                                                     "of {max res, max mu, unconverged} per step",
+                   "timing": ("HIP-graph replay" if graph else "eager launches") + " of the whole step + the "
+                             "summary kernel + the all-reduce; phases from a second, instrumented pass"},
+        "phase_ms_per_step": ({k: ph[k] / args.steps for k in ("step", "assemble", "factor", "solve", "eval")}
+                              if ph else None),
         "roofline": {"bound": "mfma", "kernel": "batched factor phase (whole LDL^T of each QP in one 8-wave "
                                                 "workgroup, fp64 MFMA)",
                      "achieved": fac, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": fac / FP64_MFMA_PEAK_TFLOPS, "traffic": None,
+                     "frac": fac / FP64_MFMA_PEAK_TFLOPS if fac else None, "traffic": None,
                      "note": "B * N^3/3 over the factor phase (HIP events), rank 0"},
     }
+    ftr = load_json("profiles/factor_traffic_c4.json") if nbatch == 1024 and world == 1 else None
+    if ftr:
+        out["roofline"]["traffic"] = ftr.get("factor_traffic_bytes_per_step")
+        out["roofline"]["traffic_source"] = ftr["source"]
+        out["roofline"]["mfma"] = ftr.get("mfma")
     qp.close()
     return out
 
@@ -169,6 +180,7 @@ def run_single(I, ctx, args, world, dist, torch, workload):
     for _ in range(args.warmup):
         qp.step(flags)
     elapsed = timed(world, dist, torch, args.steps, lambda: qp.step(flags))
+    graph = qp.last_step_graph()
     ph = None
     if not args.no_instrumented:
         qp.set_timing(True)  # resets the phase accumulators; eager launches with HIP events
@@ -198,8 +210,10 @@ def run_single(I, ctx, args, world, dist, torch, workload):
                                     ", augmented LDL^T")),
                    "parallelism": f"replicas x{world} (independent QPs, one per GPU)",
                    "blocking": dict(zip(("nbo", "nbi"), ctx.blocking(Nk))),
-                   "timing": "HIP-graph replay of the whole step (production path); phases from a second, "
-                             "instrumented pass",
+                   "timing": ("HIP-graph replay of the whole step" if graph else
+                              "eager launches of the whole step (its factor forks onto the look-ahead streams), "
+                              "at most one step in flight") +
+                             " (production path); phases from a second, instrumented pass",
                    "description": wl["desc"]},
         "restarts": s["restarts"],
     }
@@ -269,6 +283,17 @@ def main():
                                                           "shard at 8 GPUs, measured on one GPU)")
     args = ap.parse_args()
 
+    # the CPU baselines first (rank 0, one GPU): a child process on the host
+    # cores while the GPU is idle, so the GPU legs below run back to back
+    cpu = {}
+    if not args.no_cpu_baseline and int(os.environ.get("WORLD_SIZE", "1")) == 1:
+        wl0 = WORKLOADS[args.workload]
+        cpu["head"] = cpu_baseline(wl0)
+        if not wl0.get("batch") and not args.no_batched:
+            cpu["batched"] = cpu_baseline(WORKLOADS["c4"])
+        if args.workload == "c3" and not args.no_configs:
+            cpu.update({w: cpu_baseline(WORKLOADS[w]) for w in ("c2", "c5")})
+
     import torch
     import torch.distributed as dist
 
@@ -313,12 +338,13 @@ def main():
             # the other single-GPU configs of BASELINE.json, each its own line item
             out["configs"] = {w: run_single(I, ctx, args, world, dist, torch, w) for w in ("c2", "c5")}
     if rank == 0:
-        if not args.no_cpu_baseline and world == 1:
-            out["cpu_baseline"] = cpu_baseline(wl)
-            if "batched" in out:
-                out["batched"]["cpu_baseline"] = cpu_baseline(WORKLOADS["c4"])
+        if cpu:
+            out["cpu_baseline"] = cpu["head"]
+            if "batched" in out and "batched" in cpu:
+                out["batched"]["cpu_baseline"] = cpu["batched"]
             for w, sub in out.get("configs", {}).items():
-                sub["cpu_baseline"] = cpu_baseline(WORKLOADS[w])
+                if w in cpu:
+                    sub["cpu_baseline"] = cpu[w]
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()

@@ -124,7 +124,9 @@ int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N);
  * ld even).  D: device, N doubles.  ws: device workspace; it keeps the
  * inverted diagonal blocks that ipmz_ldlt_solve consumes. */
 int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, void* ws, int64_t ws_bytes);
-/* b <- K^{-1} b with the factor left by ipmz_ldlt_factor (device b). */
+/* b <- K^{-1} b with the factor left by ipmz_ldlt_factor (device b); asynchronous.
+ * ws must stay allocated until the next ipmz_ctx_sync, which reports a
+ * hand-off timeout of this solve (its sticky error words) as IPMZ_ERR_HIP. */
 int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b);
 /* Rebuild the solve workspace from an explicit unit-lower L (device). */
 int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, void* ws, int64_t ws_bytes);
@@ -200,7 +202,9 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
 #define IPMZ_EQ_REGULARIZATION 0 /* (lambda_C, lambda_C) block -delta^2, slack p: LDL^T   */
 #define IPMZ_EQ_NONE 1           /* zero (lambda_C, lambda_C) block, no p: the reference's
                                     "indefinite" case (Optimizer.cpp:63-75), factored with
-                                    Bunch-Kaufman (LinearSolvers.cpp:76-318); N <= 4096 */
+                                    Bunch-Kaufman (LinearSolvers.cpp:76-318): any N for a
+                                    single QP (the whole-device factor from N = 512), N <= 4096
+                                    per QP in batches (one workgroup per QP) */
 #define IPMZ_EQ_PENALTY 2        /* PenaltyFunction: -mu (lambda_C, lambda_C) block (mu I,
                                     mu = the iterate's environment mu), no p: LDL^T */
 #define IPMZ_EQ_PENALTY_EXTRA_DUAL 3 /* PenaltyFunctionWithExtraDual: the reference derives
@@ -262,6 +266,9 @@ int ipmz_qp_generate(ipmz_qp* qp, uint64_t seed);
                                             factor forks onto the look-ahead streams -- >= 3 outer
                                             panels -- are enqueued eagerly instead) */
 int ipmz_qp_step(ipmz_qp* qp, int flags);
+/* 1 when the last ipmz_qp_step replayed a captured hipGraph, 0 when its
+ * launches were enqueued one by one (what a benchmark reports it timed). */
+int ipmz_qp_last_step_graph(ipmz_qp* qp);
 /* Synchronize and copy the IPMZ_SC_COUNT scalars to host memory. */
 int ipmz_qp_scalars(ipmz_qp* qp, double* out);
 /* Device pointer of the scalar block (for collectives). */

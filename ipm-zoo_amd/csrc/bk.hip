@@ -745,11 +745,17 @@ hipError_t bk_factor_grid(double* A, int64_t ld, int n, int* ipiv, int* info, in
   if (n <= 0) return hipSuccess;
   const int G = device_cus();
   const int nq = (n + G - 1) / G;
+  // one workgroup per CU, all resident at once (a grid barrier per pivot
+  // step): refuse a launch whose LDS or registers would not allow it rather
+  // than let the barriers time out
+  const size_t lds = 3 * (size_t)nq * sizeof(double);
+  int per_cu = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k_bk_grid, bkg::T, lds) != hipSuccess || per_cu < 1)
+    return hipErrorInvalidConfiguration;
   char* w = static_cast<char*>(ws);
   hipError_t e = hipMemsetAsync(w + bkg::layout(n, G).ctrl, 0, 256, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_bk_grid, dim3(G), dim3(bkg::T), 3 * (size_t)nq * sizeof(double), st, A, ld, n, ipiv, info,
-                     fix_kp, w);
+  hipLaunchKernelGGL(k_bk_grid, dim3(G), dim3(bkg::T), lds, st, A, ld, n, ipiv, info, fix_kp, w);
   return hipGetLastError();
 }
 

@@ -35,6 +35,7 @@ int fail(int code, const std::string& msg) {
 
 int64_t round_up(int64_t x, int64_t a) { return (x + a - 1) / a * a; }
 int ws_status(hipStream_t st, const char* ws, int N, int nbo, int nbi, const char* what);
+int err_words_status(hipStream_t st, const unsigned* pe, const unsigned* se, const char* what);
 
 }  // namespace
 
@@ -47,10 +48,12 @@ struct ipmz_ctx {
   // priority), trailing updates on sB; forked from / joined to `stream`
   hipStream_t sA = nullptr, sB = nullptr, sC = nullptr;
   std::vector<hipEvent_t> evpool;
-  // the last workspace a device-memory factor / solve used: ipmz_ctx_sync
-  // checks its sticky error words (spin timeouts of the persistent kernels)
-  const char* check_ws = nullptr;
-  int check_N = 0;
+  // the sticky error words (spin timeouts of the persistent kernels) of the
+  // workspace the last asynchronous device-memory solve used, resolved when
+  // it was enqueued: ipmz_ctx_sync checks and clears them (the caller keeps
+  // that workspace alive until then)
+  const unsigned* check_pe = nullptr;
+  const unsigned* check_se = nullptr;
 };
 
 // outer panel width for an order-N factor: the context's, or by size --
@@ -143,10 +146,10 @@ int ipmz_ctx_reset_stream(ipmz_ctx* ctx) {
 int ipmz_ctx_sync(ipmz_ctx* ctx) {
   if (!ctx) return fail(IPMZ_ERR_INVALID, "null ctx");
   HIP_OK(hipStreamSynchronize(ctx->stream));
-  if (ctx->check_ws) {
-    const char* ws = ctx->check_ws;
-    ctx->check_ws = nullptr;
-    return ws_status(ctx->stream, ws, ctx->check_N, nbo_for(ctx, ctx->check_N), ctx->nbi, "ipmz_ctx_sync");
+  if (ctx->check_pe) {
+    const unsigned *pe = ctx->check_pe, *se = ctx->check_se;
+    ctx->check_pe = ctx->check_se = nullptr;
+    return err_words_status(ctx->stream, pe, se, "ipmz_ctx_sync");
   }
   return IPMZ_OK;
 }
@@ -210,11 +213,20 @@ hipError_t solve_ws(const double* K, int64_t ld, int N, const double* D, const c
 // Sticky error words of a workspace (synchronizes): a spin that timed out in
 // the outer-panel factor or the persistent solve (sync.h, 0.5 s) means the
 // results are invalid -- reported as IPMZ_ERR_HIP, never as success.
+const unsigned* panel_err_word(const char* ws, const WsLayout& l) {
+  return reinterpret_cast<const unsigned*>(ws + l.pctrl_off) + PANEL_ERR_WORD;
+}
+const unsigned* solve_err_word(const char* ws, const WsLayout& l) {
+  return reinterpret_cast<const unsigned*>(ws + l.ctrl_off) + SOLVE_ERR_WORD;
+}
 int ws_status(hipStream_t st, const char* ws, int N, int nbo, int nbi, const char* what) {
   const WsLayout l = ws_layout(N, nbo, nbi);
+  return err_words_status(st, panel_err_word(ws, l), solve_err_word(ws, l), what);
+}
+int err_words_status(hipStream_t st, const unsigned* pe_word, const unsigned* se_word, const char* what) {
   unsigned pe = 0, se = 0;
-  HIP_OK(hipMemcpyAsync(&pe, ws + l.pctrl_off + 4 * PANEL_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
-  HIP_OK(hipMemcpyAsync(&se, ws + l.ctrl_off + 4 * SOLVE_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&pe, pe_word, 4, hipMemcpyDeviceToHost, st));
+  HIP_OK(hipMemcpyAsync(&se, se_word, 4, hipMemcpyDeviceToHost, st));
   HIP_OK(hipStreamSynchronize(st));
   if (pe) return fail(IPMZ_ERR_HIP, std::string(what) + ": a hand-off inside the outer-panel factor kernel timed out "
                                                         "(spin limit 0.5 s); the factor is invalid");
@@ -288,9 +300,7 @@ int ipmz_ldlt_factor(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, voi
   HIP_OK(hipSetDevice(ctx->device));
   int rc = factor_impl(ctx, N, K, ld, D, static_cast<char*>(ws), nullptr);
   if (rc) return rc;
-  ctx->check_ws = static_cast<const char*>(ws);
-  ctx->check_N = N;
-  return read_info(ctx, static_cast<char*>(ws), N);
+  return read_info(ctx, static_cast<char*>(ws), N);  // synchronous: checks the error words itself
 }
 
 int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const double* D, const void* ws, double* b) {
@@ -298,8 +308,11 @@ int ipmz_ldlt_solve(ipmz_ctx* ctx, int N, const double* K, int64_t ld, const dou
   if (N == 0) return IPMZ_OK;
   HIP_OK(hipSetDevice(ctx->device));
   HIP_OK(solve_ws(K, ld, N, D, static_cast<const char*>(ws), nbo_for(ctx, N), ctx->nbi, b, ctx->stream));
-  ctx->check_ws = static_cast<const char*>(ws);  // its error word is checked by ipmz_ctx_sync
-  ctx->check_N = N;
+  // its error words are checked by ipmz_ctx_sync (addresses resolved now: a
+  // later ipmz_ctx_set_blocking does not move them)
+  const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
+  ctx->check_pe = panel_err_word(static_cast<const char*>(ws), l);
+  ctx->check_se = solve_err_word(static_cast<const char*>(ws), l);
   return IPMZ_OK;
 }
 
@@ -614,6 +627,9 @@ int ipmz_overwriting_solve_ldlt(ipmz_ctx* ctx, int N, const double* L, const dou
     rc = fail(IPMZ_ERR_HIP, "copy-in failed");
   if (!rc) rc = ipmz_ldlt_prepare_solve(ctx, N, dL, ld, ws, wsb);
   if (!rc) rc = ipmz_ldlt_solve(ctx, N, dL, ld, dD, ws, db);
+  // ws is freed below: check the solve's error words now, not at a later sync
+  ctx->check_pe = ctx->check_se = nullptr;
+  if (!rc) rc = ws_status(ctx->stream, ws, N, nbo_for(ctx, N), ctx->nbi, "ipmz_overwriting_solve_ldlt");
   if (!rc && (hipMemcpyAsync(b, db, (size_t)N * 8, hipMemcpyDeviceToHost, ctx->stream) != hipSuccess ||
               hipStreamSynchronize(ctx->stream) != hipSuccess))
     rc = fail(IPMZ_ERR_HIP, "copy-out failed");
@@ -685,6 +701,7 @@ struct ipmz_qp {
   // enqueued before it (queue depth 1, see step_impl)
   hipEvent_t step_done = nullptr;
   bool step_pending = false;
+  int last_step_graph = 0;  // the last ipmz_qp_step replayed a captured hipGraph
   int tr_cap = 0;
   double ph_ms[IPMZ_PH_COUNT] = {0};
   double tr_flops = 0.0;
@@ -1136,6 +1153,7 @@ bool step_forks(const ipmz_qp* s) {
 int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
+  s->last_step_graph = 0;
   if (step_forks(s) && !s->timing) {
     // A factorization that forks onto the look-ahead streams is enqueued
     // eagerly (~130-160 launches and event waits over four queues); with
@@ -1179,6 +1197,7 @@ int step_impl(ipmz_qp* s, int flags) {
     s->graph_flags = flags;
   }
   HIP_OK(hipGraphLaunch(s->gexec, st));
+  s->last_step_graph = 1;
   return IPMZ_OK;
 }
 
@@ -1340,6 +1359,8 @@ int ipmz_qp_generate(ipmz_qp* s, uint64_t seed) {
 }
 
 int ipmz_qp_step(ipmz_qp* s, int flags) { return step_impl(s, flags); }
+
+int ipmz_qp_last_step_graph(ipmz_qp* s) { return s ? s->last_step_graph : 0; }
 
 int ipmz_qp_scalars(ipmz_qp* s, double* out) {
   if (!s || !out) return fail(IPMZ_ERR_INVALID, "null argument");

@@ -368,9 +368,9 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 //      launch of P_{k+1}: their TRSMs / strips, pipelined behind the chain by
 //      flags -> event C_{k+1};
 //      A waits for it -> event P_{k+1} (the panel is complete)
-//   The two launches of a panel share one ticket counter (panel.hip), so any
-//   role may run in either launch: C waits for A_k as well before it touches
-//   rows panel k's roles wrote.
+//   The chain roles of a panel may run in either of its two launches
+//   (panel.hip): C waits for A_k as well before panel k+1 reuses what panel
+//   k's chain roles read (the pre-accumulated block (0, 0) slot).
 //   B (st2, low priority): [wait P_k] update P_{k+2} with P_k -> event N_k;
 //      the trailing update beyond P_{k+2} with P_k (the big GEMM, overlapping
 //      the next panels)
@@ -465,7 +465,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
       // region as a strip GEMM on C (beside the chain launch, which updates
-      // the region itself); panel k's rows roles may have run in its chain
+      // the region itself); panel k's chain roles may have run in its chain
       // launch, so C also waits for that launch
       if ((e = hipStreamWaitEvent(sC, evA[k], 0)) != hipSuccess) return e;
       if (p2 < N) {

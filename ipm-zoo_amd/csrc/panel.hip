@@ -4,8 +4,8 @@
 // those columns, as roles that hand off by flags.  ONE kernel (panel_kernel,
 // 66.5 KB of LDS) is launched twice -- on the chain stream and on the rows
 // stream, after the look-ahead strip update of the rows below -- and every
-// workgroup takes its role from a ticket counter the two launches share
-// (see panel_kernel for why that cannot deadlock):
+// workgroup takes its role from ticket counters (the chain roles' shared by
+// both launches; see panel_kernel for why that cannot deadlock):
 //
 //   chain roles (the panel's diagonal region, first updated with the previous
 //   panel; s_setprio 3):
@@ -206,27 +206,23 @@ __device__ __forceinline__ void zero_acc(typename Mfma<T>::acc_t (&acc)[4]) {
 }  // namespace
 
 // ---------------------------------------------------------------------------
-// One outer panel as ONE kernel launched twice (on the chain stream and on the
-// rows stream), every workgroup of both launches taking its role from one
-// ticket counter (area[OP_TICKET]) shared by the two launches:
-//   tickets [0, nchain)           the chain roles: 0 = the CHAIN, 1 .. nb-1 =
-//                                 region HELPERS, nb .. = TILE WORKERS
-//   tickets [nchain, nchain+nch)  the ROWS roles, one per 64 rows below the
-//                                 diagonal region
-//   later tickets                 nothing (the rows launch has max(nch, nchain)
-//                                 workgroups)
-// Every role waits only for roles with LOWER tickets, except inside the chain
-// roles (chain <-> helpers <-> tile workers), which are all in the first
-// nchain tickets -- and each launch has at least nchain workgroups, so
-// whichever launch is dispatched first holds all of them.  No launch ever
-// waits for a launch that has not started: the panel completes even when the
-// two launches run one after the other in either order (rocprofv3 --pmc
-// serializes dispatches; a device shared with other work may too).  A rows
-// role needs the look-ahead strip update of its rows, which runs before the
-// rows launch on the rows stream: a workgroup of the chain launch only gets a
-// rows ticket after a workgroup of the rows launch took an earlier one (the
-// chain launch has exactly nchain workgroups), i.e. after the strip update
-// finished.
+// One outer panel as ONE kernel launched twice -- on the chain stream (nchain
+// workgroups) and on the rows stream after the look-ahead strip update of the
+// rows below (nchain + nrows workgroups) -- with the roles handed out by two
+// ticket counters:
+//   chain tickets (area[OP_TICKET], both launches): [0, nchain) are the chain
+//     roles: 0 = the CHAIN, 1 .. nb-1 = region HELPERS, nb .. = TILE WORKERS;
+//     a workgroup that draws a later chain ticket takes no chain role;
+//   rows tickets (area[OP_TICKET + 1], rows launch only): [0, nrows) = the
+//     ROWS roles, one per 64 rows below the diagonal region.
+// Whichever launch is dispatched first can hold every chain role, so no
+// workgroup ever waits for one that has not been dispatched: the panel
+// completes even when the two launches run one after the other in either
+// order (rocprofv3 --pmc serializes dispatches; a device shared with other
+// work may too).  The rows roles stay in the launch ordered after the strip
+// update: they read its output, and a workgroup of the chain launch may have
+// started before that output existed (its L2 could then serve stale lines --
+// measured: shared rows tickets gave wrong C5 factors).
 //
 // T = float: the fp32 factor of the mixed-precision path (f32 MFMA TRSMs and
 // strip pieces; the 64 x 64 diagonal blocks are factored in fp64 and stored
@@ -448,12 +444,12 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
   publish(&area[OP_READY + c]);
 }
 
-// ---- a rows role (ticket nchain + r): the 64 rows from ce + 64 r.  Every
-// operand another role of this panel produced (and the strip update of these
-// rows, a previous kernel) is read with agent-scope loads, so the role may run
-// in either launch.  rows_prev (the kernel-chain fallback of a single-stream
-// factor): first the look-ahead update of these rows with the PREVIOUS panel,
-// A[rows, panel] -= W_prev[rows] L_prev[panel rows]^T.
+// ---- a rows role (rows ticket r): the 64 rows from ce + 64 r.  Every
+// operand another role of this panel produced is read with agent-scope loads
+// (the producer may be in the other launch).  rows_prev: first the
+// look-ahead update of these rows with the PREVIOUS panel, A[rows, panel] -=
+// W_prev[rows] L_prev[panel rows]^T (the fused factor runs it as a strip GEMM
+// on the rows stream instead).
 template <typename T>
 __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool rows_prev, double* smem,
                                           unsigned* sh_ok) {
@@ -544,14 +540,20 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
 
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_kernel(PanelArgs<T> a,
-                                                                                           int rows_prev) {
+                                                                                           int rows_launch, int rows_prev) {
   // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
   // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   __shared__ unsigned sh_ticket, sh_ok;
-  if (threadIdx.x == 0) sh_ticket = atomicAdd(&a.area[OP_TICKET], 1u);
+  if (threadIdx.x == 0) {
+    unsigned t = atomicAdd(&a.area[OP_TICKET], 1u);  // a chain role, while any is left
+    if (t >= (unsigned)a.nchain) t = rows_launch ? a.nchain + atomicAdd(&a.area[OP_TICKET + 1], 1u) : ~0u;
+    sh_ticket = t;
+  }
   __syncthreads();
-  const int t = (int)sh_ticket;
+  const unsigned tu = sh_ticket;
+  if (tu == ~0u) return;
+  const int t = (int)tu;
   if (t < a.nchain) {
     // s_setprio 3: the chain roles' waves win issue arbitration (matrix pipe
     // included) against the GEMM waves that share the CU
@@ -594,13 +596,11 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   // diagonal block (0, 0) when the look-ahead update is applied here)
   a.nchain = nb + (Wprev ? nb * (nb + 1) / 2 - 1 : 0);
   a.nrows = ce < N ? (N - ce + 63) / 64 : 0;
-  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, rows_prev ? 1 : 0);
+  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, 0, rows_prev ? 1 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess || a.nrows == 0) return e;
-  // the rows launch: at least nchain workgroups, so either launch alone can
-  // hold every chain role
-  const int g = a.nrows > a.nchain ? a.nrows : a.nchain;
-  hipLaunchKernelGGL(panel_kernel<T>, dim3(g), dim3(256), 0, st_rows, a, rows_prev ? 1 : 0);
+  // the rows launch: every chain role and every rows role, should it run first
+  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain + a.nrows), dim3(256), 0, st_rows, a, 1, rows_prev ? 1 : 0);
   return hipGetLastError();
 }
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,

@@ -5,9 +5,9 @@
 // lane stores the flag with a relaxed agent-scope atomic.  The 8 XCDs have
 // private L2s, so plain loads/stores are not enough for data that another
 // workgroup of the same launch consumes.  A hand-off may also cross two
-// launches of ONE kernel whose workgroups share a ticket counter
-// (panel.hip): roles are assigned by ticket, so a consumer never waits for
-// a workgroup that has not been dispatched.
+// concurrent launches of ONE kernel whose workgroups draw their roles from
+// shared ticket counters (panel.hip), so a consumer never waits for a
+// workgroup that has not been dispatched.
 #pragma once
 #include <hip/hip_runtime.h>
 

@@ -46,6 +46,7 @@ EXPORTS = [
     "ipmz_batch_copy_scalars", "ipmz_normal_workspace_bytes", "ipmz_normal_factor", "ipmz_normal_solve",
     "ipmz_qp_set_reduction", "ipmz_bk_factor", "ipmz_bk_factor_ex", "ipmz_bk_solve", "ipmz_symmetric_indefinite_factorization",
     "ipmz_overwriting_solve_bunch_kaufman", "ipmz_debug_inject", "ipmz_batch_summary", "ipmz_batch_set_factor_kernel",
+    "ipmz_qp_last_step_graph",
 ]
 REDUCTION_AUGMENTED, REDUCTION_NORMAL = 0, 1
 
@@ -149,6 +150,7 @@ def _load():
         "ipmz_debug_inject": ([_I], _I),
         "ipmz_batch_summary": ([_VP, _VP], _I),
         "ipmz_batch_set_factor_kernel": ([_VP, _I], _I),
+        "ipmz_qp_last_step_graph": ([_VP], _I),
     }
     for name, (args, res) in sig.items():
         fn = getattr(lib, name)
@@ -379,7 +381,7 @@ class Optimizer:
     EqualityHandling::Regularization (delta = 1e-4) when equalities exist.
     equality_handling=EQ_NONE: the zero (lambda_C, lambda_C) block the
     reference routes to solve_indefinite_ (Optimizer.cpp:63-75), factored
-    with Bunch-Kaufman (N <= 4096); EQ_PENALTY: PenaltyFunction.
+    with Bunch-Kaufman (any N; N <= 4096 per QP in batches); EQ_PENALTY: PenaltyFunction.
     inequality_handling=INEQ_SLACKS, inequality_bounds / variable_bounds =
     BOUNDS_LOWER / UPPER / NONE select the other Newton systems (absent
     blocks dropped from the Newton order, as the reference does).
@@ -415,6 +417,10 @@ class Optimizer:
 
     def step(self, flags=0):
         _check(lib.ipmz_qp_step(self.h, flags), "ipmz_qp_step")
+
+    def last_step_graph(self):
+        """True when the last step replayed a captured hipGraph."""
+        return bool(lib.ipmz_qp_last_step_graph(self.h))
 
     def set_reduction(self, reduction):
         """REDUCTION_AUGMENTED (default) or REDUCTION_NORMAL (config C2)."""

@@ -69,3 +69,23 @@ def test_factor_panel_timeout_raises(ctx):
             ctx.sync()
     finally:
         ctx.set_stream(None)
+
+
+def test_host_signature_solve_timeout_raises(ctx):
+    """ipmz_overwriting_solve_ldlt (the reference's host signature) frees its
+    workspace before returning: a solve timeout must be reported by that call
+    itself, and a later ipmz_ctx_sync must not read the freed workspace."""
+    N = 300
+    K = _qd(N, 9)
+    L, D, info = I.LinearSolvers.ldlt_decomposition(K, ctx)
+    assert info == 0
+    b = np.ones(N)
+    I.debug_inject(I.INJECT_SOLVE)
+    try:
+        with pytest.raises(I.IpmzError, match="triangular solve"):
+            I.LinearSolvers.overwriting_solve_ldlt(L, D, b.copy(), ctx)
+    finally:
+        I.debug_inject(0)
+    ctx.sync()  # nothing pending: the timeout was already reported
+    x = I.LinearSolvers.overwriting_solve_ldlt(L, D, b.copy(), ctx)
+    assert np.abs(K @ x - b).max() < 1e-10

@@ -100,3 +100,31 @@ def test_c5_mixed_newton_step_vs_oracle(ctx):
     s = g.scalars()
     print(f"C5: refinement ratio {s['ir_ratio_aff']:.2e} / {s['ir_ratio']:.2e} after "
           f"{s['ir_iters_aff']:.0f} / {s['ir_iters']:.0f} corrections", flush=True)
+
+
+def test_c2_normal_newton_steps_vs_oracle(ctx):
+    """C2 (BASELINE.json configs[1]): n=2048, m=512, the normal-equations
+    reduction (Cholesky of H, TRSM, SYRK, Cholesky of S as one pipelined
+    factor, 512-wide outer panels at this size) against the oracle's
+    augmented reference-order LDL^T from the same iterate -- the Newton
+    directions are the same system's solution (Optimizer.cpp:137-217,
+    SymbolicOptimization.cpp:465-478), at iterate 0 and after 4 steps."""
+    n, m, p, seed = 2048, 512, 0, 1234
+    qp = oracle.gen_qp(n, m, p, seed)
+    o = oracle.OracleQP(qp)
+    g = I.Optimizer(n, m, p, ctx)
+    g.generate(seed)
+    g.set_reduction(I.REDUCTION_NORMAL)
+    assert ctx.blocking(n + m)[0] == 512  # the blocking bench.py's C2 line runs
+    assert np.array_equal(g.vars(), o.vars())
+    for label, warm in (("C2 iterate 0", 0), ("C2 iterate 4", 4)):
+        for _ in range(warm):
+            g.step()
+        if warm:
+            o.set_vars(g.vars())
+        g.step()
+        done, rec = o.iterate()
+        assert done == 0
+        _check_scalars(g, rec, label)
+        _check_step(o, g, label)
+        g.set_vars(o.vars())

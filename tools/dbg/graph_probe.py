@@ -8,8 +8,12 @@ sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
 import numpy as np
 import torch
 import ipmz_amd as I
-ctypes.CDLL(os.path.join(REPO, "tools", "dbg", "libsegv.so"))
+import faulthandler
+faulthandler.enable()
+segv = ctypes.CDLL(os.path.join(REPO, "tools", "dbg", "libsegv.so"))
 torch.cuda.set_device(0)
+torch.zeros(1, device="cuda")
+segv.segv_install()  # after the HIP runtime's own initialisation (it may install handlers)
 I.debug_inject(I.INJECT_GRAPH_FORKS)
 sizes = [(int(a), int(b), int(c)) for a, b, c in (s.split(",") for s in sys.argv[1:])] or [(1024, 256, 128)]
 for use_torch_stream in (False, True):
@@ -22,6 +26,7 @@ for use_torch_stream in (False, True):
         print("N", n + m + p, "blocking", ctx.blocking(n + m + p), "torch stream", use_torch_stream, flush=True)
         e.step(1)
         print("eager ok", flush=True)
+        print("capturing", flush=True)
         g.step(3)
         print("graph captured + replayed", flush=True)
         ctx.sync()

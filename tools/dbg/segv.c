@@ -10,9 +10,10 @@ static void handler(int sig) {
   signal(sig, SIG_DFL);
   raise(sig);
 }
-__attribute__((constructor)) static void install(void) {
+void segv_install(void) {
   struct sigaction sa;
   memset(&sa, 0, sizeof sa);
   sa.sa_handler = handler;
   sigaction(SIGSEGV, &sa, 0);
 }
+__attribute__((constructor)) static void install_at_load(void) { segv_install(); }

@@ -16,7 +16,7 @@ FETCH_SIZE reports half the bytes of a 16-B/lane read on gfx950 (doubled);
 SQ_INSTS_VALU_MFMA_MOPS_F64 / _F32 count 512-flop units (C5's fp32 factor:
 the _F32 counter in the mops pass, PMCW=c5 in tools/gpu_round.sh).
 
-    python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir[,dir...]> <label> <N> > profiles/factor_traffic_c3.json
+    python tools/pmc_factor.py <fetch dir> <write dir> <mfma dir[,dir...]> <label> <N> [B] > profiles/factor_traffic_c3.json
 
 (the MFMA counters may come from several smaller passes, comma-separated:
 one large pass slows every dispatch enough that the panel path's cross-launch
@@ -27,7 +27,8 @@ import json
 import sys
 from collections import defaultdict
 
-FACTOR_KERNELS = ("gemm_nt_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel")
+FACTOR_KERNELS = ("gemm_nt_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel",
+                  "ldlt_small_kernel", "ldlt_small_pair_kernel")  # (the last two: C4's batched factor)
 
 
 def load(d):
@@ -53,6 +54,7 @@ def main():
                 mfma[k][c] += v
     label = sys.argv[4] if len(sys.argv) > 4 else ""
     N = int(sys.argv[5]) if len(sys.argv) > 5 else 11264
+    B = int(sys.argv[6]) if len(sys.argv) > 6 else 1  # QPs per factor phase (C4: 1024)
     kernels = sorted(set(fetch) | set(write) | set(mfma))
     rows = {}
     tot = defaultdict(float)
@@ -70,10 +72,11 @@ def main():
         for f in ("fetch_bytes", "write_bytes", "hbm_bytes", "f64_mfma_flops", "f32_mfma_flops", "mfma_busy_cycles",
                   "busy_cu_cycles"):
             tot[f] += row[f]
-    alg_flops = N ** 3 / 3.0
+    alg_flops = B * N ** 3 / 3.0
     out = {
         "profile": label,
         "N": N,
+        "batch": B,
         "factor_traffic_bytes_per_step": tot["hbm_bytes"],
         "mfma": {
             "f64_mfma_flops_per_step": tot["f64_mfma_flops"],
@@ -85,12 +88,17 @@ def main():
             "busy_cu_cycles": tot["busy_cu_cycles"],
             "mfma_busy_over_busy_cu": (tot["mfma_busy_cycles"] / tot["busy_cu_cycles"]
                                        if tot["busy_cu_cycles"] else None),
+            # the MFMA-busy counter counts per SIMD (4 per CU): the utilisation
+            # of the matrix pipes while the CUs are busy, <= 1
+            "mfma_util_per_simd": (tot["mfma_busy_cycles"] / (4.0 * tot["busy_cu_cycles"])
+                                   if tot["busy_cu_cycles"] else None),
         },
         "per_kernel": rows,
         "note": "one bench step (one factorization), separate --pmc passes, counters summed over the factor's "
                 "launches; FETCH_SIZE x2 + WRITE_SIZE (KiB -> B); MFMA flops = 512 x SQ_INSTS_VALU_MFMA_MOPS_F64 "
                 "(executed, incl. the masked upper halves of diagonal tiles); mfma_busy_over_busy_cu = "
-                "SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CU_CYCLES as reported (both summed over the chip)",
+                "SQ_VALU_MFMA_BUSY_CYCLES / SQ_BUSY_CU_CYCLES as reported (both summed over the chip; the MFMA "
+                "counter sums the 4 SIMDs of a CU), mfma_util_per_simd = that / 4",
     }
     print(json.dumps(out, indent=1))
 
