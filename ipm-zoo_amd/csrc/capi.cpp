@@ -258,7 +258,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
     return ctx->nbi == 64 ? solve_prep(K, ld, N, Linv, reinterpret_cast<double*>(ws + l.prep_off), ctx->stream)
                           : hipSuccess;
   };
-  if (npan < 3) {
+  if (npan < 3 || (debug_inject_mask() & IPMZ_DEBUG_ONE_STREAM)) {
     HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, nullptr, nullptr, nullptr, 0,
                        pctrl));
     HIP_OK(prep());
@@ -341,7 +341,7 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
 // factor of S K S in fp32, with the same two-stream look-ahead as the fp64 factor
 static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs& w, TrailTimer* timer) {
   const int npan = (w.N + w.nbo - 1) / w.nbo;
-  if (npan < 3) {
+  if (npan < 3 || (debug_inject_mask() & IPMZ_DEBUG_ONE_STREAM)) {
     HIP_OK(mixed_factor(K, ld, w, ctx->stream, nullptr, nullptr, nullptr, 0, timer));
     HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
     return IPMZ_OK;

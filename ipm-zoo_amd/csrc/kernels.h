@@ -16,7 +16,10 @@ namespace ipmz {
 // IPMZ_INJECT_GRAPH_FORKS: not a fault -- IPMZ_STEP_GRAPH captures steps whose
 // factor forks onto the look-ahead streams too (the capture experiment of
 // tests/test_gpu_graph.py) instead of enqueuing them eagerly.
-enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4 };
+// DEBUG bits (determinism experiments): 16 = the mixed factor stops after
+// the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
+enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
+       IPMZ_DEBUG_ONE_STREAM = 32 };
 int debug_inject_mask();
 void set_debug_inject_mask(int mask);
 // error words the persistent kernels raise on a spin timeout (sync.h): the

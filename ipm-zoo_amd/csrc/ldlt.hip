@@ -430,6 +430,12 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   hipEvent_t* evC = ev + 2 * npan;  // rows launch of panel k done (C)
   hipEvent_t* evA = ev + 3 * npan;  // chain launch of panel k done (A)
   hipEvent_t evJoin = ev[4 * npan];
+  // everything the caller enqueued on st before the factor (the mixed path's
+  // fp32 conversion, the ctrl-word memsets) comes first on B and C as well
+  hipEvent_t evEntry = ev[4 * npan + 1];
+  if ((e = hipEventRecord(evEntry, st)) != hipSuccess) return e;
+  if ((e = hipStreamWaitEvent(st2, evEntry, 0)) != hipSuccess) return e;
+  if (fused && (e = hipStreamWaitEvent(sC, evEntry, 0)) != hipSuccess) return e;
   if ((e = factor(0, false)) != hipSuccess) return e;
   if (fused) {
     if ((e = hipEventRecord(evA[0], st)) != hipSuccess) return e;

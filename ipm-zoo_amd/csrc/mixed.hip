@@ -247,6 +247,7 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   if (e != hipSuccess) return e;
   if ((e = hipMemsetAsync(w.pctrl, 0, panel_ctrl_words(N, w.nbo) * sizeof(unsigned), st)) != hipSuccess) return e;
   if ((e = solve_reset(w.y32, w.z32, sizeof(float), N, w.ctrl, st)) != hipSuccess) return e;
+  if (debug_inject_mask() & IPMZ_DEBUG_CONVERT_ONLY) return hipGetLastError();
   return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, st3, ev, nev,
                      w.pctrl);
 }
