@@ -229,10 +229,13 @@ __global__ __launch_bounds__(BKT) void k_bk_factor(double* __restrict__ Ab, int6
 // TRANS: the factor's lower triangle as its transpose LT (row j of LT =
 // column j of L, contiguous; ld = the row stride of LT): every column access of
 // the sweeps is then one coalesced row instead of a cache line per element
+// gate (may be null): run only when *gate != 0 (the fallback of the
+// device-wide solve, bk_fast_*)
 template <bool TRANS>
 __global__ __launch_bounds__(BKT) void k_bk_solve(const double* __restrict__ Lb, int64_t ld, int n, int64_t sA,
                                                   const int* __restrict__ ipivb, int64_t sP, double* __restrict__ bb,
-                                                  int64_t sb) {
+                                                  int64_t sb, const unsigned* gate) {
+  if (gate && *gate == 0u) return;
   __shared__ double sv[BKW];
   const double* L = Lb + blockIdx.x * sA;
   const int* ipiv = ipivb + blockIdx.x * sP;
@@ -775,7 +778,7 @@ hipError_t bk_factor(double* A, int64_t ld, int n, int* ipiv, int* info, int fix
 hipError_t bk_solve(const double* F, int64_t ld, int n, const int* ipiv, double* b, int batch, int64_t sA, int64_t sP,
                     int64_t sb, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bk_solve<false>, dim3(batch), dim3(BKT), 0, st, F, ld, n, sA, ipiv, sP, b, sb);
+  hipLaunchKernelGGL(k_bk_solve<false>, dim3(batch), dim3(BKT), 0, st, F, ld, n, sA, ipiv, sP, b, sb, nullptr);
   return hipGetLastError();
 }
 
@@ -805,7 +808,293 @@ hipError_t bk_transpose(const double* F, int64_t ld, int n, double* LT, hipStrea
 }
 hipError_t bk_solve_lt(const double* LT, int n, const int* ipiv, double* b, hipStream_t st) {
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(k_bk_solve<true>, dim3(1), dim3(BKT), 0, st, LT, (int64_t)n, n, 0, ipiv, 0, b, 0);
+  hipLaunchKernelGGL(k_bk_solve<true>, dim3(1), dim3(BKT), 0, st, LT, (int64_t)n, n, 0, ipiv, 0, b, 0, nullptr);
+  return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------
+// Device-wide solve (bk_fast_*).  The reference's sweeps interleave the
+// interchanges with the column updates (LinearSolvers.cpp:229-317); every
+// interchange of step j moves entries at positions >= j only, so it commutes
+// with the updates of the columns before it once those columns' rows are
+// permuted the same way.  Folding every later interchange into each column
+// of L once per factor gives A^{-1} b = P^T L'^{-T} D^{-1} L'^{-1} P b with
+// L' unit lower (a 2x2 pivot's d21 entry zeroed: the reference never
+// updates b[k+1] from column k), D block diagonal (1x1, 2x2 as the
+// reference solves them) and P the composite interchange -- so both sweeps
+// are the persistent 128-row triangular solve of the LDL^T path
+// (trsv_persist.hip) and the interchanges two gathers.  Falls back to the
+// one-workgroup sweeps (gated by meta's flag) when an all-zero column made
+// the factor singular (the reference's kp = 0 defect swaps backwards) or the
+// interchange bookkeeping does not fit one workgroup's LDS.
+namespace bkf {
+constexpr int LDS_MAX_N = 16384;     // perm + slot map in LDS: 8 n bytes
+constexpr int SLOT_MAX = 16384;      // touched positions of the interchanges (LDS doubles)
+struct Meta {
+  unsigned* flag;  // [0] 1 = fall back; [1] swaps; [2] slots
+  int *kind, *perm, *srow, *sa, *sb, *slotpos;
+  double *d11, *d21, *d22, *ones, *t;
+  size_t total;
+};
+inline Meta layout(char* base, int n) {
+  Meta m;
+  size_t off = 0;
+  auto take = [&](size_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += (bytes + 255) / 256 * 256;
+    return p;
+  };
+  m.flag = reinterpret_cast<unsigned*>(take(256));
+  m.kind = reinterpret_cast<int*>(take((size_t)n * 4));
+  m.perm = reinterpret_cast<int*>(take((size_t)n * 4));
+  m.srow = reinterpret_cast<int*>(take((size_t)n * 4));
+  m.sa = reinterpret_cast<int*>(take((size_t)n * 4));
+  m.sb = reinterpret_cast<int*>(take((size_t)n * 4));
+  m.slotpos = reinterpret_cast<int*>(take((size_t)2 * n * 4));
+  m.d11 = reinterpret_cast<double*>(take((size_t)n * 8));
+  m.d21 = reinterpret_cast<double*>(take((size_t)n * 8));
+  m.d22 = reinterpret_cast<double*>(take((size_t)n * 8));
+  m.ones = reinterpret_cast<double*>(take((size_t)n * 8));
+  m.t = reinterpret_cast<double*>(take((size_t)n * 8));
+  m.total = off;
+  return m;
+}
+
+// One workgroup: the pivot structure in the reference's order.  kind[k]: 0
+// = 1x1, 1 / 2 = first / second row of a 2x2; the interchanges in step order
+// (row srow, positions sa = srow and sb = kp, as slot indices into slotpos,
+// the distinct positions they touch); perm = the composite interchange
+// ((P b)[p] = b[perm[p]]).  Thread 0 walks ipiv in chunks staged in LDS.
+__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ ipiv, int n, const int* __restrict__ info,
+                                               Meta m) {
+  extern __shared__ int lds[];  // perm[n], slotof[n]
+  __shared__ int chunk[1025];
+  __shared__ int sh_bad, sh_ns, sh_nsl;
+  int* perm = lds;
+  int* slotof = lds + n;
+  const int tid = threadIdx.x;
+  for (int i = tid; i < n; i += 1024) {
+    perm[i] = i;
+    slotof[i] = -1;
+  }
+  if (tid == 0) {
+    sh_bad = (info && *info != 0) ? 1 : 0;  // an all-zero column: the reference divides by zero
+    sh_ns = 0;
+    sh_nsl = 0;
+  }
+  __syncthreads();
+  int k = 0;  // next pivot step (thread 0's; the chunk loop is uniform)
+  for (int c0 = 0; c0 < n; c0 += 1024) {
+    if (c0 + tid < n) chunk[tid] = ipiv[c0 + tid];
+    if (tid == 0) chunk[1024] = c0 + 1024 < n ? ipiv[c0 + 1024] : 0;
+    __syncthreads();
+    if (tid == 0) {
+      int ns = sh_ns, nsl = sh_nsl, bad = sh_bad;
+      auto slot = [&](int pos) {
+        if (slotof[pos] < 0) {
+          if (nsl < SLOT_MAX) m.slotpos[nsl] = pos;
+          slotof[pos] = nsl++;
+        }
+        return slotof[pos];
+      };
+      while (k < n && k < c0 + 1024) {
+        const int p = chunk[k - c0];
+        int r, kp, step;
+        if (p >= 0) {
+          r = k;
+          kp = p;
+          step = 1;
+          m.kind[k] = 0;
+        } else {
+          r = k + 1;
+          kp = -p;
+          step = 2;
+          m.kind[k] = 1;
+          if (k + 1 < n) m.kind[k + 1] = 2;
+        }
+        if (kp != r && r < n) {
+          if (kp < r || kp >= n) bad = 1;  // a backward interchange (the kp = 0 defect)
+          else {
+            m.srow[ns] = r;
+            m.sa[ns] = slot(r);
+            m.sb[ns] = slot(kp);
+            ++ns;
+            const int t = perm[r];
+            perm[r] = perm[kp];
+            perm[kp] = t;
+          }
+        }
+        k += step;
+      }
+      sh_ns = ns;
+      sh_nsl = nsl;
+      sh_bad = bad || nsl > SLOT_MAX;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += 1024) m.perm[i] = perm[i];
+  if (tid == 0) {
+    m.flag[0] = sh_bad ? 1u : 0u;
+    m.flag[1] = (unsigned)sh_ns;
+    m.flag[2] = (unsigned)sh_nsl;
+  }
+}
+
+// the pivot blocks of D (from F, before it is overwritten) and the ones vector
+__global__ void k_extract(const double* __restrict__ F, int64_t ld, int n, Meta m) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  m.ones[k] = 1.0;
+  const double d11 = F[(int64_t)k * ld + k];
+  m.d11[k] = d11;
+  const int kd = m.kind[k];
+  if (kd == 1) {
+    m.d21[k] = F[(int64_t)(k + 1) * ld + k];
+    m.d22[k] = F[(int64_t)(k + 1) * ld + k + 1];
+  }
+  // a zero pivot (an all-zero column): the reference divides by zero in its
+  // own order -- the fallback reproduces that order
+  if ((kd == 0 && d11 == 0.0) || (kd == 1 && m.d21[k] == 0.0)) atomicOr(&m.flag[0], 1u);
+}
+
+// column c of L (row c of LT): every interchange after the column's pivot
+// step applied to its entries (through the touched slots, in LDS), and a 2x2
+// pivot's d21 zeroed
+__global__ __launch_bounds__(256) void k_lprime(double* __restrict__ LT, int n, Meta m) {
+  if (m.flag[0]) return;
+  extern __shared__ double vals[];
+  __shared__ int sh_s0;
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int kd = m.kind[c];
+  const int cp = kd == 1 ? c + 1 : c;  // last row of the column's pivot step
+  const int ns = (int)m.flag[1], nsl = (int)m.flag[2];
+  double* row = LT + (int64_t)c * n;
+  if (kd == 1 && tid == 0) row[c + 1] = 0.0;
+  if (tid == 0) {  // first interchange of a later step: srow > cp (srow increases)
+    int lo = 0, hi = ns;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (m.srow[mid] > cp) hi = mid;
+      else lo = mid + 1;
+    }
+    sh_s0 = lo;
+  }
+  __syncthreads();
+  const int s0 = sh_s0;
+  if (s0 >= ns) return;
+  for (int t = tid; t < nsl; t += 256) {
+    const int pos = m.slotpos[t];
+    vals[t] = pos > cp ? row[pos] : 0.0;
+  }
+  __syncthreads();
+  if (tid == 0)
+    for (int s = s0; s < ns; ++s) {
+      const int a = m.sa[s], b = m.sb[s];
+      const double v = vals[a];
+      vals[a] = vals[b];
+      vals[b] = v;
+    }
+  __syncthreads();
+  for (int t = tid; t < nsl; t += 256) {
+    const int pos = m.slotpos[t];
+    if (pos > cp) row[pos] = vals[t];
+  }
+}
+
+// Lp[i][j] = LT[j][i], i > j (64 x 64 tiles through LDS)
+__global__ __launch_bounds__(256) void k_untranspose(const double* __restrict__ LT, int n, double* __restrict__ Lp,
+                                                     int64_t ld, const unsigned* __restrict__ flag) {
+  if (flag[0]) return;
+  __shared__ double t[64][65];
+  const int bi = blockIdx.y, bj = blockIdx.x;  // destination tile rows 64 bi.., columns 64 bj..
+  if (bj > bi) return;
+  const int c = threadIdx.x & 63;
+  for (int r = threadIdx.x >> 6; r < 64; r += 4) {  // LT rows 64 bj + r, columns 64 bi + c
+    const int j = 64 * bj + r, i = 64 * bi + c;
+    t[r][c] = (i < n && j < n && i > j) ? LT[(int64_t)j * n + i] : 0.0;
+  }
+  __syncthreads();
+  for (int r = threadIdx.x >> 6; r < 64; r += 4) {
+    const int i = 64 * bi + r, j = 64 * bj + c;
+    if (i < n && j < n && i > j) Lp[(int64_t)i * ld + j] = t[c][r];
+  }
+}
+
+__global__ void k_set_fallback(unsigned* flag) {
+  if (threadIdx.x == 0) flag[0] = 1u;
+}
+__global__ void k_gather(const double* __restrict__ b, int n, Meta m) {
+  if (m.flag[0]) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) m.t[p] = b[m.perm[p]];
+}
+__global__ void k_scatter(double* __restrict__ b, int n, Meta m) {
+  if (m.flag[0]) return;
+  const int p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) b[m.perm[p]] = m.t[p];
+}
+// y <- D^{-1} y in the reference's arithmetic (LinearSolvers.cpp:238, :250-258)
+__global__ void k_dsolve(double* __restrict__ y, int n, Meta m) {
+  if (m.flag[0]) return;
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int kd = m.kind[k];
+  if (kd == 0) {
+    y[k] = y[k] / m.d11[k];
+  } else if (kd == 1) {
+    const double akm1k = m.d21[k];
+    const double akm1 = m.d11[k] / akm1k;
+    const double ak = m.d22[k] / akm1k;
+    const double denom = akm1 * ak - 1.0;
+    const double bkm1 = y[k] / akm1k;
+    const double bk = y[k + 1] / akm1k;
+    y[k] = (ak * bkm1 - bk) / denom;
+    y[k + 1] = (akm1 * bk - bkm1) / denom;
+  }
+}
+}  // namespace bkf
+
+size_t bk_fast_meta_bytes(int n) { return bkf::layout(nullptr, n).total; }
+const unsigned* bk_fast_flag(const void* meta) { return static_cast<const unsigned*>(meta); }
+const double* bk_fast_ones(const void* meta, int n) { return bkf::layout(static_cast<char*>(const_cast<void*>(meta)), n).ones; }
+double* bk_fast_tmp(void* meta, int n) { return bkf::layout(static_cast<char*>(meta), n).t; }
+
+hipError_t bk_fast_prepare(const double* F, int64_t ld, int n, const int* ipiv, const int* info, double* LT,
+                           double* Lp, int64_t ldp, void* meta, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  bkf::Meta m = bkf::layout(static_cast<char*>(meta), n);
+  if (n > bkf::LDS_MAX_N) {  // the interchange bookkeeping lives in one workgroup's LDS: fall back
+    hipLaunchKernelGGL(bkf::k_set_fallback, dim3(1), dim3(64), 0, st, m.flag);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL(bkf::k_scan, dim3(1), dim3(1024), (size_t)2 * n * sizeof(int), st, ipiv, n, info, m);
+  hipLaunchKernelGGL(bkf::k_extract, dim3((n + 255) / 256), dim3(256), 0, st, F, ld, n, m);
+  hipLaunchKernelGGL(bkf::k_lprime, dim3(n), dim3(256), (size_t)bkf::SLOT_MAX * sizeof(double), st, LT, n, m);
+  const int nb = (n + 63) / 64;
+  hipLaunchKernelGGL(bkf::k_untranspose, dim3(nb, nb), dim3(256), 0, st, (const double*)LT, n, Lp, ldp,
+                     (const unsigned*)m.flag);
+  return hipGetLastError();
+}
+
+hipError_t bk_fast_gather(const double* b, int n, void* meta, hipStream_t st) {
+  hipLaunchKernelGGL(bkf::k_gather, dim3((n + 255) / 256), dim3(256), 0, st, b, n,
+                     bkf::layout(static_cast<char*>(meta), n));
+  return hipGetLastError();
+}
+hipError_t bk_fast_dsolve(double* y, int n, void* meta, hipStream_t st) {
+  hipLaunchKernelGGL(bkf::k_dsolve, dim3((n + 255) / 256), dim3(256), 0, st, y, n,
+                     bkf::layout(static_cast<char*>(meta), n));
+  return hipGetLastError();
+}
+hipError_t bk_fast_scatter(double* b, int n, void* meta, hipStream_t st) {
+  hipLaunchKernelGGL(bkf::k_scatter, dim3((n + 255) / 256), dim3(256), 0, st, b, n,
+                     bkf::layout(static_cast<char*>(meta), n));
+  return hipGetLastError();
+}
+hipError_t bk_fast_fallback(const double* LT, int n, const int* ipiv, double* b, const void* meta, hipStream_t st) {
+  hipLaunchKernelGGL(k_bk_solve<true>, dim3(1), dim3(BKT), 0, st, LT, (int64_t)n, n, 0, ipiv, 0, b, 0,
+                     bk_fast_flag(meta));
   return hipGetLastError();
 }
 

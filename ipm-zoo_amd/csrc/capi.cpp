@@ -236,6 +236,64 @@ int err_words_status(hipStream_t st, const unsigned* pe_word, const unsigned* se
 }
 }  // namespace
 
+}  // extern "C"
+
+// The device-wide Bunch-Kaufman solve's workspace (bk.hip bk_fast_*): the
+// persistent triangular solve's operators for L' (64 x 64 inverse diagonal
+// blocks, the 128-row-block prep), its y / x vectors and ctrl words, and the
+// interchange bookkeeping (meta)
+namespace {
+struct BkWs {
+  double *Linv = nullptr, *P = nullptr, *y = nullptr, *x = nullptr;
+  unsigned* ctrl = nullptr;
+  char* meta = nullptr;
+  int64_t total = 0;
+};
+BkWs bk_ws(char* base, int N) {
+  BkWs w;
+  int64_t off = 0;
+  auto take = [&](int64_t bytes) {
+    char* p = base ? base + off : nullptr;
+    off += round_up(bytes, 256);
+    return p;
+  };
+  w.Linv = reinterpret_cast<double*>(take((int64_t)((N + 63) / 64) * 64 * 64 * 8));
+  w.P = reinterpret_cast<double*>(take(solve_prep_elems(N) * 8));
+  w.y = reinterpret_cast<double*>(take((int64_t)N * 8));
+  w.x = reinterpret_cast<double*>(take((int64_t)N * 8));
+  w.ctrl = reinterpret_cast<unsigned*>(take(256));
+  w.meta = take((int64_t)bk_fast_meta_bytes(N));
+  w.total = off;
+  return w;
+}
+// once per factor: L' (into Lp, may be F), then the persistent solve's operators
+hipError_t bk_setup(const double* F, int64_t ld, int N, const int* ipiv, const int* info, double* LT, double* Lp,
+                    int64_t ldp, const BkWs& w, hipStream_t st) {
+  hipError_t e = bk_fast_prepare(F, ld, N, ipiv, info, LT, Lp, ldp, w.meta, st);
+  if (e == hipSuccess) e = linv_from_l(Lp, ldp, N, 64, w.Linv, st);
+  if (e == hipSuccess) e = solve_prep(Lp, ldp, N, w.Linv, w.P, st);
+  if (e == hipSuccess) e = solve_reset(w.y, w.x, sizeof(double), N, w.ctrl, st);
+  return e;
+}
+// b <- A^{-1} b: P^T L'^{-T} D^{-1} L'^{-1} P b, or the one-workgroup sweeps on
+// LT when the factor needs the reference's exact interchange order
+hipError_t bk_run(const double* Lp, int64_t ldp, int N, const double* LT, const int* ipiv, const BkWs& w, double* b,
+                  hipStream_t st) {
+  const unsigned* flag = bk_fast_flag(w.meta);
+  double* t = bk_fast_tmp(w.meta, N);
+  const double* ones = bk_fast_ones(w.meta, N);
+  hipError_t e = bk_fast_gather(b, N, w.meta, st);
+  if (e == hipSuccess) e = ldlt_solve_persistent_sweep(Lp, ldp, N, ones, w.P, t, w.y, w.x, w.ctrl, false, st, flag);
+  if (e == hipSuccess) e = bk_fast_dsolve(w.y, N, w.meta, st);
+  if (e == hipSuccess) e = ldlt_solve_persistent_sweep(Lp, ldp, N, ones, w.P, t, w.y, w.x, w.ctrl, true, st, flag);
+  if (e == hipSuccess) e = bk_fast_scatter(b, N, w.meta, st);
+  if (e == hipSuccess) e = bk_fast_fallback(LT, N, ipiv, b, w.meta, st);
+  return e;
+}
+}  // namespace
+
+extern "C" {
+
 int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N) {
   if (!ctx || N < 0) return 0;
   return ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
@@ -509,13 +567,28 @@ int ipmz_bk_solve(ipmz_ctx* ctx, int N, const double* F, int64_t ld, const int* 
     HIP_OK(bk_solve(F, ld, N, ipiv, b, 1, 0, 0, 0, ctx->stream));
     return IPMZ_OK;
   }
-  // large N: through a transposed copy (coalesced column sweeps)
-  double* lt = nullptr;
+  // large N: the device-wide solve (L' with the interchanges folded in,
+  // built here from F into stream-ordered buffers, freed after the solve)
+  const int64_t ldp = round_up(N, 64);
+  const BkWs wsz = bk_ws(nullptr, N);
+  double *lt = nullptr, *lp = nullptr;
+  char* wb = nullptr;
   HIP_OK(hipMallocAsync(reinterpret_cast<void**>(&lt), (size_t)N * N * sizeof(double), ctx->stream));
-  hipError_t e = bk_transpose(F, ld, N, lt, ctx->stream);
-  if (e == hipSuccess) e = bk_solve_lt(lt, N, ipiv, b, ctx->stream);
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&lp), (size_t)N * ldp * sizeof(double), ctx->stream);
+  if (e == hipSuccess) e = hipMallocAsync(reinterpret_cast<void**>(&wb), (size_t)wsz.total, ctx->stream);
+  const BkWs w = bk_ws(wb, N);
+  if (e == hipSuccess) e = bk_transpose(F, ld, N, lt, ctx->stream);
+  if (e == hipSuccess) e = bk_setup(F, ld, N, ipiv, nullptr, lt, lp, ldp, w, ctx->stream);
+  if (e == hipSuccess) e = bk_run(lp, ldp, N, lt, ipiv, w, b, ctx->stream);
+  unsigned serr = 0;
+  if (e == hipSuccess) e = hipMemcpyAsync(&serr, w.ctrl + SOLVE_ERR_WORD, 4, hipMemcpyDeviceToHost, ctx->stream);
+  if (wb) hipFreeAsync(wb, ctx->stream);
+  if (lp) hipFreeAsync(lp, ctx->stream);
   hipFreeAsync(lt, ctx->stream);
   HIP_OK(e);
+  HIP_OK(hipStreamSynchronize(ctx->stream));
+  if (serr) return fail(IPMZ_ERR_HIP, "ipmz_bk_solve: a hand-off inside the persistent triangular solve timed out "
+                                      "(spin limit 0.5 s); the solution is invalid");
   return IPMZ_OK;
 }
 
@@ -676,7 +749,8 @@ struct ipmz_qp {
   // EqualityHandling::None: Bunch-Kaufman factor (pivots per QP)
   bool eqnone = false;
   char* bkws = nullptr;  // the whole-device Bunch-Kaufman factor's workspace (B == 1, N >= IPMZ_BK_GRID_MIN)
-  double* bklt = nullptr;  // its factor transposed (N x N), for coalesced solves
+  double* bklt = nullptr;  // its factor transposed (N x N): the interchange folding's input, the fallback's factor
+  char* bkfws = nullptr;   // the device-wide solve's workspace (bk_ws), L' in K
   unsigned* pflags = nullptr;  // B > 1: the two-workgroup small factor's flags + sticky error word
   int small_kernel = IPMZ_BATCH_FACTOR_AUTO;  // ipmz_batch_set_factor_kernel
   bool eqpen = false;  // EqualityHandling::PenaltyFunction (LDL^T)
@@ -754,7 +828,9 @@ void carve(const ipmz_qp* s, double* base, double** slots) {
 QPDev& q0(ipmz_qp* s) { return s->hq[0]; }
 
 int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
-  if (s->eqnone && s->bklt) {  // overwriting_solve_bunch_kaufman on the transposed factor
+  if (s->eqnone && s->bkfws) {  // overwriting_solve_bunch_kaufman, device-wide (L' in K)
+    HIP_OK(bk_run(s->K, s->ldk, s->N, s->bklt, s->ipiv, bk_ws(s->bkfws, s->N), q0(s).b, st));
+  } else if (s->eqnone && s->bklt) {  // overwriting_solve_bunch_kaufman on the transposed factor
     HIP_OK(bk_solve_lt(s->bklt, s->N, s->ipiv, q0(s).b, st));
   } else if (s->eqnone) {  // overwriting_solve_bunch_kaufman
     HIP_OK(bk_solve(s->K, s->ldk, s->N, s->ipiv, q0(s).b, s->B, s->sK, s->sP, s->sb, st));
@@ -780,6 +856,9 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
     if (s->bkws) {
       HIP_OK(bk_factor_grid(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->bkws, s->ctx->stream));
       HIP_OK(bk_transpose(s->K, s->ldk, s->N, s->bklt, s->ctx->stream));
+      if (s->bkfws)  // L' into K (the factor is not read again this step)
+        HIP_OK(bk_setup(s->K, s->ldk, s->N, s->ipiv, s->binfo, s->bklt, s->K, s->ldk, bk_ws(s->bkfws, s->N),
+                        s->ctx->stream));
       return IPMZ_OK;
     }
     HIP_OK(bk_factor(s->K, s->ldk, s->N, s->ipiv, s->binfo, 0, s->B, s->sK, s->sP, s->ctx->stream));
@@ -1026,6 +1105,10 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
       if (ok) ok = hipMalloc(&w, (size_t)N * N * sizeof(double)) == hipSuccess;
       if (ok) s->allocs.push_back(w);
       s->bklt = static_cast<double*>(w);
+      const int64_t bkb = bk_ws(nullptr, N).total;
+      if (ok) ok = hipMalloc(&w, (size_t)bkb) == hipSuccess && hipMemset(w, 0, (size_t)bkb) == hipSuccess;
+      if (ok) s->allocs.push_back(w);
+      s->bkfws = static_cast<char*>(w);
     }
   }
   if (!ok) {
@@ -1226,11 +1309,15 @@ int qp_status(ipmz_qp* s) {
                                      "step is invalid");
   }
   if (s->bkws) {
-    unsigned e = 0;
-    HIP_OK(hipMemcpyAsync(&e, bk_grid_err_word(s->bkws, s->N), 4, hipMemcpyDeviceToHost, st));
+    unsigned e[2] = {0, 0};
+    HIP_OK(hipMemcpyAsync(&e[0], bk_grid_err_word(s->bkws, s->N), 4, hipMemcpyDeviceToHost, st));
+    if (s->bkfws)
+      HIP_OK(hipMemcpyAsync(&e[1], bk_ws(s->bkfws, s->N).ctrl + SOLVE_ERR_WORD, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
-    if (e) return fail(IPMZ_ERR_HIP, "Newton step: a grid barrier of the whole-device Bunch-Kaufman factor timed "
-                                     "out; the step is invalid");
+    if (e[0]) return fail(IPMZ_ERR_HIP, "Newton step: a grid barrier of the whole-device Bunch-Kaufman factor timed "
+                                        "out; the step is invalid");
+    if (e[1]) return fail(IPMZ_ERR_HIP, "Newton step: a hand-off inside the persistent triangular solve of the "
+                                        "Bunch-Kaufman factor timed out; the step is invalid");
   }
   return IPMZ_OK;  // batched / one-workgroup Bunch-Kaufman kernels have no cross-workgroup spins
 }

@@ -124,6 +124,11 @@ hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, do
 hipError_t solve_prep(const float* K, int64_t ld, int N, const float* Linv, float* P, hipStream_t st);
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* P, double* b,
                                  double* ybuf, double* xbuf, unsigned* ctrl, hipStream_t st);
+// one sweep (forward: ybuf = L^{-1} b; backward: b = L^{-T} (ybuf / D)); skip
+// (device flag, may be null): return at once when set
+hipError_t ldlt_solve_persistent_sweep(const double* K, int64_t ld, int N, const double* D, const double* P,
+                                       double* b, double* ybuf, double* xbuf, unsigned* ctrl, bool backward,
+                                       hipStream_t st, const unsigned* skip);
 // fp32 variant; skip (device flag, may be null): return at once when set
 hipError_t ldlt_solve_persistent(const float* K, int64_t ld, int N, const float* D, const float* P, float* b,
                                  float* ybuf, float* xbuf, unsigned* ctrl, hipStream_t st,
@@ -171,6 +176,26 @@ const unsigned* bk_grid_err_word(const void* ws, int n);
 // factor): coalesced sweeps, the same arithmetic as bk_solve
 hipError_t bk_transpose(const double* F, int64_t ld, int n, double* LT, hipStream_t st);
 hipError_t bk_solve_lt(const double* LT, int n, const int* ipiv, double* b, hipStream_t st);
+// Device-wide solve: A^{-1} b = P^T L'^{-T} D^{-1} L'^{-1} P b, L' = L with every
+// later interchange folded into its columns (once per factor, bk_fast_prepare:
+// from F, ipiv, the factor's info word and LT = bk_transpose(F); LT is
+// permuted in place, L' written to the strict lower triangle of Lp, which may
+// be F itself; meta: bk_fast_meta_bytes).  Then the persistent solve's
+// operators are built from Lp (linv_from_l, solve_prep, solve_reset) and a
+// solve is gather -> forward sweep -> dsolve (ybuf) -> backward sweep (D =
+// ones) -> scatter, all gated on meta's fallback flag, + bk_fast_fallback
+// (the one-workgroup sweeps on the untouched LT, run only when the flag is
+// set: a singular factor, or n > 16384).
+size_t bk_fast_meta_bytes(int n);
+const unsigned* bk_fast_flag(const void* meta);
+const double* bk_fast_ones(const void* meta, int n);
+double* bk_fast_tmp(void* meta, int n);
+hipError_t bk_fast_prepare(const double* F, int64_t ld, int n, const int* ipiv, const int* info, double* LT,
+                           double* Lp, int64_t ldp, void* meta, hipStream_t st);
+hipError_t bk_fast_gather(const double* b, int n, void* meta, hipStream_t st);
+hipError_t bk_fast_dsolve(double* y, int n, void* meta, hipStream_t st);
+hipError_t bk_fast_scatter(double* b, int n, void* meta, hipStream_t st);
+hipError_t bk_fast_fallback(const double* LT, int n, const int* ipiv, double* b, const void* meta, hipStream_t st);
 
 // newton.hip -----------------------------------------------------------------
 enum Slot { X = 0, LA, LC, S, P, LG, LH, LY, LZ, G, H, Y, Z, NSLOT };

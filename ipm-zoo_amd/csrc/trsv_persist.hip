@@ -564,6 +564,27 @@ static hipError_t solve_persistent_t(const T* K, int64_t ld, int N, const T* D, 
   return hipGetLastError();
 }
 
+// one sweep of the persistent solve (forward: y = L^{-1} b into ybuf;
+// backward: b = L^{-T} (ybuf / D)) -- the Bunch-Kaufman solve applies its
+// block-diagonal D between the two (bk_fast_dsolve on ybuf, D = ones here)
+hipError_t ldlt_solve_persistent_sweep(const double* K, int64_t ld, int N, const double* D, const double* P,
+                                       double* b, double* ybuf, double* xbuf, unsigned* ctrl, bool backward,
+                                       hipStream_t st, const unsigned* skip) {
+  if (N <= 0) return hipSuccess;
+  if (ld % 2) return hipErrorInvalidValue;
+  const int nb = (N + SB - 1) / SB;
+  const int64_t q = (int64_t)nb * SB * SB;
+  const int grid = nb < 256 ? nb : 256;
+  const int inject = debug_inject_mask() & IPMZ_INJECT_SOLVE;
+  if (backward)
+    hipLaunchKernelGGL((trsv128_kernel<double, true>), dim3(grid), dim3(SNT), 0, st, K, ld, N, D, P, P + q, P + 2 * q,
+                       P + 3 * q, b, ybuf, xbuf, ctrl, nb, skip, inject);
+  else
+    hipLaunchKernelGGL((trsv128_kernel<double, false>), dim3(grid), dim3(SNT), 0, st, K, ld, N, D, P, P + q,
+                       P + 2 * q, P + 3 * q, b, ybuf, xbuf, ctrl, nb, skip, inject);
+  return hipGetLastError();
+}
+
 hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st) {
   hipError_t e = hipMemsetAsync(ctrl, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), st);  // tickets + sticky error
   if (e == hipSuccess) e = hipMemsetAsync(ybuf, 0xff, (size_t)N * elem, st);

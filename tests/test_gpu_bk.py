@@ -162,3 +162,42 @@ def test_bk_grid_fix_kp(ctx):
         _, po, info_o = oracle.bk_factor(K, fix_kp=fix)
         assert info == info_o + 1
         assert np.array_equal(piv, po.astype(np.int32))
+
+
+# ---------------------------------------------------------------------------
+# The device-wide solve (bk_fast_*, from N = 512): the interleaved
+# interchanges folded into L' once per factor, the two sweeps on the
+# persistent triangular solve, D's 1x1 / 2x2 blocks in the reference's
+# arithmetic (LinearSolvers.cpp:209-318).  Tolerance as the golden solves:
+# 1e-12 relative to the oracle's reference-order solve.
+@pytest.mark.parametrize("n,m", [(700, 300), (3000, 600)])
+def test_bk_fast_solve_kkt_vs_oracle(ctx, n, m):
+    K = _kkt_zero_block(n, m, n + 1)
+    F, ipiv = I.LinearSolvers.symmetric_indefinite_factorization(K, ctx)
+    Fo, po, _ = oracle.bk_factor(K)
+    assert (po < 0).any() and (po != np.arange(n + m)).any()  # 2x2 pivots and interchanges
+    assert np.array_equal(ipiv, po.astype(np.int32)) and np.array_equal(F, Fo)
+    b = np.random.default_rng(2).uniform(-1, 1, n + m)
+    ref = oracle.bk_solve(Fo, po, b)
+    x = b.copy()
+    I.LinearSolvers.overwriting_solve_bunch_kaufman(F, ipiv, x, ctx)
+    assert np.abs(x - ref).max() <= 1e-12 * max(1.0, np.abs(ref).max())
+    assert np.abs(K @ x - b).max() < 1e-10 * max(1.0, np.abs(K).max() * np.abs(x).max())
+
+
+def test_bk_fast_solve_singular_falls_back(ctx):
+    # all-zero columns: the reference divides by zero (and its kp = 0 defect
+    # swaps backwards); the device solve then runs the reference's own
+    # interleaved sweeps, so the non-finite entries are the oracle's
+    N = 900
+    K = _indef(N, 11, zeros=2)
+    F, ipiv = I.LinearSolvers.symmetric_indefinite_factorization(K, ctx)
+    Fo, po, _ = oracle.bk_factor(K)
+    assert np.array_equal(ipiv, po.astype(np.int32))
+    b = np.random.default_rng(3).uniform(-1, 1, N)
+    ref = oracle.bk_solve(Fo, po, b)
+    x = b.copy()
+    I.LinearSolvers.overwriting_solve_bunch_kaufman(F, ipiv, x, ctx)
+    assert np.array_equal(np.isfinite(x), np.isfinite(ref))
+    fin = np.isfinite(ref)
+    assert np.abs(x[fin] - ref[fin]).max() <= 1e-12 * max(1.0, np.abs(ref[fin]).max())
