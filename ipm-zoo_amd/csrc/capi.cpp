@@ -327,6 +327,7 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
   // fork: A, C (panel path) and B (trailing updates) start after the caller's stream
+  IPMZ_TRACE("factor_impl: fork");
   HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
   HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
   HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
@@ -334,8 +335,10 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
                      pctrl));
   // join (A has already waited for B's tail)
+  IPMZ_TRACE("factor_impl: join");
   HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
   HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  IPMZ_TRACE("factor_impl: joined");
   HIP_OK(prep());
   return IPMZ_OK;
 }
@@ -891,6 +894,7 @@ int run_step(ipmz_qp* s, int flags) {
   const QPBatch& qb = s->qb;
   const bool t = s->timing;
   auto mark = [&](int i) {
+    IPMZ_TRACE("step: phase mark %d", i);
     if (t) hipEventRecord(s->ev[i], st);
   };
   const bool restart = flags & IPMZ_STEP_RESTART_IF_CONVERGED;
@@ -1264,12 +1268,15 @@ int step_impl(ipmz_qp* s, int flags) {
     // legacy default stream (torch's), which cannot be captured; the graph
     // is then launched on the caller's stream
     hipStream_t cap = s->ctx->own;
+    IPMZ_TRACE("capture: begin");
     HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
     s->ctx->stream = cap;
     int rc = run_step(s, flags);
     s->ctx->stream = st;
+    IPMZ_TRACE("capture: step enqueued rc=%d", rc);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(cap, &g);
+    IPMZ_TRACE("capture: ended %d", (int)e);
     if (rc) {
       if (g) hipGraphDestroy(g);
       return rc;
@@ -1277,9 +1284,11 @@ int step_impl(ipmz_qp* s, int flags) {
     if (e != hipSuccess) return fail(IPMZ_ERR_HIP, std::string("graph capture: ") + hipGetErrorString(e));
     s->graph = g;
     HIP_OK(hipGraphInstantiate(&s->gexec, g, nullptr, nullptr, 0));
+    IPMZ_TRACE("capture: instantiated");
     s->graph_flags = flags;
   }
   HIP_OK(hipGraphLaunch(s->gexec, st));
+  IPMZ_TRACE("graph launched");
   s->last_step_graph = 1;
   return IPMZ_OK;
 }

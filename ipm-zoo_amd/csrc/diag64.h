@@ -140,10 +140,16 @@ using namespace diag64;
 // zero, identity padding past b) -- handed over through LDS by its producer.
 // NW: waves in the workgroup (4 or 8); waves >= 4 only load/store and join
 // the barriers.
-template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4>
+// PRE_WB: called by every thread once L, D and X are final in LDS, before
+// their write-back (the panel chain issues the next block's operand loads
+// there, so their latency overlaps the write-back's stores).
+struct NoHook {
+  __device__ void operator()() const {}
+};
+template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
-                                            double* dsh, unsigned long long* clkbuf) {
+                                            double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB()) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
@@ -183,9 +189,12 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     acc = tile_nt_lds(Mt(i, p), Mt(j, p), &dsh[16 * p], acc, lane);
     tile_store(Mt(i, j), acc, lane);
   };
-  auto xoff = [&](int p, int j) {  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
+  auto xsum = [&](int p, int j) {  // S = sum_{k=j}^{p-1} L_pk X_kj
     double4_t sacc = {0.0, 0.0, 0.0, 0.0};
     for (int k = j; k < p; ++k) sacc = tile_nn(Mt(p, k), Xt(k, j), sacc, lane);
+    return sacc;
+  };
+  auto xmul = [&](int p, int j, double4_t sacc) {  // X_pj = -X_pp S
     // S in accumulator layout IS the NN B-fragment
     double4_t acc = {0.0, 0.0, 0.0, 0.0};
     const double* xp = Xt(p, p);
@@ -193,6 +202,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     for (int q = 0; q < 4; ++q) acc = mfma_f64_16x16x4(-xp[(lane & 15) * DS + 4 * q + (lane >> 4)], sacc[q], acc);
     tile_store(Xt(p, j), acc, lane);
   };
+  auto xoff = [&](int p, int j) { xmul(p, j, xsum(p, j)); };  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
   if (wave == 0) colpass16(M, dsh, 0, lane);
   __syncthreads();
   clk();
@@ -226,12 +236,16 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     __syncthreads();
     clk();
   }
-  // ---- the last row of inverse tiles
+  // ---- the last row of inverse tiles: X_33 on wave 0 while waves 1..3 sum
+  // S_3j = sum_k L_3k X_kj (X_33 is not needed for those), then X_3j = -X_33 S_3j
+  double4_t s3 = {0.0, 0.0, 0.0, 0.0};
   if (wave == 0) inv16(Mt(3, 3), Xt(3, 3), lane);
+  else if (wave < 4) s3 = xsum(3, wave - 1);
   __syncthreads();
-  if (wave < 3) xoff(3, wave);
+  if (wave >= 1 && wave < 4) xmul(3, wave - 1, s3);
   __syncthreads();
   clk();
+  pre_wb();
   // write back L (strict lower), D, and L^{-1} (64 x 64 row-major, identity-padded)
 #pragma unroll 4
   for (int idx = tid; idx < 64 * 64; idx += 64 * NW) {

@@ -40,10 +40,11 @@ using GemmArgs = GemmArgsT<double>;
 // Tile pipeline: one LDS buffer is computed while the next k-chunk sits in
 // registers (loads issued before the MFMAs, written to the other buffer
 // after them): one barrier per 16-deep k-chunk.
-template <typename T, int BM, int BN, int NTH>
+template <typename T, int BM, int BN, int NTH, int BK_ = 16>
 struct TileLoader {
   typedef typename Mfma<T>::vec2_t V2;
-  static constexpr int BK = 16, PAD = 18;
+  static constexpr int BK = BK_, PAD = BK_ + 2;  // (PAD = BK + 2: conflict-free fragment reads for BK 16 and 32)
+  static constexpr int CPR = BK / 2;             // double2 / float2 chunks per row
   static constexpr int QA = BM * BK / 2 / NTH, QB = BN * BK / 2 / NTH;  // double2 per thread
   // every thread loads whole double2 chunks: a tile side with fewer chunks
   // than threads (e.g. BM = 64 at 16 waves) would load NOTHING
@@ -53,12 +54,12 @@ struct TileLoader {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch / CPR, c = (ch % CPR) * 2;
       ra[q] = fetch(g.A, g.lda, i0 + r, g.M, kk + c, g.Kd);
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch / CPR, c = (ch % CPR) * 2;
       rb[q] = fetch(g.B, g.ldb, j0 + r, g.N, kk + c, g.Kd);
     }
   }
@@ -66,12 +67,12 @@ struct TileLoader {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int q = 0; q < QA; ++q) {
-      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch / CPR, c = (ch % CPR) * 2;
       *reinterpret_cast<V2*>(&As[r * PAD + c]) = ra[q];
     }
 #pragma unroll
     for (int q = 0; q < QB; ++q) {
-      const int ch = tid + NTH * q, r = ch >> 3, c = (ch & 7) * 2;
+      const int ch = tid + NTH * q, r = ch / CPR, c = (ch % CPR) * 2;
       *reinterpret_cast<V2*>(&Bs[r * PAD + c]) = rb[q];
     }
   }
@@ -134,11 +135,12 @@ __device__ __forceinline__ void grouped_tile(int bid, int ntm, int& tm, int& tn)
 // silently halves the occupancy.
 template <int NW>
 constexpr int gemm_waves_per_eu() { return NW == 16 ? 8 : NW == 8 ? 4 : 1; }
-template <typename T, int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2>
+// BK: k-depth of one LDS stage (one barrier per stage)
+template <typename T, int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2, int BK = 16>
 __global__ __launch_bounds__(64 * WGM * WGN)
 __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_nt_kernel(GemmArgsT<T> g) {
   typedef Mfma<T> MF;
-  constexpr int BK = 16, PAD = 18, NTH = 64 * WGM * WGN;
+  constexpr int PAD = BK + 2, NTH = 64 * WGM * WGN;
   if (blockIdx.y) {
     const int64_t z = blockIdx.y;
     g.A += z * g.sA;
@@ -189,7 +191,7 @@ __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_n
 #pragma unroll
     for (int b = 0; b < TN; ++b) acc[a][b] = (typename MF::acc_t){T(0), T(0), T(0), T(0)};
 
-  TileLoader<T, BM, BN, NTH> ld;
+  TileLoader<T, BM, BN, NTH, BK> ld;
   const int nch = (g.Kd + BK - 1) / BK;
   ld.load(g, i0, j0, 0);
   ld.store(As[0], Bs[0]);
@@ -248,7 +250,7 @@ __attribute__((amdgpu_waves_per_eu(gemm_waves_per_eu<WGM * WGN>()))) void gemm_n
   }  // tiles
 }
 
-template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2, typename T = double>
+template <int BM, int BN, int EPI, int WGM = 2, int WGN = 2, int OPT = OPT_NOR2, int BK = 16, typename T = double>
 static hipError_t launch_gemm(GemmArgsT<T> g, hipStream_t st, int batch = 1) {
   g.ntm = (g.M + BM - 1) / BM;
   g.ntn = (g.N + BN - 1) / BN;
@@ -261,7 +263,7 @@ static hipError_t launch_gemm(GemmArgsT<T> g, hipStream_t st, int batch = 1) {
     else g.lower = 1;
   }
   if ((OPT & OPT_PERSIST) && g.persist > 0 && nblk > g.persist) nblk = g.persist;
-  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, EPI, WGM, WGN, OPT>), dim3((unsigned)nblk, (unsigned)batch),
+  hipLaunchKernelGGL((gemm_nt_kernel<T, BM, BN, EPI, WGM, WGN, OPT, BK>), dim3((unsigned)nblk, (unsigned)batch),
                      dim3(64 * WGM * WGN), 0, st, g);
   return hipGetLastError();
 }

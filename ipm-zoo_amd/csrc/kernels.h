@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #define IPMZ_NBO_MAX 512
 #define IPMZ_PANEL_CTRL_WORDS 256
@@ -18,8 +19,17 @@ namespace ipmz {
 // tests/test_gpu_graph.py) instead of enqueuing them eagerly.
 // DEBUG bits (determinism experiments): 16 = the mixed factor stops after
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
+// 64 = trace the host calls of a step to stderr (the capture experiment)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
-       IPMZ_DEBUG_ONE_STREAM = 32 };
+       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64 };
+#define IPMZ_TRACE(...)                                                  \
+  do {                                                                   \
+    if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
+      fprintf(stderr, "[ipmz] " __VA_ARGS__);                            \
+      fputc('\n', stderr);                                              \
+      fflush(stderr);                                                    \
+    }                                                                    \
+  } while (0)
 int debug_inject_mask();
 void set_debug_inject_mask(int mask);
 // error words the persistent kernels raise on a spin timeout (sync.h): the

@@ -433,6 +433,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // everything the caller enqueued on st before the factor (the mixed path's
   // fp32 conversion, the ctrl-word memsets) comes first on B and C as well
   hipEvent_t evEntry = ev[4 * npan + 1];
+  IPMZ_TRACE("factor: N=%d npan=%d look-ahead", N, npan);
   if ((e = hipEventRecord(evEntry, st)) != hipSuccess) return e;
   if ((e = hipStreamWaitEvent(st2, evEntry, 0)) != hipSuccess) return e;
   if (fused && (e = hipStreamWaitEvent(sC, evEntry, 0)) != hipSuccess) return e;
@@ -448,6 +449,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     const int p2 = p1 < N ? p1 + pw(k + 1) : N;      // start of P_{k+2}
     const int p3 = p2 < N ? p2 + pw(k + 2) : N;      // start of P_{k+3}
     if (p1 >= N) break;
+    IPMZ_TRACE("factor: panel %d", k);
     if ((e = hipEventRecord(evP[k], st)) != hipSuccess) return e;
     // ---- stream B: P_{k+2} columns first, then the rest
     if ((e = hipStreamWaitEvent(st2, evP[k], 0)) != hipSuccess) return e;

@@ -302,15 +302,35 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
     for (int j = 0; j < nb; ++j) {
       const int j0 = k0 + 64 * j, bj = bsz(j);
       T* Lb = Lb0 + (int64_t)j * 64 * 64;
-      if (j == 0 && !Wprev) diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr);
-      else diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr);
-      if (j + 1 >= nb) {
+      // ---- block row c = j + 1: (c, j) and (c, c) from helper c.  Once the
+      // diagonal block is final in LDS and before its write-back, one load
+      // per 128-byte line of both tiles pulls them into this XCD's L2 (the
+      // helper stored them write-through): the operand loads after the
+      // write-back then hit L2 instead of paying the HBM latency on the chain
+      const bool more = j + 1 < nb;
+      const int c = j + 1, r0 = k0 + 64 * c, rows = more ? bsz(c) : 0;
+      bool ok = true;
+      T pf[2] = {T(0), T(0)};
+      auto next_prefetch = [&]() {
+        if (!more) return;
+        ok = wait_flag(&area[OP_READY + c], err, sh_ok);  // (uniform)
+        if (!ok) return;
+        const int line = threadIdx.x, rr = line >> 2, cc = (line & 3) * (128 / (int)sizeof(T));
+        if (rr < rows) {
+          pf[0] = ld_sc1(&K[(int64_t)(r0 + rr) * ld + j0 + (cc < 64 ? cc : 0)]);
+          pf[1] = ld_sc1(&K[(int64_t)(r0 + rr) * ld + r0 + (cc <= rr ? cc : 0)]);
+        }
+      };
+      if (j == 0 && !Wprev)
+        diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr, next_prefetch);
+      else
+        diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr, next_prefetch);
+      if (!more) {
         if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
         break;
       }
-      // ---- block row c = j + 1: (c, j) and (c, c) from helper c
-      const int c = j + 1, r0 = k0 + 64 * c, rows = bsz(c);
-      if (!wait_flag(&area[OP_READY + c], err, sh_ok)) return;
+      if (!ok) return;
+      asm volatile("" ::"v"(pf[0]), "v"(pf[1]));  // the prefetches stay live (not eliminated) until here
       // A(c, j) into M (free: L_jj is in K), the own block (c, c) into registers
       stage_tile<T, true>(reinterpret_cast<T*>(M), K + (int64_t)r0 * ld + j0, ld, rows, 64);
       acc_t own[4];

@@ -50,3 +50,14 @@ for N in [int(a) for a in sys.argv[1:]] or [1024, 4096, 11264]:
     torch.cuda.synchronize()
     ts = time.perf_counter() - t
     print(f"bk solve     N={N:6d}: {ts * 1e3:9.2f} ms", flush=True)
+    if N >= 2048:  # the solve inside the EQ None Newton step: once-per-factor prep in the factor phase
+        n_, p_ = N - N // 8 - N // 16, N // 16
+        g = I.Optimizer(n_, N // 8, p_, ctx, equality_handling=I.EQ_NONE)
+        g.generate(1)
+        g.set_timing(True)
+        for _ in range(2):
+            g.step()
+        ph = g.phase_times()
+        print(f"EQ None step N={N:6d}: factor {ph['factor'] / 2:8.2f} ms, two solves {ph['solve'] / 2:7.3f} ms per step",
+              flush=True)
+        g.close()

@@ -14,7 +14,7 @@ segv = ctypes.CDLL(os.path.join(REPO, "tools", "dbg", "libsegv.so"))
 torch.cuda.set_device(0)
 torch.zeros(1, device="cuda")
 segv.segv_install()  # after the HIP runtime's own initialisation (it may install handlers)
-I.debug_inject(I.INJECT_GRAPH_FORKS)
+I.debug_inject(I.INJECT_GRAPH_FORKS | (64 if os.environ.get('PROBE_TRACE') else 0))
 sizes = [(int(a), int(b), int(c)) for a, b, c in (s.split(",") for s in sys.argv[1:])] or [(1024, 256, 128)]
 for use_torch_stream in (False, True):
     ctx = I.Context(0, stream=torch.cuda.current_stream().cuda_stream) if use_torch_stream else I.Context(0)

@@ -5,7 +5,7 @@ k_assemble and the first solve kernel after it.  Prints, per queue, busy time
 and idle gaps, and per outer panel the panel launch and what the other queue
 ran meanwhile.
 
-    python tools/factor_timeline.py <kernel_trace.csv> [--all]
+    python tools/factor_timeline.py <kernel_trace.csv> [--all] [--at i]   (i-th assembly, default -1 = last)
 """
 import csv
 import sys
@@ -30,7 +30,10 @@ def main():
                    int(r.get("Grid_Size_X", r.get("Grid_Size", 0)))))
     rs.sort()
     # bench trace: after the last KKT assembly; kbench trace: after the last fill
-    ia = [i for i, r in enumerate(rs) if "k_assemble" in r[2] or "fill_qd" in r[2]][-1]
+    at = int(sys.argv[sys.argv.index("--at") + 1]) if "--at" in sys.argv else -1
+    starts = [i for i, r in enumerate(rs) if "k_assemble" in r[2] or "fill_qd" in r[2]]
+    print(f"{len(starts)} factor phases in the trace; showing #{at}")
+    ia = starts[at]
     fac = []
     for r in rs[ia + 1:]:
         if "trsv" in r[2] or "fill_qd" in r[2]:

@@ -155,6 +155,28 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (mode == "g32") {  // fp32 trailing-update variants: kbench N g32 v1 v2 ... (rank 512, R = N - 512)
+    float* K32 = reinterpret_cast<float*>(K);
+    float* W32 = reinterpret_cast<float*>(W);
+    const int64_t ld32 = ld;
+    for (int a = 3; a < argc; ++a) {
+      const int var = std::atoi(argv[a]);
+      for (int R : {N / 2, N - 512}) {
+        const int rank = 512;
+        hipError_t e = ipmz::gemm_nt_sub_variant32(var, R, R, rank, W32, rank, K32, ld32, K32 + (int64_t)rank * ld32 + rank, ld32, st);
+        if (e != hipSuccess) {
+          std::printf("g32 %d: %s\n", var, hipGetErrorString(e));
+          break;
+        }
+        t.start(st);
+        for (int r = 0; r < 5; ++r)
+          CK(ipmz::gemm_nt_sub_variant32(var, R, R, rank, W32, rank, K32, ld32, K32 + (int64_t)rank * ld32 + rank, ld32, st));
+        const float ms = t.stop(st) / 5;
+        std::printf("g32 %2d R=%5d rank=%d: %.3f ms %.2f TFLOP/s\n", var, R, rank, ms, (double)R * (R + 1) * rank / ms / 1e9);
+      }
+    }
+    return 0;
+  }
   if (mode == "sustain") {  // the trailing update back to back: clock / power drift over ~60 ms
     const int rank = 512, R = N - 3 * rank;
     for (int g = 0; g < 8; ++g) {

@@ -44,6 +44,39 @@ hipError_t gemm_nt_sub_variant(int variant, int M, int N, int Kd, const double* 
     case 21: return launch_gemm<64, 64, EPI_SUB_STRIP, 2, 2, OPT_NOR2>(g, st);
     case 22: return launch_gemm<64, 128, EPI_SUB_STRIP, 2, 4, OPT_NOR2>(g, st);
     case 24: return launch_gemm<128, 128, EPI_SUB_STRIP, 4, 4, OPT_NOR2>(g, st);
+    default: break;
+  }
+  g.lower = 2;
+  switch (variant) {  // stage depth BK = 32 (half the barriers per k)
+    case 40: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP, 32>(g, st);
+    case 41: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP, 32>(g, st);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// fp32 trailing-update variants (the mixed-precision factor, C5)
+hipError_t gemm_nt_sub_variant32(int variant, int M, int N, int Kd, const float* A, int64_t lda, const float* B,
+                                 int64_t ldb, float* C, int64_t ldc, hipStream_t st) {
+  GemmArgsT<float> g{};
+  g.M = M;
+  g.N = N;
+  g.Kd = Kd;
+  g.A = A;
+  g.lda = lda;
+  g.B = B;
+  g.ldb = ldb;
+  g.C = C;
+  g.ldc = ldc;
+  g.lower = 2;
+  switch (variant) {
+    case 0: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st);  // the product's fp32 tile
+    case 1: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st);
+    case 2: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP, 32>(g, st);
+    case 3: return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP, 32>(g, st);
+    case 4: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_GRP, 32>(g, st);
+    case 5: return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP, 64>(g, st);
+    case 6: return launch_gemm<256, 256, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP, 16>(g, st);
+    case 7: return launch_gemm<256, 256, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP, 32>(g, st);
     default: return hipErrorInvalidValue;
   }
 }
