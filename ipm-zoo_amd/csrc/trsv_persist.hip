@@ -34,8 +34,8 @@
 
 namespace ipmz {
 
-// -DIPMZ_SOLVE_STAMPS: per forward block start / bulk done / critical wait / stored clocks (tools/kbench)
-__device__ unsigned long long g_sstamp[2][256][4];
+// -DIPMZ_SOLVE_STAMPS: per forward block start / bulk done / critical wait / stored / y_{J-1} seen clocks (tools/kbench)
+__device__ unsigned long long g_sstamp[2][256][6];
 #ifdef IPMZ_SOLVE_STAMPS
 #define SSTAMP(J, i) \
   if (tid == 0 && (J) < 256) g_sstamp[0][J][i] = __builtin_amdgcn_s_memrealtime()
@@ -352,13 +352,7 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
       auto row_ok = [&](int k) { return RP_ROWS * rg + k < R; };
       T acc[RP_ROWS] = {T(0), T(0), T(0), T(0)};
       Tile ta, tb;  // the next two tiles in flight
-      // X_J and b_J -> LDS up front; M_J is loaded when the bulk is done (its
-      // latency hides behind X_J v and the wait for y_{J-1})
-      if (J > 0) {  // M_J through LDS once: warms this XCD's L2 for the reload after the bulk
-        load_rows(ta, M + (int64_t)J * SB * SB);
-        put_xs(ta);
-        lds_sync();
-      }
+      // X_J and b_J -> LDS up front
       load_rows(ta, X + (int64_t)J * SB * SB);
       if (tid < SB) bj[tid] = tid < R ? b[J0 + tid] : T(0);
       put_xs(ta);
@@ -373,21 +367,37 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
             t[8 * k + 2 * j + 1] = v2.y;
           }
       };
-      // bulk: K < J-1, in pairs of tiles as their vectors complete, the next
-      // pair in flight
-      const int Kend = J - 1;
-      if (Kend > 0) load_tile(ta, 0);
-      if (Kend > 1) load_tile(tb, 1);
-      for (int Kc = 0; Kc < Kend; Kc += 2) {
-        const bool two = Kc + 1 < Kend;
+      // bulk: K < J-1.  Tiles K < J-2 in pairs as their vectors complete, the
+      // next pair in flight; the last one, L_{J,J-2}, alone, so that M_J is
+      // loaded into the other register tile as soon as y_{J-3} has been
+      // consumed -- two hops before the hand-off needs it (loaded after the
+      // bulk, its reload sat on the chain: DESIGN.md §4, the solve)
+      const int Kp = J - 2;  // pairs region [0, Kp)
+      const T* Mj = M + (int64_t)J * SB * SB;
+      if (Kp > 0) {
+        load_tile(ta, 0);
+        if (Kp > 1) load_tile(tb, 1);
+        else load_rows(tb, Mj);
+      } else if (J >= 1) {
+        if (J == 2) load_tile(ta, 0);
+        load_rows(tb, Mj);
+      }
+      for (int Kc = 0; Kc < Kp; Kc += 2) {
+        const bool two = Kc + 1 < Kp;
         if (!stage(ybuf, Kc, two ? 2 : 1, 1)) return;
         dot_rows(acc, ta, vs[0]);
         if (two) dot_rows(acc, tb, vs[1]);
-        if (Kc + 2 < Kend) load_tile(ta, Kc + 2);
-        if (Kc + 3 < Kend) load_tile(tb, Kc + 3);
+        load_tile(ta, Kc + 2 < Kp ? Kc + 2 : J - 2);
+        if (two) {  // tb consumed: the next pair's second tile, or M_J
+          if (Kc + 3 < Kp) load_tile(tb, Kc + 3);
+          else load_rows(tb, Mj);
+        }
+      }
+      if (J >= 2) {  // L_{J,J-2} y_{J-2}
+        if (!stage(ybuf, J - 2, 1, 1)) return;
+        dot_rows(acc, ta, vs[0]);
       }
       SSTAMP(J, 1);
-      if (J > 0) load_rows(tb, M + (int64_t)J * SB * SB);  // an L2 hit
 #pragma unroll
       for (int k = 0; k < RP_ROWS; ++k) acc[k] = lanes16_sum(acc[k]);
       lds_sync();  // vec / vs reuse; xs, bj staged
@@ -404,6 +414,7 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
       if (J > 0) {     // the hand-off: y_J = X_J v - M_J y_{J-1}
         SSTAMP(J, 2);
         if (!stage(ybuf, J - 1, 1, 1)) return;
+        SSTAMP(J, 4);
         T d[RP_ROWS] = {T(0), T(0), T(0), T(0)};
         dot_rows(d, tb, vs[0]);
 #pragma unroll
@@ -430,12 +441,7 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
       T acc[4] = {T(0), T(0), T(0), T(0)};  // columns 2 ccg + 64 j + e
       Tile ta, tb;
       // X_J^T and z_J = y_J / D_J -> LDS up front (y_J from the forward
-      // launch: complete); Q_J is loaded when the bulk is done
-      if (!last) {  // Q_J through LDS once: warms this XCD's L2 for the reload after the bulk
-        load_rows(ta, Q + (int64_t)J * SB * SB);
-        put_xs(ta);
-        lds_sync();
-      }
+      // launch: complete)
       load_rows(ta, XT + (int64_t)J * SB * SB);
       if (tid < SB) bj[tid] = tid < R ? ybuf[J0 + tid] / D[J0 + tid] : T(0);
       if (tid < R) st_sc1(&ybuf[J0 + tid], sentinel<T>());  // only this block reads y_J: reset for the next solve
@@ -467,19 +473,35 @@ __global__ __launch_bounds__(SNT) void trsv128_kernel(const T* __restrict__ K, i
 #pragma unroll
           for (int i = 0; i < 4; ++i) acc[i] = fma(t[4 * k + i], xv[k], acc[i]);
       };
-      // bulk: K > J+1 from the bottom, in pairs as their vectors complete
-      const int Klo = J + 2;
-      if (nb - 1 >= Klo) load_tile(ta, nb - 1);
-      if (nb - 2 >= Klo) load_tile(tb, nb - 2);
+      // bulk: K > J+1 from the bottom.  Tiles K > J+2 in pairs as their
+      // vectors complete; the last one, block J+2, alone, so that Q_J is
+      // loaded into the other register tile as soon as x_{J+3} has been
+      // consumed (the forward sweep's M_J schedule, mirrored)
+      const int Klo = J + 3;  // pairs region [Klo, nb)
+      const T* Qj = Q + (int64_t)J * SB * SB;
+      if (nb - 1 >= Klo) {
+        load_tile(ta, nb - 1);
+        if (nb - 2 >= Klo) load_tile(tb, nb - 2);
+        else load_rows(tb, Qj);
+      } else if (!last) {
+        if (J + 2 <= nb - 1) load_tile(ta, J + 2);
+        load_rows(tb, Qj);
+      }
       for (int Kc = nb - 1; Kc >= Klo; Kc -= 2) {
         const bool two = Kc - 1 >= Klo;
         if (!stage(xbuf, Kc, two ? 2 : 1, -1)) return;
         dot_cols(ta, vs[0]);
         if (two) dot_cols(tb, vs[1]);
-        if (Kc - 2 >= Klo) load_tile(ta, Kc - 2);
-        if (Kc - 3 >= Klo) load_tile(tb, Kc - 3);
+        load_tile(ta, Kc - 2 >= Klo ? Kc - 2 : J + 2);
+        if (two) {  // tb consumed: the next pair's second tile, or Q_J
+          if (Kc - 3 >= Klo) load_tile(tb, Kc - 3);
+          else load_rows(tb, Qj);
+        }
       }
-      if (!last) load_rows(tb, Q + (int64_t)J * SB * SB);
+      if (J + 2 <= nb - 1) {  // L_{J+2,J}^T x_{J+2}
+        if (!stage(xbuf, J + 2, 1, 1)) return;
+        dot_cols(ta, vs[0]);
+      }
       lds_sync();
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -532,7 +554,7 @@ static hipError_t solve_prep_t(const T* K, int64_t ld, int N, const T* Linv, T* 
   return hipGetLastError();
 }
 hipError_t solve_stamps(unsigned long long* out) {  // DEBUG
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamp), sizeof(unsigned long long) * 2 * 256 * 4);
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sstamp), sizeof(unsigned long long) * 2 * 256 * 6);
 }
 hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, double* P, hipStream_t st) {
   return solve_prep_t<double>(K, ld, N, Linv, P, st);

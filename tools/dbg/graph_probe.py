@@ -8,8 +8,6 @@ sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
 import numpy as np
 import torch
 import ipmz_amd as I
-import faulthandler
-faulthandler.enable()
 segv = ctypes.CDLL(os.path.join(REPO, "tools", "dbg", "libsegv.so"))
 torch.cuda.set_device(0)
 torch.zeros(1, device="cuda")

@@ -75,6 +75,53 @@ int main(int argc, char** argv) {
   CK(hipMemset(pctrl, 0, ipmz::panel_ctrl_words(N, 64) * 4));
   Timer t;
   hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+  if (mode == "capture") {  // kbench N capture NBO DBG: the product factor's fork/join under hipStreamBeginCapture
+    const int nbo = argc > 3 ? std::atoi(argv[3]) : 256;
+    const int dbg = argc > 4 ? std::atoi(argv[4]) : 0;
+    ipmz::set_debug_inject_mask(dbg);
+    const int npan = (N + nbo - 1) / nbo, nev = 4 * npan + 4;
+    std::vector<hipEvent_t> ev(nev);
+    for (auto& evi : ev) CK(hipEventCreateWithFlags(&evi, hipEventDisableTiming));
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    hipStream_t orig, sA, sB, sC;
+    CK(hipStreamCreateWithFlags(&orig, hipStreamNonBlocking));
+    CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+    CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+    CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
+    CK(hipStreamSynchronize(st));
+    auto enqueue = [&]() {  // capi.cpp factor_impl's sequence
+      CK(hipMemsetAsync(info, 0x7f, 4, orig));
+      CK(hipMemsetAsync(pctrl, 0, ipmz::panel_ctrl_words(N, nbo) * 4, orig));
+      CK(hipEventRecord(ev[nev - 2], orig));
+      CK(hipStreamWaitEvent(sA, ev[nev - 2], 0));
+      CK(hipStreamWaitEvent(sB, ev[nev - 2], 0));
+      CK(hipStreamWaitEvent(sC, ev[nev - 2], 0));
+      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, 64, info, sA, nullptr, sB, sC, ev.data(), nev - 2, pctrl));
+      CK(hipEventRecord(ev[nev - 1], sA));
+      CK(hipStreamWaitEvent(orig, ev[nev - 1], 0));
+    };
+    enqueue();
+    CK(hipStreamSynchronize(orig));
+    std::printf("eager factor done (N=%d nbo=%d npan=%d)\n", N, nbo, npan);
+    CK(hipStreamBeginCapture(orig, hipStreamCaptureModeThreadLocal));
+    enqueue();
+    std::printf("enqueued, ending capture\n");
+    hipGraph_t g = nullptr;
+    CK(hipStreamEndCapture(orig, &g));
+    size_t nn = 0;
+    CK(hipGraphGetNodes(g, nullptr, &nn));
+    std::printf("captured: %zu nodes\n", nn);
+    hipGraphExec_t ge;
+    CK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, orig, K, ld, N, 7ull);
+    CK(hipGraphLaunch(ge, orig));
+    CK(hipStreamSynchronize(orig));
+    unsigned hc[IPMZ_PANEL_CTRL_WORDS];
+    CK(hipMemcpy(hc, pctrl, sizeof(hc), hipMemcpyDeviceToHost));
+    std::printf("replayed ok%s\n", hc[ipmz::PANEL_ERR_WORD] ? " PANEL ERROR" : "");
+    return 0;
+  }
   if (mode == "probe") {  // f64 MFMA throughput vs independent chains, 1 WG per CU
     for (int threads : {256, 512})
       for (int nacc : {1, 4, 8, 16}) {
@@ -249,13 +296,13 @@ int main(int argc, char** argv) {
   for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve_persistent(K, ld, N, D, P, b, yb, xb, ctrl, st));
   const float sms = t.stop(st) / 5;
   {
-    static unsigned long long stp[2][256][4];
+    static unsigned long long stp[2][256][6];
     CK(ipmz::solve_stamps(&stp[0][0][0]));
     const double t0 = (double)stp[0][0][0];
-    std::printf("fwd block: start bulkdone critin stored (us from block 0 start)\n");
+    std::printf("fwd block: start bulkdone critin seen stored (us from block 0 start)\n");
     for (int j = 0; j < (N + 127) / 128 && j < 256; ++j)
-      std::printf("%3d %8.2f %8.2f %8.2f %8.2f\n", j, (stp[0][j][0] - t0) / 100.0, (stp[0][j][1] - t0) / 100.0,
-                  (stp[0][j][2] - t0) / 100.0, (stp[0][j][3] - t0) / 100.0);
+      std::printf("%3d %8.2f %8.2f %8.2f %8.2f %8.2f\n", j, (stp[0][j][0] - t0) / 100.0, (stp[0][j][1] - t0) / 100.0,
+                  (stp[0][j][2] - t0) / 100.0, (stp[0][j][4] - t0) / 100.0, (stp[0][j][3] - t0) / 100.0);
   }
   unsigned hctrl[8];
   CK(hipMemcpy(hctrl, ctrl, sizeof(hctrl), hipMemcpyDeviceToHost));
