@@ -76,6 +76,20 @@ static int ensure_events(ipmz_ctx* ctx, size_t n) {
   return IPMZ_OK;
 }
 
+// the end of a factorization that forked onto the look-ahead streams: the
+// caller's stream waits for each of them (the chain stream A has already
+// waited for B's and C's work; the explicit waits keep every stream a capture
+// forked joined back into its origin -- ldlt.hip stream_wait)
+static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev3) {
+  hipStream_t side[3] = {ctx->sA, ctx->sB, ctx->sC};
+  for (int i = 0; i < 3; ++i) {
+    hipError_t e = stream_record(ev3[i], side[i]);
+    if (e == hipSuccess) e = stream_wait(ctx->stream, ev3[i]);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
+}
+
 static int check_device(int device) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -323,21 +337,20 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
     return IPMZ_OK;
   }
   const int nev = 4 * npan + 4;
-  int rc = ensure_events(ctx, (size_t)nev);
+  int rc = ensure_events(ctx, (size_t)nev + 3);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
   // fork: A, C (panel path) and B (trailing updates) start after the caller's stream
   IPMZ_TRACE("factor_impl: fork");
-  HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
-  HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
-  HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(hipStreamWaitEvent(ctx->sC, ev[nev - 2], 0));
+  HIP_OK(stream_record(ev[nev - 2], ctx->stream));
+  HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
+  HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
+  HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
   HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
                      pctrl));
   // join (A has already waited for B's tail)
   IPMZ_TRACE("factor_impl: join");
-  HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
-  HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  HIP_OK(join_side_streams(ctx, ev + nev));
   IPMZ_TRACE("factor_impl: joined");
   HIP_OK(prep());
   return IPMZ_OK;
@@ -408,16 +421,15 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
     return IPMZ_OK;
   }
   const int nev = 4 * npan + 4;
-  int rc = ensure_events(ctx, (size_t)nev);
+  int rc = ensure_events(ctx, (size_t)nev + 3);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
-  HIP_OK(hipEventRecord(ev[nev - 2], ctx->stream));
-  HIP_OK(hipStreamWaitEvent(ctx->sA, ev[nev - 2], 0));
-  HIP_OK(hipStreamWaitEvent(ctx->sB, ev[nev - 2], 0));
-  HIP_OK(hipStreamWaitEvent(ctx->sC, ev[nev - 2], 0));
+  HIP_OK(stream_record(ev[nev - 2], ctx->stream));
+  HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
+  HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
+  HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
   HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer));
-  HIP_OK(hipEventRecord(ev[nev - 1], ctx->sA));
-  HIP_OK(hipStreamWaitEvent(ctx->stream, ev[nev - 1], 0));
+  HIP_OK(join_side_streams(ctx, ev + nev));
   HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
   return IPMZ_OK;
 }
@@ -1225,10 +1237,14 @@ int load_one(ipmz_qp* s, int i, const double* Q, const double* c, const double* 
 }
 
 // Does the step's factorization fork onto the look-ahead streams?  Such a
-// step is enqueued eagerly even when IPMZ_STEP_GRAPH is asked for: capturing
-// the two-stream fork/join crashes inside hipGraph on ROCm 7.2 (segfault at
-// the first capture, N >= 3 outer panels), and a multi-millisecond step hides
-// its launch latency anyway.
+// step is enqueued eagerly even when IPMZ_STEP_GRAPH is asked for: its graph
+// replay is slower than the eager launches (tools/graph_ab.py, profiles/r03_s3:
+// C2 2.4-3.0 vs 1.75 ms, C3 16.7 vs 14.6, C5 35.3 vs 25.7 ms per step -- the
+// replayed look-ahead loses its stream priorities and overlap), and a
+// multi-millisecond step hides its launch latency anyway.  The capture itself
+// is correct (debug bit IPMZ_INJECT_GRAPH_FORKS; tests/test_gpu_graph.py:
+// bitwise the eager step): it once crashed inside hipStreamEndCapture of the
+// HIP runtime torch bundles, fixed by ldlt.hip's stream_record / stream_wait.
 bool step_forks(const ipmz_qp* s) {
   if (s->eqnone || s->B > 1) return false;
   if (debug_inject_mask() & IPMZ_INJECT_GRAPH_FORKS) return false;
@@ -1269,6 +1285,7 @@ int step_impl(ipmz_qp* s, int flags) {
     // is then launched on the caller's stream
     hipStream_t cap = s->ctx->own;
     IPMZ_TRACE("capture: begin");
+    set_capture_origin(cap);  // ldlt.hip stream_wait: the look-ahead streams' ordering inside the capture
     HIP_OK(hipStreamBeginCapture(cap, hipStreamCaptureModeThreadLocal));
     s->ctx->stream = cap;
     int rc = run_step(s, flags);
@@ -1276,6 +1293,7 @@ int step_impl(ipmz_qp* s, int flags) {
     IPMZ_TRACE("capture: step enqueued rc=%d", rc);
     hipGraph_t g = nullptr;
     hipError_t e = hipStreamEndCapture(cap, &g);
+    set_capture_origin(nullptr);
     IPMZ_TRACE("capture: ended %d", (int)e);
     if (rc) {
       if (g) hipGraphDestroy(g);

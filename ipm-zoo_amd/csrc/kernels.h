@@ -16,7 +16,8 @@ namespace ipmz {
 // hand-off, so every consumer times out and raises the sticky error word.
 // IPMZ_INJECT_GRAPH_FORKS: not a fault -- IPMZ_STEP_GRAPH captures steps whose
 // factor forks onto the look-ahead streams too (the capture experiment of
-// tests/test_gpu_graph.py) instead of enqueuing them eagerly.
+// tests/test_gpu_graph.py, bitwise the eager step) instead of enqueuing them
+// eagerly (the production choice: graph replay of a forked step is slower).
 // DEBUG bits (determinism experiments): 16 = the mixed factor stops after
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
 // 64 = trace the host calls of a step to stderr (the capture experiment)
@@ -31,6 +32,11 @@ enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4
     }                                                                    \
   } while (0)
 int debug_inject_mask();
+// cross-stream ordering that a capture on the HIP runtime torch bundles can
+// end (ldlt.hip): event records / waits of the factor's look-ahead streams
+hipError_t stream_record(hipEvent_t e, hipStream_t s);
+hipError_t stream_wait(hipStream_t s, hipEvent_t e);
+void set_capture_origin(hipStream_t s);  // the stream a capture began on (nullptr: none)
 void set_debug_inject_mask(int mask);
 // error words the persistent kernels raise on a spin timeout (sync.h): the
 // panel kernel's ctrl[PANEL_ERR_WORD], the solve's ctrl[1]

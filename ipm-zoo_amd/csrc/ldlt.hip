@@ -20,6 +20,8 @@
 // changes rounding at the 1e-16 level (parity tolerance: tests/).
 #include <cstdlib>
 #include <cstring>
+#include <unordered_map>
+#include <vector>
 
 #include "common.h"
 #include "diag64.h"
@@ -32,6 +34,65 @@ static int g_inject = 0;
 
 int debug_inject_mask() { return g_inject; }
 void set_debug_inject_mask(int mask) { g_inject = mask; }
+
+// ---------------------------------------------------------------------------
+// Capture-safe cross-stream ordering.  The HIP runtime torch bundles
+// (7.0.51831; libipmz shares it when loaded after torch) recurses without end
+// inside hipStreamEndCapture once two side streams of a capture have waited on
+// each other's events -- the look-ahead's chain / rows / trailing streams do
+// that every panel (tools/dbg/graph_mini.cpp patterns 2 and 5 crash; 0, 1, 3,
+// 6, 7 do not; /opt/rocm's 7.2 captures all of them).  So while a stream is
+// capturing, stream_record notes the nodes an event stands for, and
+// stream_wait between side streams adds those nodes to the waiter's capture
+// dependencies (hipStreamUpdateCaptureDependencies) instead of waiting on the
+// event: the same graph edges, no stream-to-stream wait.  A stream joining the
+// capture (its first wait) and the capture's origin stream (set_capture_origin)
+// wait on the event as usual.  Outside a capture both are the plain calls.
+namespace {
+struct Noted {
+  unsigned long long id;
+  std::vector<hipGraphNode_t> nodes;
+};
+thread_local std::unordered_map<hipEvent_t, Noted> t_noted;
+thread_local hipStream_t t_origin = nullptr;
+}  // namespace
+void set_capture_origin(hipStream_t s) {
+  t_origin = s;
+  t_noted.clear();
+}
+hipError_t stream_record(hipEvent_t e, hipStream_t s) {
+  hipError_t r = hipEventRecord(e, s);
+  if (r != hipSuccess) return r;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if ((r = hipStreamIsCapturing(s, &cs)) != hipSuccess) return r;
+  if (cs != hipStreamCaptureStatusActive) {
+    t_noted.erase(e);
+    return hipSuccess;
+  }
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t n = 0;
+  if ((r = hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &n)) != hipSuccess) return r;
+  t_noted[e] = Noted{id, std::vector<hipGraphNode_t>(deps, deps + n)};
+  return hipSuccess;
+}
+hipError_t stream_wait(hipStream_t s, hipEvent_t e) {
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipError_t r = hipStreamIsCapturing(s, &cs);
+  if (r != hipSuccess) return r;
+  auto it = t_noted.find(e);
+  if (cs != hipStreamCaptureStatusActive || s == t_origin || it == t_noted.end()) return hipStreamWaitEvent(s, e, 0);
+  unsigned long long id = 0;
+  hipGraph_t g = nullptr;
+  const hipGraphNode_t* deps = nullptr;
+  size_t n = 0;
+  if ((r = hipStreamGetCaptureInfo_v2(s, &cs, &id, &g, &deps, &n)) != hipSuccess) return r;
+  if (id != it->second.id) return hipStreamWaitEvent(s, e, 0);
+  if (it->second.nodes.empty()) return hipSuccess;
+  return hipStreamUpdateCaptureDependencies(s, it->second.nodes.data(), it->second.nodes.size(),
+                                            hipStreamAddCaptureDependencies);
+}
 
 // ---------------------------------------------------------------------------
 // Diagonal block (NB x NB, NB in {64, 128}) in REGISTERS.
@@ -434,14 +495,14 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // fp32 conversion, the ctrl-word memsets) comes first on B and C as well
   hipEvent_t evEntry = ev[4 * npan + 1];
   IPMZ_TRACE("factor: N=%d npan=%d look-ahead", N, npan);
-  if ((e = hipEventRecord(evEntry, st)) != hipSuccess) return e;
-  if ((e = hipStreamWaitEvent(st2, evEntry, 0)) != hipSuccess) return e;
-  if (fused && (e = hipStreamWaitEvent(sC, evEntry, 0)) != hipSuccess) return e;
+  if ((e = stream_record(evEntry, st)) != hipSuccess) return e;
+  if ((e = stream_wait(st2, evEntry)) != hipSuccess) return e;
+  if (fused && (e = stream_wait(sC, evEntry)) != hipSuccess) return e;
   if ((e = factor(0, false)) != hipSuccess) return e;
   if (fused) {
-    if ((e = hipEventRecord(evA[0], st)) != hipSuccess) return e;
-    if ((e = hipEventRecord(evC[0], sC)) != hipSuccess) return e;
-    if ((e = hipStreamWaitEvent(st, evC[0], 0)) != hipSuccess) return e;
+    if ((e = stream_record(evA[0], st)) != hipSuccess) return e;
+    if ((e = stream_record(evC[0], sC)) != hipSuccess) return e;
+    if ((e = stream_wait(st, evC[0])) != hipSuccess) return e;
   }
   for (int k = 0; k < npan; ++k) {
     const int k0 = k * nbo, bo = pw(k);
@@ -450,13 +511,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     const int p3 = p2 < N ? p2 + pw(k + 2) : N;      // start of P_{k+3}
     if (p1 >= N) break;
     IPMZ_TRACE("factor: panel %d", k);
-    if ((e = hipEventRecord(evP[k], st)) != hipSuccess) return e;
+    if ((e = stream_record(evP[k], st)) != hipSuccess) return e;
     // ---- stream B: P_{k+2} columns first, then the rest
-    if ((e = hipStreamWaitEvent(st2, evP[k], 0)) != hipSuccess) return e;
+    if ((e = stream_wait(st2, evP[k])) != hipSuccess) return e;
     if (p2 < N) {
       if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p2, p3, false, st2)) != hipSuccess) return e;
     }
-    if ((e = hipEventRecord(evN[k], st2)) != hipSuccess) return e;
+    if ((e = stream_record(evN[k], st2)) != hipSuccess) return e;
     if (p3 < N) {
       hipEvent_t* te = timer && N - p3 > IPMZ_TRAIL_SMALL_M ? timer->next() : nullptr;
       if (te) hipEventRecord(te[0], st2);
@@ -467,31 +528,31 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
     // ---- streams A (and C): update P_{k+1} with P_k, factor P_{k+1}
     if (k >= 1) {
-      if ((e = hipStreamWaitEvent(st, evN[k - 1], 0)) != hipSuccess) return e;
-      if (fused && (e = hipStreamWaitEvent(sC, evN[k - 1], 0)) != hipSuccess) return e;
+      if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
+      if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
     }
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
       // region as a strip GEMM on C (beside the chain launch, which updates
       // the region itself); panel k's chain roles may have run in its chain
       // launch, so C also waits for that launch
-      if ((e = hipStreamWaitEvent(sC, evA[k], 0)) != hipSuccess) return e;
+      if ((e = stream_wait(sC, evA[k])) != hipSuccess) return e;
       if (p2 < N) {
         if ((e = gemm_nt_sub_t<T>(N - p2, p2 - p1, bo, Wb(k) + (int64_t)p2 * nbo, nbo, K + (int64_t)p1 * ld + k0, ld,
                                   K + (int64_t)p2 * ld + p1, ld, p2, p1, false, sC, nullptr)) != hipSuccess)
           return e;
       }
       if ((e = factor(k + 1, true)) != hipSuccess) return e;
-      if ((e = hipEventRecord(evA[k + 1], st)) != hipSuccess) return e;
-      if ((e = hipEventRecord(evC[k + 1], sC)) != hipSuccess) return e;
-      if ((e = hipStreamWaitEvent(st, evC[k + 1], 0)) != hipSuccess) return e;
+      if ((e = stream_record(evA[k + 1], st)) != hipSuccess) return e;
+      if ((e = stream_record(evC[k + 1], sC)) != hipSuccess) return e;
+      if ((e = stream_wait(st, evC[k + 1])) != hipSuccess) return e;
     } else {
       if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
       if ((e = factor(k + 1, false)) != hipSuccess) return e;
     }
   }
-  if ((e = hipEventRecord(evJoin, st2)) != hipSuccess) return e;
-  return hipStreamWaitEvent(st, evJoin, 0);
+  if ((e = stream_record(evJoin, st2)) != hipSuccess) return e;
+  return stream_wait(st, evJoin);
 }
 
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,

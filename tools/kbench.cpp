@@ -54,6 +54,7 @@ int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IONBF, 0);
   const int N = argc > 1 ? std::atoi(argv[1]) : 11264;
   const std::string mode = argc > 2 ? argv[2] : "factor";
+  if (const char* dbg = std::getenv("KB_DEBUG")) ipmz::set_debug_inject_mask(std::atoi(dbg));  // tool only (A/B bits)
   hipStream_t st;
   CK(hipStreamCreate(&st));
   const int64_t ld = (N + 63) / 64 * 64;
