@@ -20,9 +20,10 @@ namespace ipmz {
 // eagerly (the production choice: graph replay of a forked step is slower).
 // DEBUG bits (determinism experiments): 16 = the mixed factor stops after
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
-// 64 = trace the host calls of a step to stderr (the capture experiment)
+// 64 = trace the host calls of a step to stderr (the capture experiment),
+// 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
-       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64 };
+       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -70,6 +71,8 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 // trailing updates of order <= this run on 64 x 64 tiles, larger ones on the
 // 128 x 128 kernel (the one TrailTimer times: the roofline kernel of bench.py)
 #define IPMZ_TRAIL_SMALL_M 3072
+// fp32 trailing updates of at least this order run on rocBLAS SYRKX (ldlt.hip)
+#define IPMZ_BLAS_MIN_R 4096
 struct TrailTimer {  // HIP-event pairs around every dominant trailing-update launch
   hipEvent_t (*pairs)[2] = nullptr;
   int cap = 0, used = 0;

@@ -18,8 +18,12 @@
 // fits one block factors bit-identically to the reference.  Across blocks the
 // MFMA accumulates a block's contributions before subtracting them, which
 // changes rounding at the 1e-16 level (parity tolerance: tests/).
+#include <rocblas/rocblas.h>
+
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <unordered_map>
 #include <vector>
 
@@ -279,6 +283,46 @@ static void launch_diag64(int B, hipStream_t st, float* K, int64_t ld, int j0, i
   hipLaunchKernelGGL((ldlt_diag_kernel<float, 64>), dim3(B), dim3(256), 0, st, K, ld, j0, bi, D, Lb, info, sK, sD, sL);
 }
 
+// ---------------------------------------------------------------------------
+// The fp32 trailing update (mixed-precision factor, C5) through rocBLAS
+// SYRKX: measured 112.5 vs 88.9 TFLOP/s for gemm_nt_kernel<float> at R =
+// 15872, rank 512 (profiles/r03_s3/gemmref32.log); C5 38.7 -> 41.6 steps/s,
+// factor 21.5 -> 19.9 ms (profiles/r03_s3/blas_ab.log) -- a plain library
+// BLAS-3 call on the same operands.  (The fp32 look-ahead strips through
+// SGEMM / SYRKX as well: no further gain, 41.3 steps/s.)  One handle per (device, stream),
+// made on first use (never inside a graph capture: the hand-written kernel
+// runs there).
+static rocblas_handle blas_for(hipStream_t st) {
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, rocblas_handle> handles;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = handles.find({dev, st});
+  if (it != handles.end()) return it->second;
+  rocblas_handle h = nullptr;
+  if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
+  if (rocblas_set_stream(h, st) != rocblas_status_success) {
+    rocblas_destroy_handle(h);
+    return nullptr;
+  }
+  handles[{dev, st}] = h;
+  return h;
+}
+// row-major C (lower, R x R, ldc) -= W (R x k, ldw) L^T (L: R x k, ldl) as the
+// column-major upper triangle: C' -= L'^T W' with L' = L^T (k x R, ldl), W' = W^T
+static bool blas_trailing(int R, int k, const float* W, int64_t ldw, const float* L, int64_t ldl, float* C,
+                          int64_t ldc, hipStream_t st) {
+  if (R < IPMZ_BLAS_MIN_R || (debug_inject_mask() & IPMZ_DEBUG_NO_BLAS)) return false;
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
+  rocblas_handle h = blas_for(st);
+  if (!h) return false;
+  const float alpha = -1.f, beta = 1.f;
+  return rocblas_ssyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, k, &alpha, L, (rocblas_int)ldl, W,
+                        (rocblas_int)ldw, &beta, C, (rocblas_int)ldc) == rocblas_status_success;
+}
+
 // C[i][j] -= sum_k A[i][k] B[j][k] over the lower part of a trailing region.
 template <typename T>
 static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, const T* B, int64_t ldb, T* C,
@@ -319,6 +363,8 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // gvar, R = 10880, rank 384), 40.8 vs 38.9 in situ, C3 60.6 -> 61.8
   // steps/s; the fp32 factor (C5) keeps 2 x 4 (71 vs 67 TFLOP/s in situ)
   if (square_lower) {
+    if constexpr (std::is_same<T, float>::value)
+      if (batch == 1 && M == N && blas_trailing(M, Kd, A, lda, B, ldb, C, ldc, st)) return hipSuccess;
     if (M <= IPMZ_TRAIL_SMALL_M) return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch);
     if constexpr (std::is_same<T, double>::value)
       return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);

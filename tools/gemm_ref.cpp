@@ -16,12 +16,60 @@
     }                                                                      \
   } while (0)
 
+// fp32 (the mixed-precision factor's trailing update): rocblas_sgemm on the
+// full square and rocblas_ssyrkx on the lower triangle (R^2 k flops counted)
+static void fp32(rocblas_handle h, hipStream_t st) {
+  for (int R : {8192, 15872}) {
+    const int nbo = 512;
+    const int64_t ld = (R + 63) / 64 * 64;
+    float *C, *W, *L;
+    CK(hipMalloc(&C, ld * R * 4));
+    CK(hipMalloc(&W, (int64_t)R * nbo * 4));
+    CK(hipMalloc(&L, (int64_t)R * nbo * 4));
+    CK(hipMemset(C, 0, ld * R * 4));
+    CK(hipMemset(W, 0, (int64_t)R * nbo * 4));
+    CK(hipMemset(L, 0, (int64_t)R * nbo * 4));
+    const float alpha = -1.f, beta = 1.f;
+    for (int which = 0; which < 2; ++which) {
+      auto run = [&]() {
+        if (which == 0)
+          CK(rocblas_sgemm(h, rocblas_operation_transpose, rocblas_operation_none, R, R, nbo, &alpha, L, nbo, W, nbo,
+                           &beta, C, ld));
+        else  // col-major upper of C' = lower of row-major C: C' -= L'^T W' (op T)
+          CK(rocblas_ssyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, nbo, &alpha, L, nbo, W, nbo, &beta,
+                            C, ld));
+      };
+      run();
+      hipEvent_t a, b;
+      CK(hipEventCreate(&a));
+      CK(hipEventCreate(&b));
+      CK(hipEventRecord(a, st));
+      for (int r = 0; r < 5; ++r) run();
+      CK(hipEventRecord(b, st));
+      CK(hipEventSynchronize(b));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a, b));
+      ms /= 5;
+      const double fl = which == 0 ? 2.0 * R * R * nbo : (double)R * (R + 1) * nbo;
+      std::printf("%s R=%d k=%d: %.3f ms %.2f TFLOP/s (%s)\n", which == 0 ? "rocblas_sgemm " : "rocblas_ssyrkx", R, nbo,
+                  ms, fl / ms / 1e9, which == 0 ? "full 2R^2k" : "lower R(R+1)k");
+    }
+    CK(hipFree(C));
+    CK(hipFree(W));
+    CK(hipFree(L));
+  }
+}
+
 int main(int argc, char** argv) {
   rocblas_handle h;
   CK(rocblas_create_handle(&h));
   hipStream_t st;
   CK(hipStreamCreate(&st));
   CK(rocblas_set_stream(h, st));
+  if (argc > 1 && argv[1][0] == 's') {
+    fp32(h, st);
+    return 0;
+  }
   for (int nbo : {256, 512}) {
     for (int R : {2048, 5632, 11008}) {
       const int64_t ld = (R + 63) / 64 * 64;
