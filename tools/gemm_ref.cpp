@@ -60,6 +60,42 @@ static void fp32(rocblas_handle h, hipStream_t st) {
   }
 }
 
+// fp64 SYRKX on the C3 trailing shapes (R(R+1)k flops counted)
+static void fp64syrkx(rocblas_handle h, hipStream_t st) {
+  for (int R : {5632, 10752}) {
+    const int nbo = 512;
+    const int64_t ld = (R + 63) / 64 * 64;
+    double *C, *W, *L;
+    CK(hipMalloc(&C, ld * R * 8));
+    CK(hipMalloc(&W, (int64_t)R * nbo * 8));
+    CK(hipMalloc(&L, (int64_t)R * nbo * 8));
+    CK(hipMemset(C, 0, ld * R * 8));
+    CK(hipMemset(W, 0, (int64_t)R * nbo * 8));
+    CK(hipMemset(L, 0, (int64_t)R * nbo * 8));
+    const double alpha = -1.0, beta = 1.0;
+    auto run = [&]() {
+      CK(rocblas_dsyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, nbo, &alpha, L, nbo, W, nbo, &beta, C,
+                        ld));
+    };
+    run();
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a, st));
+    for (int r = 0; r < 5; ++r) run();
+    CK(hipEventRecord(b, st));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    ms /= 5;
+    std::printf("rocblas_dsyrkx R=%d k=%d: %.3f ms %.2f TFLOP/s (lower R(R+1)k)\n", R, nbo, ms,
+                (double)R * (R + 1) * nbo / ms / 1e9);
+    CK(hipFree(C));
+    CK(hipFree(W));
+    CK(hipFree(L));
+  }
+}
+
 int main(int argc, char** argv) {
   rocblas_handle h;
   CK(rocblas_create_handle(&h));
@@ -68,6 +104,10 @@ int main(int argc, char** argv) {
   CK(rocblas_set_stream(h, st));
   if (argc > 1 && argv[1][0] == 's') {
     fp32(h, st);
+    return 0;
+  }
+  if (argc > 1 && argv[1][0] == 'x') {
+    fp64syrkx(h, st);
     return 0;
   }
   for (int nbo : {256, 512}) {
