@@ -46,7 +46,7 @@ struct ipmz_ctx {
   int nbo = 0, nbi = 64;  // nbo 0: by matrix order (nbo_for)
   // factorization look-ahead: panel chain on sA and panel rows on sC (high
   // priority), trailing updates on sB; forked from / joined to `stream`
-  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr;
+  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
   std::vector<hipEvent_t> evpool;
   // the sticky error words (spin timeouts of the persistent kernels) of the
   // workspace the last asynchronous device-memory solve used, resolved when
@@ -80,9 +80,10 @@ static int ensure_events(ipmz_ctx* ctx, size_t n) {
 // caller's stream waits for each of them (the chain stream A has already
 // waited for B's and C's work; the explicit waits keep every stream a capture
 // forked joined back into its origin -- ldlt.hip stream_wait)
-static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev3) {
-  hipStream_t side[3] = {ctx->sA, ctx->sB, ctx->sC};
-  for (int i = 0; i < 3; ++i) {
+static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev4) {
+  hipStream_t side[4] = {ctx->sA, ctx->sB, ctx->sC, ctx->sD};
+  hipEvent_t* ev3 = ev4;
+  for (int i = 0; i < 4; ++i) {
     hipError_t e = stream_record(ev3[i], side[i]);
     if (e == hipSuccess) e = stream_wait(ctx->stream, ev3[i]);
     if (e != hipSuccess) return e;
@@ -123,7 +124,8 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
   hipDeviceGetStreamPriorityRange(&least, &greatest);
   if (hipStreamCreateWithPriority(&c->sA, hipStreamNonBlocking, greatest) != hipSuccess ||
       hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->sC, hipStreamNonBlocking, greatest) != hipSuccess) {
+      hipStreamCreateWithPriority(&c->sC, hipStreamNonBlocking, greatest) != hipSuccess ||
+      hipStreamCreateWithPriority(&c->sD, hipStreamNonBlocking, greatest) != hipSuccess) {
     ipmz_ctx_destroy(c);
     return fail(IPMZ_ERR_HIP, "hipStreamCreateWithPriority failed");
   }
@@ -135,7 +137,7 @@ int ipmz_ctx_destroy(ipmz_ctx* ctx) {
   if (!ctx) return IPMZ_OK;
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB, ctx->sC})
+  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB, ctx->sC, ctx->sD})
     if (s) {
       hipStreamSynchronize(s);
       hipStreamDestroy(s);
@@ -336,8 +338,8 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
     HIP_OK(prep());
     return IPMZ_OK;
   }
-  const int nev = 4 * npan + 4;
-  int rc = ensure_events(ctx, (size_t)nev + 3);
+  const int nev = 5 * npan + 5;  // ldlt_factor's 5 npan + 3, the fork, one spare
+  int rc = ensure_events(ctx, (size_t)nev + 4);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
   // fork: A, C (panel path) and B (trailing updates) start after the caller's stream
@@ -346,8 +348,9 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
+  HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
   HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
-                     pctrl));
+                     pctrl, ctx->sD));
   // join (A has already waited for B's tail)
   IPMZ_TRACE("factor_impl: join");
   HIP_OK(join_side_streams(ctx, ev + nev));
@@ -420,15 +423,16 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
     HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
     return IPMZ_OK;
   }
-  const int nev = 4 * npan + 4;
-  int rc = ensure_events(ctx, (size_t)nev + 3);
+  const int nev = 5 * npan + 5;  // ldlt_factor's 5 npan + 3, the fork, one spare
+  int rc = ensure_events(ctx, (size_t)nev + 4);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
   HIP_OK(stream_record(ev[nev - 2], ctx->stream));
   HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
-  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer));
+  HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
+  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer, ctx->sD));
   HIP_OK(join_side_streams(ctx, ev + nev));
   HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
   return IPMZ_OK;

@@ -21,9 +21,11 @@ namespace ipmz {
 // DEBUG bits (determinism experiments): 16 = the mixed factor stops after
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
 // 64 = trace the host calls of a step to stderr (the capture experiment),
-// 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B)
+// 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B),
+// 256 = the look-ahead strip on the trailing stream before the trailing update (no fourth stream)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
-       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128 };
+       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128,
+       IPMZ_DEBUG_NO_FOURTH = 256 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -86,12 +88,12 @@ struct TrailTimer {  // HIP-event pairs around every dominant trailing-update la
 // strip kernel chain.
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                        int* info, hipStream_t st, TrailTimer* timer = nullptr, hipStream_t st2 = nullptr,
-                       hipStream_t st3 = nullptr, hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr);
+                       hipStream_t st3 = nullptr, hipEvent_t* ev = nullptr, int nev = 0, unsigned* pctrl = nullptr, hipStream_t st4 = nullptr);
 // the same blocked LDL^T in fp32 (fp32 MFMA trailing update): the factor of
 // the mixed-precision solve (C5)
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
                        hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
-                       unsigned* pctrl = nullptr);
+                       unsigned* pctrl = nullptr, hipStream_t st4 = nullptr);
 // ctrl words of the panel path: a shared area (sticky error word) + one
 // area per outer panel, then two 64 x 64 (8-byte) tiles: the next panel's
 // block (0, 0) look-ahead update, pre-accumulated by the rows launch
@@ -168,7 +170,7 @@ int64_t mixed_ws_bytes(int N, int nbo);
 int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w);  // base == nullptr: size only
 // scale + convert + fp32 factor of the lower triangle of K (fp64, row-major)
 hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipStream_t st3,
-                        hipEvent_t* ev, int nev, TrailTimer* timer = nullptr);
+                        hipEvent_t* ev, int nev, TrailTimer* timer = nullptr, hipStream_t st4 = nullptr);
 // b <- K^{-1} b by iterative refinement (device-side stop test)
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,
                        hipStream_t st);

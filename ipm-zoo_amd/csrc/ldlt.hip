@@ -491,13 +491,17 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 template <typename T>
 static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, int nbo, int nbi, int* info,
                                 hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev,
-                                int nev, unsigned* pctrl) {
+                                int nev, unsigned* pctrl, hipStream_t st4) {
   if (N <= 0) return hipSuccess;
   if (nbi != 64 && nbi != 128) return hipErrorInvalidValue;
   if (nbo % nbi != 0 || nbo > IPMZ_NBO_MAX) return hipErrorInvalidValue;
   const int npan = (N + nbo - 1) / nbo;
   const bool fused = pctrl != nullptr && nbi == 64;
   const bool two = st2 != nullptr && ev != nullptr && nev >= 4 * npan + 2 && (!fused || st3 != nullptr);
+  // st4 (a fourth, high-priority stream): B's look-ahead strip beside the
+  // trailing update instead of before it on B -- its short grid fills the
+  // device's slots next to the trailing launch rather than running alone
+  const bool four = two && st4 != nullptr && nev >= 5 * npan + 3 && !(debug_inject_mask() & IPMZ_DEBUG_NO_FOURTH);
   const int64_t wsz = (int64_t)N * nbo;
   auto Wb = [&](int k) { return W + (two ? (k % 3) : 0) * wsz; };  // T*
   auto pw = [&](int k) { return N - k * nbo < nbo ? N - k * nbo : nbo; };
@@ -536,7 +540,9 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   hipEvent_t* evN = ev + npan;      // P_{k+2} updated with P_k (B)
   hipEvent_t* evC = ev + 2 * npan;  // rows launch of panel k done (C)
   hipEvent_t* evA = ev + 3 * npan;  // chain launch of panel k done (A)
+  hipEvent_t* evT = ev + 4 * npan + 2;  // trailing update with panel k done (B; four streams)
   hipEvent_t evJoin = ev[4 * npan];
+  hipEvent_t evJoin4 = four ? ev[5 * npan + 2] : nullptr;
   // everything the caller enqueued on st before the factor (the mixed path's
   // fp32 conversion, the ctrl-word memsets) comes first on B and C as well
   hipEvent_t evEntry = ev[4 * npan + 1];
@@ -558,12 +564,19 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (p1 >= N) break;
     IPMZ_TRACE("factor: panel %d", k);
     if ((e = stream_record(evP[k], st)) != hipSuccess) return e;
-    // ---- stream B: P_{k+2} columns first, then the rest
+    // ---- stream B: P_{k+2} columns first, then the rest (four streams: the
+    // P_{k+2} strip on st4 after B's previous trailing update, which last
+    // touched those columns; B goes straight on with the rest)
     if ((e = stream_wait(st2, evP[k])) != hipSuccess) return e;
-    if (p2 < N) {
-      if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p2, p3, false, st2)) != hipSuccess) return e;
+    hipStream_t sN = four ? st4 : st2;  // the stream of the P_{k+2} strip and N_k
+    if (four) {
+      if ((e = stream_wait(st4, evP[k])) != hipSuccess) return e;
+      if (k >= 1 && (e = stream_wait(st4, evT[k - 1])) != hipSuccess) return e;
     }
-    if ((e = stream_record(evN[k], st2)) != hipSuccess) return e;
+    if (p2 < N) {
+      if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p2, p3, false, sN)) != hipSuccess) return e;
+    }
+    if ((e = stream_record(evN[k], sN)) != hipSuccess) return e;
     if (p3 < N) {
       hipEvent_t* te = timer && N - p3 > IPMZ_TRAIL_SMALL_M ? timer->next() : nullptr;
       if (te) hipEventRecord(te[0], st2);
@@ -572,6 +585,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if (te) timer->flops += (double)(N - p3) * (double)(N - p3 + 1) * (double)bo;
       if (e != hipSuccess) return e;
     }
+    if (four && (e = stream_record(evT[k], st2)) != hipSuccess) return e;
     // ---- streams A (and C): update P_{k+1} with P_k, factor P_{k+1}
     if (k >= 1) {
       if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
@@ -598,18 +612,22 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
   }
   if ((e = stream_record(evJoin, st2)) != hipSuccess) return e;
+  if (four) {
+    if ((e = stream_record(evJoin4, st4)) != hipSuccess) return e;
+    if ((e = stream_wait(st, evJoin4)) != hipSuccess) return e;
+  }
   return stream_wait(st, evJoin);
 }
 
 hipError_t ldlt_factor(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                        int* info, hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev,
-                       int nev, unsigned* pctrl) {
-  return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl);
+                       int nev, unsigned* pctrl, hipStream_t st4) {
+  return ldlt_factor_t<double>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl, st4);
 }
 hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float* W, int nbo, int nbi, int* info,
                        hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
-                       unsigned* pctrl) {
-  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl);
+                       unsigned* pctrl, hipStream_t st4) {
+  return ldlt_factor_t<float>(K, ld, N, D, Linv, W, nbo, nbi, info, st, timer, st2, st3, ev, nev, pctrl, st4);
 }
 
 }  // namespace ipmz

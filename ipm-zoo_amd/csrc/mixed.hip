@@ -238,7 +238,7 @@ int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w) {
 
 hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st, hipStream_t st2, hipStream_t st3,
                         hipEvent_t* ev,
-                        int nev, TrailTimer* timer) {
+                        int nev, TrailTimer* timer, hipStream_t st4) {
   const int N = w.N;
   if (N <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_mx_scale, dim3((N + MNT - 1) / MNT), dim3(MNT), 0, st, K, ld, N, w.s);
@@ -249,7 +249,7 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   if ((e = solve_reset(w.y32, w.z32, sizeof(float), N, w.ctrl, st)) != hipSuccess) return e;
   if (debug_inject_mask() & IPMZ_DEBUG_CONVERT_ONLY) return hipGetLastError();
   return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, st3, ev, nev,
-                     w.pctrl);
+                     w.pctrl, st4);
 }
 
 hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, double tol, int max_refine,
