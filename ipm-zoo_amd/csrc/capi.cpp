@@ -1446,6 +1446,8 @@ int ipmz_qp_destroy(ipmz_qp* s) {
     delete[] s->tr_pairs;
   }
   for (void* p : s->allocs) hipFree(p);
+  if (s->mw.hev) hipEventDestroy(s->mw.hev);
+  if (s->mw.hst) hipHostFree(s->mw.hst);
   delete s;
   return IPMZ_OK;
 }
@@ -1577,6 +1579,15 @@ int ipmz_qp_set_mixed_precision(ipmz_qp* s, int enable, double tol, int max_refi
     HIP_OK(hipMemset(w, 0, (size_t)bytes));  // sticky error words start clear
     s->mws = static_cast<char*>(w);
     mixed_ws_carve(s->mws, s->N, nbo_for(s->ctx, s->N), s->mw);
+    void* h = nullptr;  // the stop test's host-mapped word (eager solves wait on it)
+    if (hipHostMalloc(&h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+      return fail(IPMZ_ERR_NOMEM, "host allocation failed");
+    s->mw.hst = static_cast<unsigned*>(h);
+    s->mw.hst[0] = s->mw.hst[1] = 0u;
+    void* hd = nullptr;
+    HIP_OK(hipHostGetDevicePointer(&hd, h, 0));
+    s->mw.hst_dev = static_cast<unsigned*>(hd);
+    HIP_OK(hipEventCreateWithFlags(&s->mw.hev, hipEventDisableTiming));
   }
   s->mixed = enable != 0;
   s->ir_tol = tol;

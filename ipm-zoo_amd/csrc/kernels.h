@@ -22,10 +22,11 @@ namespace ipmz {
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
 // 64 = trace the host calls of a step to stderr (the capture experiment),
 // 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B),
-// 256 = the look-ahead strip on the trailing stream before the trailing update (no fourth stream)
+// 256 = the look-ahead strip on the trailing stream before the trailing update (no fourth stream),
+// 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128,
-       IPMZ_DEBUG_NO_FOURTH = 256 };
+       IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -165,6 +166,11 @@ struct MixedWs {
   int* info = nullptr;
   double *s = nullptr, *x = nullptr, *colp = nullptr, *rowp = nullptr, *part = nullptr;
   double* stat = nullptr;  // {||r||_inf / ||b||_inf, corrections} of the last solve
+  // host-mapped {done, corrections} written by the stop test, and the event
+  // the host waits on before reading it (eager solves only: mixed_solve)
+  unsigned *hst = nullptr, *hst_dev = nullptr;
+  hipEvent_t hev = nullptr;
+  int last_iters = 2;  // refinement passes the previous eager solve ran
 };
 int64_t mixed_ws_bytes(int N, int nbo);
 int64_t mixed_ws_carve(char* base, int N, int nbo, MixedWs& w);  // base == nullptr: size only

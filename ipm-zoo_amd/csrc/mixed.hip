@@ -15,7 +15,14 @@
 // per-row-block partials and reduced deterministically (no atomics).
 // Convergence is decided on the device; once it holds every remaining
 // refinement kernel (and the fp32 solve) returns at once, so the loop needs
-// no host round trip and captures into a hipGraph.
+// no host round trip and captures into a hipGraph.  Eagerly, a pass that
+// returns at once still costs its five launches (~30 us, ~1-2 ms for the
+// 20-pass limit of C5), so the eager loop enqueues as many passes as the
+// previous solve needed, waits for the stop test (host-mapped word) and only
+// then enqueues more -- the same kernels in the same order up to the pass
+// that converged, hence the same bits as the full loop.
+#include <algorithm>
+
 #include "common.h"
 #include "kernels.h"
 
@@ -48,7 +55,8 @@ __global__ __launch_bounds__(MNT) void k_mx_to_f32(const double* __restrict__ K,
 
 // x = 0, r32 = fp32(S b), state reset
 __global__ void k_mx_begin(int N, const double* __restrict__ b, const double* __restrict__ s,
-                           double* __restrict__ x, float* __restrict__ r32, unsigned* __restrict__ state) {
+                           double* __restrict__ x, float* __restrict__ r32, unsigned* __restrict__ state,
+                           unsigned* __restrict__ hst) {
   const int i = blockIdx.x * MNT + threadIdx.x;
   if (i < N) {
     x[i] = 0.0;
@@ -57,6 +65,7 @@ __global__ void k_mx_begin(int N, const double* __restrict__ b, const double* __
   if (i == 0) {
     state[ST_DONE] = 0u;
     state[ST_ITERS] = 0u;
+    if (hst) hst[ST_DONE] = 0u;
   }
 }
 
@@ -173,7 +182,7 @@ __global__ __launch_bounds__(MNT) void k_mx_resid(int N, const double* __restric
 
 // convergence test: ||r||_inf <= tol ||b||_inf ; stat = {ratio, corrections}
 __global__ void k_mx_check(int nparts, const double* __restrict__ part, double tol, unsigned* __restrict__ state,
-                           double* __restrict__ stat) {
+                           double* __restrict__ stat, unsigned* __restrict__ hst) {
   if (state[ST_DONE]) return;
   double rr = 0.0, bb = 0.0;
   for (int i = threadIdx.x; i < nparts; i += 64) {
@@ -188,8 +197,13 @@ __global__ void k_mx_check(int nparts, const double* __restrict__ part, double t
       stat[0] = ratio;
       stat[1] = (double)state[ST_ITERS];
     }
+    const unsigned iters = state[ST_ITERS];
     if (ratio <= tol) state[ST_DONE] = 1u;
-    else state[ST_ITERS] += 1u;
+    else state[ST_ITERS] = iters + 1u;
+    if (hst) {
+      hst[ST_ITERS] = iters;
+      hst[ST_DONE] = ratio <= tol ? 1u : 0u;
+    }
   }
 }
 
@@ -258,18 +272,37 @@ hipError_t mixed_solve(const double* K, int64_t ld, MixedWs& w, double* b, doubl
   if (N <= 0) return hipSuccess;
   const int nblk = (N + 63) / 64;
   const dim3 gv((N + MNT - 1) / MNT), bt(MNT);
-  hipLaunchKernelGGL(k_mx_begin, gv, bt, 0, st, N, b, w.s, w.x, w.r32, w.state);
-  for (int it = 0; it <= max_refine; ++it) {
-    hipError_t e = ldlt_solve_persistent(w.K32, w.ld32, N, w.D32, w.P32, w.r32, w.y32, w.z32, w.ctrl, st,
-                                         it ? w.state : nullptr);
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_mx_accum, gv, bt, 0, st, N, w.s, w.r32, w.x, w.state);
-    hipLaunchKernelGGL(k_mx_symv, dim3((nblk + 1) / 2, NSPLIT), bt, 0, st, K, ld, N, w.x, w.colp, w.rowp, nblk,
-                       w.state);
-    hipLaunchKernelGGL(k_mx_resid, dim3((N + 63) / 64), bt, 0, st, N, b, w.s, w.colp, w.rowp, nblk, w.r32, w.part,
-                       w.state);
-    hipLaunchKernelGGL(k_mx_check, dim3(1), dim3(64), 0, st, (N + 63) / 64, w.part, tol, w.state, w.stat);
+  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+  hipError_t e = hipStreamIsCapturing(st, &cs);
+  if (e != hipSuccess) return e;
+  const bool eager = w.hst && w.hev && cs == hipStreamCaptureStatusNone && !(debug_inject_mask() & IPMZ_DEBUG_IR_FULL);
+  unsigned* hst = eager ? w.hst_dev : nullptr;
+  hipLaunchKernelGGL(k_mx_begin, gv, bt, 0, st, N, b, w.s, w.x, w.r32, w.state, hst);
+  const int passes = max_refine + 1;
+  int it = 0, chunk = eager ? std::min(std::max(w.last_iters, 1), passes) : passes;
+  while (it < passes) {
+    for (const int end = std::min(passes, it + chunk); it < end; ++it) {
+      e = ldlt_solve_persistent(w.K32, w.ld32, N, w.D32, w.P32, w.r32, w.y32, w.z32, w.ctrl, st,
+                                it ? w.state : nullptr);
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(k_mx_accum, gv, bt, 0, st, N, w.s, w.r32, w.x, w.state);
+      hipLaunchKernelGGL(k_mx_symv, dim3((nblk + 1) / 2, NSPLIT), bt, 0, st, K, ld, N, w.x, w.colp, w.rowp, nblk,
+                         w.state);
+      hipLaunchKernelGGL(k_mx_resid, dim3((N + 63) / 64), bt, 0, st, N, b, w.s, w.colp, w.rowp, nblk, w.r32, w.part,
+                         w.state);
+      hipLaunchKernelGGL(k_mx_check, dim3(1), dim3(64), 0, st, (N + 63) / 64, w.part, tol, w.state, w.stat, hst);
+    }
+    if (!eager || it >= passes) break;
+    if ((e = hipEventRecord(w.hev, st)) != hipSuccess) return e;
+    if ((e = hipEventSynchronize(w.hev)) != hipSuccess) return e;
+    const volatile unsigned* h = w.hst;
+    if (h[ST_DONE]) {
+      w.last_iters = (int)h[ST_ITERS] + 1;
+      break;
+    }
+    chunk = 1;
   }
+  if (eager && it >= passes) w.last_iters = std::max(1, passes - 1);  // learn the count next time
   hipLaunchKernelGGL(k_mx_finish, gv, bt, 0, st, N, w.x, b);
   return hipGetLastError();
 }
