@@ -311,6 +311,29 @@ static rocblas_handle blas_for(hipStream_t st) {
 }
 // row-major C (lower, R x R, ldc) -= W (R x k, ldw) L^T (L: R x k, ldl) as the
 // column-major upper triangle: C' -= L'^T W' with L' = L^T (k x R, ldl), W' = W^T
+//
+// SYRKX recurses down to 16 x 16 diagonal blocks, and at C5 its small launches
+// (the 16-wide diagonal kernel, 32 x 16 / 16 x 32 tiles) take ~4.4 of its
+// ~16 ms per factor for ~3 % of the flops (profiles/r03_s5/c5_rocblas_kernels.txt).  So the triangle is
+// split here instead: R = 2^L w (w <= IPMZ_BLAS_W); level l of the halving
+// tree is ONE strided-batched SGEMM over its 2^l off-diagonal squares of order
+// R / 2^(l+1), and the 2^L diagonal w x w triangles are ONE batched launch of
+// the hand-written triangular-grid kernel (batch strides below).  Every
+// element of C is updated by exactly one launch, in a fixed order: the
+// result does not depend on scheduling.  R without such a split: SYRKX.
+static int blas_split_levels(int R) {
+  static const int wmax = [] {
+    const char* e = getenv("IPMZ_BLAS_W");
+    const int v = e ? atoi(e) : 512;
+    return v > 0 ? v : 0;  // 0: SYRKX
+  }();
+  if (!wmax) return -1;
+  for (int L = 0; L < 12; ++L) {
+    if (R % (1 << L)) return -1;
+    if ((R >> L) <= wmax) return (R >> L) >= 64 ? L : -1;
+  }
+  return -1;
+}
 static bool blas_trailing(int R, int k, const float* W, int64_t ldw, const float* L, int64_t ldl, float* C,
                           int64_t ldc, hipStream_t st) {
   if (R < IPMZ_BLAS_MIN_R || (debug_inject_mask() & IPMZ_DEBUG_NO_BLAS)) return false;
@@ -319,8 +342,37 @@ static bool blas_trailing(int R, int k, const float* W, int64_t ldw, const float
   rocblas_handle h = blas_for(st);
   if (!h) return false;
   const float alpha = -1.f, beta = 1.f;
-  return rocblas_ssyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, k, &alpha, L, (rocblas_int)ldl, W,
-                        (rocblas_int)ldw, &beta, C, (rocblas_int)ldc) == rocblas_status_success;
+  const int levels = blas_split_levels(R);
+  if (levels < 0)
+    return rocblas_ssyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, k, &alpha, L, (rocblas_int)ldl, W,
+                          (rocblas_int)ldw, &beta, C, (rocblas_int)ldc) == rocblas_status_success;
+  // level l: squares p = 0..2^l-1 of order S/2 (S = R / 2^l): rows
+  // [pS + S/2, pS + S), columns [pS, pS + S/2) of the row-major C, i.e. the
+  // column-major C'(cols, rows) -= L'(:, cols)^T W'(:, rows)
+  for (int l = 0; l < levels; ++l) {
+    const int64_t S = R >> l, hS = S / 2;
+    if (rocblas_sgemm_strided_batched(h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)hS,
+                                      (rocblas_int)hS, k, &alpha, L, (rocblas_int)ldl, S * ldl,
+                                      W + hS * ldw, (rocblas_int)ldw, S * ldw, &beta, C + hS * ldc,
+                                      (rocblas_int)ldc, S * ldc + S, 1 << l) != rocblas_status_success)
+      return false;
+  }
+  const int w = R >> levels;
+  GemmArgsT<float> g{};
+  g.M = g.N = w;
+  g.Kd = k;
+  g.A = W;
+  g.lda = ldw;
+  g.B = L;
+  g.ldb = ldl;
+  g.C = C;
+  g.ldc = ldc;
+  g.lower = 2;
+  g.sA = (int64_t)w * ldw;
+  g.sB = (int64_t)w * ldl;
+  g.sC = (int64_t)w * ldc + w;
+  if (w > 512) return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, 1 << levels) == hipSuccess;
+  return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, 1 << levels) == hipSuccess;
 }
 
 // C[i][j] -= sum_k A[i][k] B[j][k] over the lower part of a trailing region.
