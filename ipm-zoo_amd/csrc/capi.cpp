@@ -80,10 +80,10 @@ static int ensure_events(ipmz_ctx* ctx, size_t n) {
 // caller's stream waits for each of them (the chain stream A has already
 // waited for B's and C's work; the explicit waits keep every stream a capture
 // forked joined back into its origin -- ldlt.hip stream_wait)
-static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev4) {
+static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev4, bool fourth) {
   hipStream_t side[4] = {ctx->sA, ctx->sB, ctx->sC, ctx->sD};
   hipEvent_t* ev3 = ev4;
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < (fourth ? 4 : 3); ++i) {
     hipError_t e = stream_record(ev3[i], side[i]);
     if (e == hipSuccess) e = stream_wait(ctx->stream, ev3[i]);
     if (e != hipSuccess) return e;
@@ -348,12 +348,13 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
+  const bool fourth = !(debug_inject_mask() & IPMZ_DEBUG_NO_FOURTH);
+  if (fourth) HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
   HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
-                     pctrl, ctx->sD));
+                     pctrl, fourth ? ctx->sD : nullptr));
   // join (A has already waited for B's tail)
   IPMZ_TRACE("factor_impl: join");
-  HIP_OK(join_side_streams(ctx, ev + nev));
+  HIP_OK(join_side_streams(ctx, ev + nev, fourth));
   IPMZ_TRACE("factor_impl: joined");
   HIP_OK(prep());
   return IPMZ_OK;
@@ -431,9 +432,10 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
   HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
-  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer, ctx->sD));
-  HIP_OK(join_side_streams(ctx, ev + nev));
+  const bool fourth = !(debug_inject_mask() & IPMZ_DEBUG_NO_FOURTH);
+  if (fourth) HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
+  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer, fourth ? ctx->sD : nullptr));
+  HIP_OK(join_side_streams(ctx, ev + nev, fourth));
   HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
   return IPMZ_OK;
 }
@@ -793,6 +795,7 @@ struct ipmz_qp {
   // completion of the last multi-stream (eager) step: the next one is not
   // enqueued before it (queue depth 1, see step_impl)
   hipEvent_t step_done = nullptr;
+  hipEvent_t step_in = nullptr;  // the caller's stream reached the step (the fork onto ctx->own)
   bool step_pending = false;
   int last_step_graph = 0;  // the last ipmz_qp_step replayed a captured hipGraph
   int tr_cap = 0;
@@ -1261,7 +1264,7 @@ int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
   s->last_step_graph = 0;
-  if (step_forks(s) && !s->timing) {
+  if (step_forks(s) && (!s->timing || s->ctx->stream != s->ctx->own)) {  // timing: phase events on own, below
     // A factorization that forks onto the look-ahead streams is enqueued
     // eagerly (~130-160 launches and event waits over four queues); with
     // the next step's packets already queued behind it the command processor
@@ -1271,9 +1274,30 @@ int step_impl(ipmz_qp* s, int flags) {
     if (!s->step_done) HIP_OK(hipEventCreateWithFlags(&s->step_done, hipEventDisableTiming));
     if (s->step_pending) HIP_OK(hipEventSynchronize(s->step_done));
     s->step_pending = false;
+    // On a stream the caller made (torch's default or side streams) the step
+    // runs on the context's own stream, forked from the caller's, and the host
+    // waits for it before the caller's stream is joined to it: a join left
+    // pending on the caller's stream while the step runs cost ~1.2 ms per C3
+    // step (15.7 vs 14.5 ms; the step on the caller's stream itself the same),
+    // profiles/r03_s5/origin_stream_ab.log.  The host would wait for the step
+    // before enqueuing the next one anyway (queue depth 1).
+    hipStream_t caller = s->ctx->stream, own = s->ctx->own;
+    const bool hop = caller != own;
+    if (hop) {
+      if (!s->step_in) HIP_OK(hipEventCreateWithFlags(&s->step_in, hipEventDisableTiming));
+      HIP_OK(hipEventRecord(s->step_in, caller));
+      HIP_OK(hipStreamWaitEvent(own, s->step_in, 0));
+      s->ctx->stream = own;
+    }
     const int rc = run_step(s, flags);
+    s->ctx->stream = caller;
     if (rc) return rc;
-    HIP_OK(hipEventRecord(s->step_done, s->ctx->stream));
+    HIP_OK(hipEventRecord(s->step_done, own));
+    if (hop) {
+      HIP_OK(hipEventSynchronize(s->step_done));
+      HIP_OK(hipStreamWaitEvent(caller, s->step_done, 0));  // complete: orders nothing pending
+      return IPMZ_OK;
+    }
     s->step_pending = true;
     return IPMZ_OK;
   }
@@ -1438,6 +1462,7 @@ int ipmz_qp_destroy(ipmz_qp* s) {
   if (s->graph) hipGraphDestroy(s->graph);
   for (auto e : s->ev) hipEventDestroy(e);
   if (s->step_done) hipEventDestroy(s->step_done);
+  if (s->step_in) hipEventDestroy(s->step_in);
   if (s->tr_pairs) {
     for (int i = 0; i < s->tr_cap; ++i) {
       hipEventDestroy(s->tr_pairs[i][0]);

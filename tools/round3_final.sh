@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3 validation: smoke, every GPU test, default bench line, kernel stats (profiles/r03_s4)
+# round-3 validation: smoke, every GPU test, default bench line, kernel stats (profiles/r03_s5)
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
