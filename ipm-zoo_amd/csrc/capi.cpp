@@ -348,8 +348,10 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
   HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
-  const bool fourth = !(debug_inject_mask() & IPMZ_DEBUG_NO_FOURTH);
-  if (fourth) HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
+  // the fourth look-ahead stream pays for the fp32 factor only (C5 23.6 ->
+  // 22.9 ms per step); the fp64 one runs faster without it (C3 14.2 -> 14.0
+  // ms), profiles/r03_s5/fourth_stream_ab.log -- not forked at all here
+  const bool fourth = false;
   HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
                      pctrl, fourth ? ctx->sD : nullptr));
   // join (A has already waited for B's tail)

@@ -22,7 +22,7 @@ namespace ipmz {
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
 // 64 = trace the host calls of a step to stderr (the capture experiment),
 // 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B),
-// 256 = the look-ahead strip on the trailing stream before the trailing update (no fourth stream),
+// 256 = the fp32 factor's look-ahead strip on the trailing stream before the trailing update (no fourth stream),
 // 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128,
