@@ -250,8 +250,9 @@ def run_single(I, ctx, args, world, dist, torch, workload):
             trk = load_json("profiles/pmc_traffic.json") if workload == "c3" else None
             tach = ph["trailing_flops"] / tr_s / 1e12
             roof["trailing"] = {
-                "kernel": ("rocblas_ssyrkx for trailing orders >= 4096, gemm_nt_kernel<float,128,128,EPI_SUB,2,4> "
-                           "below (trailing update A22 -= W21 L21^T)" if mixed else
+                "kernel": ("trailing orders >= 4096: a halving tree of rocblas_sgemm_strided_batched levels + one "
+                           "batched gemm_nt_kernel<float,64,64> launch for the 512-wide diagonal blocks; "
+                           "gemm_nt_kernel<float,...> below (trailing update A22 -= W21 L21^T)" if mixed else
                            "gemm_nt_kernel<double,128,128,EPI_SUB,4,4> (trailing update A22 -= W21 L21^T)"),
                 "achieved": tach, "peak": peak, "unit": "TFLOP/s", "frac": tach / peak,
                 "traffic": trk.get("traffic_bytes_per_launch") if trk else None,

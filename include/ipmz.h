@@ -260,7 +260,12 @@ int ipmz_qp_load_host(ipmz_qp* qp, const double* Q, const double* c, const doubl
                       const double* u_A, const double* C, const double* d, const double* l_x, const double* u_x);
 /* The synthetic QP of SURVEY.md §8d generated in place on the device. */
 int ipmz_qp_generate(ipmz_qp* qp, uint64_t seed);
-/* Enqueue one Newton step (asynchronous).  flags: */
+/* Enqueue one Newton step (asynchronous).  A step whose factor forks onto the
+ * look-ahead streams (>= 3 outer panels) is kept to one in flight: on the
+ * context's own stream the next call waits for it; on a stream set with
+ * ipmz_ctx_set_stream it runs on the context's own stream and the call
+ * returns once it completed, the caller's stream joined to it (a join left
+ * pending on the caller's stream slows the step).  flags: */
 #define IPMZ_STEP_RESTART_IF_CONVERGED 1 /* reset a converged iterate to the initial one first */
 #define IPMZ_STEP_GRAPH 2                /* capture once into a hipGraph, then replay (steps whose
                                             factor forks onto the look-ahead streams -- >= 3 outer

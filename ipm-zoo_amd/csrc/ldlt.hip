@@ -315,22 +315,19 @@ static rocblas_handle blas_for(hipStream_t st) {
 // SYRKX recurses down to 16 x 16 diagonal blocks, and at C5 its small launches
 // (the 16-wide diagonal kernel, 32 x 16 / 16 x 32 tiles) take ~4.4 of its
 // ~16 ms per factor for ~3 % of the flops (profiles/r03_s5/c5_rocblas_kernels.txt).  So the triangle is
-// split here instead: R = 2^L w (w <= IPMZ_BLAS_W); level l of the halving
+// split here instead: R = 2^L w (w <= IPMZ_BLAS_TREE_W = 512, measured
+// against 128 / 256 / 1024 / 2048, profiles/r03_s5/blas_tree_ab.log); level l of the halving
 // tree is ONE strided-batched SGEMM over its 2^l off-diagonal squares of order
 // R / 2^(l+1), and the 2^L diagonal w x w triangles are ONE batched launch of
 // the hand-written triangular-grid kernel (batch strides below).  Every
 // element of C is updated by exactly one launch, in a fixed order: the
-// result does not depend on scheduling.  R without such a split: SYRKX.
+// result does not depend on scheduling.  R without such a split (or debug
+// bit IPMZ_DEBUG_SYRKX): SYRKX.
 static int blas_split_levels(int R) {
-  static const int wmax = [] {
-    const char* e = getenv("IPMZ_BLAS_W");
-    const int v = e ? atoi(e) : 512;
-    return v > 0 ? v : 0;  // 0: SYRKX
-  }();
-  if (!wmax) return -1;
+  if (debug_inject_mask() & IPMZ_DEBUG_SYRKX) return -1;
   for (int L = 0; L < 12; ++L) {
     if (R % (1 << L)) return -1;
-    if ((R >> L) <= wmax) return (R >> L) >= 64 ? L : -1;
+    if ((R >> L) <= IPMZ_BLAS_TREE_W) return (R >> L) >= 64 ? L : -1;
   }
   return -1;
 }

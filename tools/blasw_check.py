@@ -1,5 +1,6 @@
 """C5 fp32 trailing update: SYRKX vs the halving tree (IPMZ_BLAS_W, read once
-per process).  Prints the refinement statistics and the iterate after K steps
+per process by the experiment build of profiles/r03_s5/blas_tree_ab.log; the
+product has w = 512 built in, debug bit 1024 = SYRKX).  Prints the refinement statistics and the iterate after K steps
 (saved to gpurun_out/blasw_<W>.npy for cross-run comparison), twice, and
 whether the two runs are bitwise equal (determinism), then ms per step.
     IPMZ_BLAS_W=256 python tools/blasw_check.py"""

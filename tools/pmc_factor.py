@@ -28,7 +28,8 @@ import sys
 from collections import defaultdict
 
 FACTOR_KERNELS = ("gemm_nt_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel",
-                  "ldlt_small_kernel", "ldlt_small_pair_kernel")  # (the last two: C4's batched factor)
+                  "ldlt_small_kernel", "ldlt_small_pair_kernel",  # (these two: C4's batched factor)
+                  "Cijk_", "rocblas_")  # C5's fp32 trailing update (rocBLAS SGEMM levels of the halving tree)
 
 
 def load(d):
