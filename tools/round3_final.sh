@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-3 validation: smoke, every GPU test, default bench line, kernel stats (profiles/r03_s5)
+# round-3 validation: smoke, every GPU test, default bench line, kernel stats (profiles/r03_s5, r03_s6)
 set -u
 export TMPDIR=/tmp
 mkdir -p gpurun_out
