@@ -41,13 +41,13 @@ FP32_MFMA_PEAK_TFLOPS = 157.3  # MI355X f32-input MFMA peak (MI355X_MICROARCH.md
 
 HEADLINE_METRIC = "Newton steps/sec + factor TFLOP/s, dense QP n=8192, 1/2/4/8 MI355X"  # BASELINE.json metric
 WORKLOADS = {
-    "c3": dict(n=8192, m=2048, p=1024, sample_scale=2, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
+    "c3": dict(n=8192, m=2048, p=1024, sample_scale=1, desc="dense QP n=8192, m=2048 ineq (SlackedSlacks), p=1024 eq "
                                           "(Regularization), augmented LDL^T, KKT N=11264"),
     "c2": dict(n=2048, m=512, p=0, normal=True, sample_scale=1,
                desc="dense QP n=2048, m=512 ineq, normal equations: Cholesky(H) + TRSM + SYRK + Cholesky(S)"),
     "c2_aug": dict(n=2048, m=512, p=0, sample_scale=1, desc="C2's QP (n=2048, m=512) with the augmented LDL^T, for comparison"),
     "small": dict(n=1024, m=256, p=128, sample_scale=1, desc="dense QP n=1024, m=256, p=128 (smoke size)"),
-    "c5": dict(n=16384, m=0, p=0, mixed=True, sample_scale=8,
+    "c5": dict(n=16384, m=0, p=0, mixed=True, sample_scale=2,
                desc="dense QP n=16384 box-only (SlackedSlacks), fp32 LDL^T of the scaled KKT + fp64 iterative "
                     "refinement to 1e-12"),
     "c4": dict(n=256, m=64, p=0, batch=1024, sample_scale=1,
@@ -58,21 +58,42 @@ WORKLOADS = {
 }
 
 
-def cpu_child(*args):
+def cpu_start(*args):
     """oracle/cpu_bench.py as a child process (it never touches the GPU)."""
-    r = subprocess.run([sys.executable, os.path.join(REPO, "oracle", "cpu_bench.py"), *map(str, args)],
-                       capture_output=True, text=True, timeout=600)
-    if r.returncode != 0:
-        return {"error": r.stderr[-400:]}
-    return json.loads(r.stdout.strip().splitlines()[-1])
+    return subprocess.Popen([sys.executable, os.path.join(REPO, "oracle", "cpu_bench.py"), *map(str, args)],
+                            stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
 
 
-def cpu_baseline(wl):
-    if wl.get("batch"):
-        one = cpu_child("batch", wl["n"], wl["m"], 10, 1)
-        one["all_cores"] = cpu_child("batch", wl["n"], wl["m"], 8, 16)
-        return one
-    return cpu_child("step", wl["n"], wl["m"], wl["p"], wl.get("sample_scale", 4))
+def cpu_finish(proc):
+    try:
+        out, err = proc.communicate(timeout=900)
+    except subprocess.TimeoutExpired:
+        proc.kill()
+        proc.communicate()
+        return {"error": "timed out after 900 s"}
+    if proc.returncode != 0:
+        return {"error": err[-400:]}
+    return json.loads(out.strip().splitlines()[-1])
+
+
+def cpu_baselines(names):
+    """The single-core CPU legs of `names` side by side, each pinned to its own
+    core (so the wall time is the longest one, ~3 min for a full-size C3
+    step), then C4's all-core leg alone (it takes 16 cores)."""
+    procs, slot = {}, 0
+    for w in names:
+        wl = WORKLOADS[w]
+        if wl.get("batch"):
+            procs[w] = cpu_start("batch", wl["n"], wl["m"], 10, 1)
+        else:
+            procs[w] = cpu_start("step", wl["n"], wl["m"], wl["p"], wl.get("sample_scale", 4), slot)
+        slot += 1
+    out = {w: cpu_finish(p) for w, p in procs.items()}
+    for w in names:
+        wl = WORKLOADS[w]
+        if wl.get("batch"):
+            out[w]["all_cores"] = cpu_finish(cpu_start("batch", wl["n"], wl["m"], 8, 16))
+    return out
 
 
 def load_json(rel):
@@ -290,11 +311,16 @@ def main():
     cpu = {}
     if not args.no_cpu_baseline and int(os.environ.get("WORLD_SIZE", "1")) == 1:
         wl0 = WORKLOADS[args.workload]
-        cpu["head"] = cpu_baseline(wl0)
+        names = [args.workload]
         if not wl0.get("batch") and not args.no_batched:
-            cpu["batched"] = cpu_baseline(WORKLOADS["c4"])
+            names.append("c4")
         if args.workload == "c3" and not args.no_configs:
-            cpu.update({w: cpu_baseline(WORKLOADS[w]) for w in ("c2", "c5")})
+            names += ["c2", "c5"]
+        res = cpu_baselines(names)
+        cpu["head"] = res[args.workload]
+        if "c4" in res and args.workload != "c4":
+            cpu["batched"] = res["c4"]
+        cpu.update({w: res[w] for w in ("c2", "c5") if w in res and w != args.workload})
 
     import torch
     import torch.distributed as dist

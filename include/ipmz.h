@@ -265,7 +265,13 @@ int ipmz_qp_generate(ipmz_qp* qp, uint64_t seed);
  * context's own stream the next call waits for it; on a stream set with
  * ipmz_ctx_set_stream it runs on the context's own stream and the call
  * returns once it completed, the caller's stream joined to it (a join left
- * pending on the caller's stream slows the step).  flags: */
+ * pending on the caller's stream slows the step).  A step
+ * through the mixed-precision solve (ipmz_qp_set_mixed_precision) also
+ * blocks the host while its refinement runs: the eager loop reads a
+ * host-mapped stop test after each pass instead of enqueuing all
+ * max_refine + 1 passes.  When the caller's stream is capturing a hipGraph
+ * the step is enqueued into that capture on that stream (no host wait, all
+ * refinement passes, IPMZ_STEP_GRAPH ignored).  flags: */
 #define IPMZ_STEP_RESTART_IF_CONVERGED 1 /* reset a converged iterate to the initial one first */
 #define IPMZ_STEP_GRAPH 2                /* capture once into a hipGraph, then replay (steps whose
                                             factor forks onto the look-ahead streams -- >= 3 outer

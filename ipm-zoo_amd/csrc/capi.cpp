@@ -1266,6 +1266,22 @@ int step_impl(ipmz_qp* s, int flags) {
   if (!s || !s->loaded) return fail(IPMZ_ERR_STATE, "load or generate the QP first");
   HIP_OK(hipSetDevice(s->ctx->device));
   s->last_step_graph = 0;
+  {
+    // The caller's stream is capturing (torch.cuda.graph around step()): the
+    // whole step goes into the caller's capture on that stream -- no hop to
+    // the own stream, no host wait, no nested capture (the look-ahead
+    // streams order through capture dependencies, ldlt.hip stream_wait; the
+    // mixed solve enqueues all its passes, mixed.hip)
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    HIP_OK(hipStreamIsCapturing(s->ctx->stream, &cs));
+    if (cs != hipStreamCaptureStatusNone) {
+      if (s->timing) return fail(IPMZ_ERR_STATE, "phase timing inside a caller's graph capture");
+      set_capture_origin(s->ctx->stream);
+      const int rc = run_step(s, flags & ~IPMZ_STEP_GRAPH);
+      set_capture_origin(nullptr);
+      return rc;
+    }
+  }
   if (step_forks(s) && (!s->timing || s->ctx->stream != s->ctx->own)) {  // timing: phase events on own, below
     // A factorization that forks onto the look-ahead streams is enqueued
     // eagerly (~130-160 launches and event waits over four queues); with

@@ -21,13 +21,12 @@ namespace ipmz {
 // DEBUG bits (determinism experiments): 16 = the mixed factor stops after
 // the scale + fp32 conversion, 32 = factors run on one stream (no look-ahead)
 // 64 = trace the host calls of a step to stderr (the capture experiment),
-// 128 = the fp32 trailing update on gemm_nt_kernel even where rocBLAS SYRKX would run (A/B),
+// 128 = the fp32 trailing and strip updates on the gemm.h engine instead of gemm32.h (A/B),
 // 256 = the fp32 factor's look-ahead strip on the trailing stream before the trailing update (no fourth stream),
-// 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test),
-// 1024 = the fp32 trailing update as one rocBLAS SSYRKX (not the halving tree)
+// 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
-       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_NO_BLAS = 128,
-       IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512, IPMZ_DEBUG_SYRKX = 1024 };
+       IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
+       IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -66,6 +65,8 @@ bool small_pair_eligible(int B, int N);
 #define IPMZ_SMALL_NMAX 1024
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs);
+hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, double* D, double* Linv, double* W,
+                                     int* info, hipStream_t st, const BatchStrides& bs);  // kbench only
 hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int nbo, int nbi,
                                int* info, hipStream_t st, const BatchStrides& bs);
 // In-place blocked LDL^T of the lower triangle of K (row-major, ld).
@@ -75,9 +76,6 @@ hipError_t ldlt_factor_batched(double* K, int64_t ld, int N, double* D, double* 
 // trailing updates of order <= this run on 64 x 64 tiles, larger ones on the
 // 128 x 128 kernel (the one TrailTimer times: the roofline kernel of bench.py)
 #define IPMZ_TRAIL_SMALL_M 3072
-// fp32 trailing updates of at least this order run on rocBLAS SYRKX (ldlt.hip)
-#define IPMZ_BLAS_MIN_R 4096
-#define IPMZ_BLAS_TREE_W 512  // the halving tree's diagonal blocks (ldlt.hip blas_trailing)
 struct TrailTimer {  // HIP-event pairs around every dominant trailing-update launch
   hipEvent_t (*pairs)[2] = nullptr;
   int cap = 0, used = 0;

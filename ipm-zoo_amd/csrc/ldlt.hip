@@ -18,8 +18,6 @@
 // fits one block factors bit-identically to the reference.  Across blocks the
 // MFMA accumulates a block's contributions before subtracting them, which
 // changes rounding at the 1e-16 level (parity tolerance: tests/).
-#include <rocblas/rocblas.h>
-
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -30,6 +28,7 @@
 #include "common.h"
 #include "diag64.h"
 #include "gemm.h"
+#include "gemm32.h"
 #include "kernels.h"
 
 namespace ipmz {
@@ -284,92 +283,22 @@ static void launch_diag64(int B, hipStream_t st, float* K, int64_t ld, int j0, i
 }
 
 // ---------------------------------------------------------------------------
-// The fp32 trailing update (mixed-precision factor, C5) through rocBLAS
-// SYRKX: measured 112.5 vs 88.9 TFLOP/s for gemm_nt_kernel<float> at R =
-// 15872, rank 512 (profiles/r03_s3/gemmref32.log); C5 38.7 -> 41.6 steps/s,
-// factor 21.5 -> 19.9 ms (profiles/r03_s3/blas_ab.log) -- a plain library
-// BLAS-3 call on the same operands.  (The fp32 look-ahead strips through
-// SGEMM / SYRKX as well: no further gain, 41.3 steps/s.)  One handle per (device, stream),
-// made on first use (never inside a graph capture: the hand-written kernel
-// runs there).
-static rocblas_handle blas_for(hipStream_t st) {
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, rocblas_handle> handles;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> lock(mu);
-  auto it = handles.find({dev, st});
-  if (it != handles.end()) return it->second;
-  rocblas_handle h = nullptr;
-  if (rocblas_create_handle(&h) != rocblas_status_success) return nullptr;
-  if (rocblas_set_stream(h, st) != rocblas_status_success) {
-    rocblas_destroy_handle(h);
-    return nullptr;
+// The fp32 updates of the mixed-precision factor (C5) on the 32 x 32 x 2 f32
+// MFMA kernel of gemm32.h: the trailing triangle as ONE launch over its lower
+// tiles (the round-3 rocBLAS halving tree of strided-batched SGEMMs is gone),
+// and the look-ahead strips.  Tile choice by size (tools/sgemm_bench.cpp,
+// profiles/r04_*/sgemm*.log).  Operands whose rows are not 16-byte aligned
+// (never the factor's own: ld and nbo are multiples of 64) take the gemm.h
+// engine; so does debug bit IPMZ_DEBUG_F32_ENGINE (A/B).
+static bool sgemm_sub(GemmArgsT<float>& g, bool square_lower, hipStream_t st, hipError_t& e) {
+  if (!sgemm_aligned(g) || (debug_inject_mask() & IPMZ_DEBUG_F32_ENGINE)) return false;
+  if (square_lower) {
+    e = g.M <= IPMZ_TRAIL_SMALL_M ? launch_sgemm<64, 64, 2, 2, 32, 4>(g, st) : launch_sgemm<128, 128, 2, 2, 32, 2>(g, st);
+    return true;
   }
-  handles[{dev, st}] = h;
-  return h;
-}
-// row-major C (lower, R x R, ldc) -= W (R x k, ldw) L^T (L: R x k, ldl) as the
-// column-major upper triangle: C' -= L'^T W' with L' = L^T (k x R, ldl), W' = W^T
-//
-// SYRKX recurses down to 16 x 16 diagonal blocks, and at C5 its small launches
-// (the 16-wide diagonal kernel, 32 x 16 / 16 x 32 tiles) take ~4.4 of its
-// ~16 ms per factor for ~3 % of the flops (profiles/r03_s5/c5_rocblas_kernels.txt).  So the triangle is
-// split here instead: R = 2^L w (w <= IPMZ_BLAS_TREE_W = 512, measured
-// against 128 / 256 / 1024 / 2048, profiles/r03_s5/blas_tree_ab.log); level l of the halving
-// tree is ONE strided-batched SGEMM over its 2^l off-diagonal squares of order
-// R / 2^(l+1), and the 2^L diagonal w x w triangles are ONE batched launch of
-// the hand-written triangular-grid kernel (batch strides below).  Every
-// element of C is updated by exactly one launch, in a fixed order: the
-// result does not depend on scheduling.  R without such a split (or debug
-// bit IPMZ_DEBUG_SYRKX): SYRKX.
-static int blas_split_levels(int R) {
-  if (debug_inject_mask() & IPMZ_DEBUG_SYRKX) return -1;
-  for (int L = 0; L < 12; ++L) {
-    if (R % (1 << L)) return -1;
-    if ((R >> L) <= IPMZ_BLAS_TREE_W) return (R >> L) >= 64 ? L : -1;
-  }
-  return -1;
-}
-static bool blas_trailing(int R, int k, const float* W, int64_t ldw, const float* L, int64_t ldl, float* C,
-                          int64_t ldc, hipStream_t st) {
-  if (R < IPMZ_BLAS_MIN_R || (debug_inject_mask() & IPMZ_DEBUG_NO_BLAS)) return false;
-  hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return false;
-  rocblas_handle h = blas_for(st);
-  if (!h) return false;
-  const float alpha = -1.f, beta = 1.f;
-  const int levels = blas_split_levels(R);
-  if (levels < 0)
-    return rocblas_ssyrkx(h, rocblas_fill_upper, rocblas_operation_transpose, R, k, &alpha, L, (rocblas_int)ldl, W,
-                          (rocblas_int)ldw, &beta, C, (rocblas_int)ldc) == rocblas_status_success;
-  // level l: squares p = 0..2^l-1 of order S/2 (S = R / 2^l): rows
-  // [pS + S/2, pS + S), columns [pS, pS + S/2) of the row-major C, i.e. the
-  // column-major C'(cols, rows) -= L'(:, cols)^T W'(:, rows)
-  for (int l = 0; l < levels; ++l) {
-    const int64_t S = R >> l, hS = S / 2;
-    if (rocblas_sgemm_strided_batched(h, rocblas_operation_transpose, rocblas_operation_none, (rocblas_int)hS,
-                                      (rocblas_int)hS, k, &alpha, L, (rocblas_int)ldl, S * ldl,
-                                      W + hS * ldw, (rocblas_int)ldw, S * ldw, &beta, C + hS * ldc,
-                                      (rocblas_int)ldc, S * ldc + S, 1 << l) != rocblas_status_success)
-      return false;
-  }
-  const int w = R >> levels;
-  GemmArgsT<float> g{};
-  g.M = g.N = w;
-  g.Kd = k;
-  g.A = W;
-  g.lda = ldw;
-  g.B = L;
-  g.ldb = ldl;
-  g.C = C;
-  g.ldc = ldc;
-  g.lower = 2;
-  g.sA = (int64_t)w * ldw;
-  g.sB = (int64_t)w * ldl;
-  g.sC = (int64_t)w * ldc + w;
-  if (w > 512) return launch_gemm<128, 128, EPI_SUB, 2, 4, OPT_NOR2 | OPT_GRP>(g, st, 1 << levels) == hipSuccess;
-  return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, 1 << levels) == hipSuccess;
+  e = g.M <= 4096 ? launch_sgemm<64, 64, 2, 2, 32, 4, EPI_SUB_STRIP>(g, st)
+                  : launch_sgemm<128, 128, 2, 2, 32, 2, EPI_SUB_STRIP>(g, st);
+  return true;
 }
 
 // C[i][j] -= sum_k A[i][k] B[j][k] over the lower part of a trailing region.
@@ -411,9 +340,11 @@ static hipError_t gemm_nt_sub_t(int M, int N, int Kd, const T* A, int64_t lda, c
   // two workgroups = 32 waves per CU): 56.6 vs 55.2 TFLOP/s alone (kbench
   // gvar, R = 10880, rank 384), 40.8 vs 38.9 in situ, C3 60.6 -> 61.8
   // steps/s; the fp32 factor (C5) keeps 2 x 4 (71 vs 67 TFLOP/s in situ)
+  if constexpr (std::is_same<T, float>::value) {
+    hipError_t e = hipSuccess;
+    if (batch == 1 && sgemm_sub(g, square_lower, st, e)) return e;
+  }
   if (square_lower) {
-    if constexpr (std::is_same<T, float>::value)
-      if (batch == 1 && M == N && blas_trailing(M, Kd, A, lda, B, ldb, C, ldc, st)) return hipSuccess;
     if (M <= IPMZ_TRAIL_SMALL_M) return launch_gemm<64, 64, EPI_SUB, 2, 2, OPT_NOR2 | OPT_GRP>(g, st, batch);
     if constexpr (std::is_same<T, double>::value)
       return launch_gemm<128, 128, EPI_SUB, 4, 4, OPT_NOR2 | OPT_GRP>(g, st, batch);

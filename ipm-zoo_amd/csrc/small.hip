@@ -386,4 +386,17 @@ hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, do
   return hipGetLastError();
 }
 
+// experiment entry (tools/kbench.cpp "smallv"): the one-workgroup factor with
+// SNW = 4 waves (two workgroups -- two QPs -- per CU) or 8
+hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, double* D, double* Linv, double* W,
+                                     int* info, hipStream_t st, const BatchStrides& bs) {
+  if (snw == 4)
+    hipLaunchKernelGGL(ldlt_small_kernel<4>, dim3(bs.B), dim3(64 * 4), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
+                       bs.sD, bs.sL, bs.sW);
+  else
+    hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
+                       bs.sD, bs.sL, bs.sW);
+  return hipGetLastError();
+}
+
 }  // namespace ipmz

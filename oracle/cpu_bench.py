@@ -7,8 +7,9 @@ after its timed GPU region (the child never touches the GPU).  The LDL^T is
 the reference's own loop order (LinearSolvers.cpp:14-42, serial), not the
 blocked form the parity tests use.
 
-    python oracle/cpu_bench.py step  N_n N_m N_p SCALE     one Newton step at dims/SCALE, pinned to one core,
-                                                          extrapolated per phase to the full dims (N^3 / N^2)
+    python oracle/cpu_bench.py step  N_n N_m N_p SCALE [SLOT]  one Newton step at dims/SCALE, pinned to one core
+                                                          (the SLOT-th available one), extrapolated per phase to
+                                                          the full dims (N^3 / N^2); SCALE 1 = measured as is
     python oracle/cpu_bench.py batch n m SECONDS WORKERS   QP-steps/s of WORKERS single-core processes (one QP
                                                           per process at a time, 3 steps each, seeds disjoint)
 Prints one JSON object.
@@ -43,9 +44,10 @@ def pin(cpu):
     os.environ["OMP_NUM_THREADS"] = "1"
 
 
-def step(n, m, p, scale):
+def step(n, m, p, scale, slot=0):
     model, nproc, avail = cpu_info()
-    pin(avail[0])
+    cpu = avail[slot % len(avail)]
+    pin(cpu)
     import oracle
     oracle.set_serial_ldlt(True)  # the reference's loop order
     ns, ms, ps = n // scale, m // scale, p // scale
@@ -57,11 +59,15 @@ def step(n, m, p, scale):
     r = Nf / Ns
     head = wall - (ph["assemble"] + ph["ldlt"] + ph["rest"])  # objective / res / mu
     t_full = ph["ldlt"] * r ** 3 + (ph["assemble"] + ph["rest"] + head) * r ** 2
-    return {"value": 1.0 / t_full, "unit": "steps/s", "cores": 1, "kind": "port",
-            "sample": (f"1 Newton step of the oracle (reference loop order, serial LDL^T) at n={ns}, m={ms}, p={ps} "
-                       f"(N={Ns}) took {wall:.2f} s (LDL^T {ph['ldlt']:.2f} s); extrapolated to N={Nf} as "
-                       f"LDL^T x{r ** 3:.0f} (N^3) + rest x{r ** 2:.0f} (N^2) = {t_full:.1f} s/step"),
-            "cpu_model": model, "nproc": nproc, "cpus_available": len(avail), "pinned_cpu": avail[0]}
+    if scale == 1:
+        sample = (f"1 full-size Newton step of the oracle (reference loop order, serial LDL^T) at n={n}, m={m}, "
+                  f"p={p} (N={Nf}): {wall:.1f} s (LDL^T {ph['ldlt']:.1f} s), measured, not extrapolated")
+    else:
+        sample = (f"1 Newton step of the oracle (reference loop order, serial LDL^T) at n={ns}, m={ms}, p={ps} "
+                  f"(N={Ns}) took {wall:.2f} s (LDL^T {ph['ldlt']:.2f} s); extrapolated to N={Nf} as "
+                  f"LDL^T x{r ** 3:.0f} (N^3) + rest x{r ** 2:.0f} (N^2) = {t_full:.1f} s/step")
+    return {"value": 1.0 / t_full, "unit": "steps/s", "cores": 1, "kind": "port", "sample": sample,
+            "cpu_model": model, "nproc": nproc, "cpus_available": len(avail), "pinned_cpu": cpu}
 
 
 def _batch_worker(args):
@@ -101,7 +107,7 @@ def batch(n, m, seconds, workers):
 def main():
     mode = sys.argv[1]
     if mode == "step":
-        out = step(*(int(a) for a in sys.argv[2:6]))
+        out = step(*(int(a) for a in sys.argv[2:7]))
     elif mode == "batch":
         out = batch(int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4]), int(sys.argv[5]))
     else:

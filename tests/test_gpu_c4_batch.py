@@ -64,6 +64,54 @@ def test_c4_batch1024_vs_oracle_and_golden(ctx):
             bt.set_state(i, o.vars())
 
 
+def test_c4_graph_replay_vs_eager_and_oracle(ctx):
+    """The step bench.py times: STEP_RESTART_IF_CONVERGED | STEP_GRAPH on a
+    B = 1024 Batch, captured once and replayed for 12 steps -- past the
+    step where every QP has converged (7 steps) and restarts from its initial
+    iterate inside the replayed graph.  Against the eager batch stepped with
+    the same flags minus STEP_GRAPH (bitwise: scalars and every QP's iterate
+    and both directions) and a strided QP sample against the oracle from the
+    same pre-step iterate (the initial one after a restart), Δx < 1e-10."""
+    steps = 12
+    gb = I.Batch(N_, M_, 0, B_, ctx)
+    eb = I.Batch(N_, M_, 0, B_, ctx)
+    gb.generate(0)
+    eb.generate(0)
+    sample = list(range(0, B_, 32)) + [B_ - 1]
+    orcs = {i: oracle.OracleQP(oracle.gen_qp(N_, M_, 0, i)) for i in sample}
+    init = {i: o.vars() for i, o in orcs.items()}
+    restarts = 0
+    for it in range(steps):
+        pre = {i: gb.state(i, 0) for i in sample}
+        conv = gb.batch_scalars()[:, I.SC["converged"]].copy()
+        gb.step(I.STEP_RESTART_IF_CONVERGED | I.STEP_GRAPH)
+        eb.step(I.STEP_RESTART_IF_CONVERGED)
+        if it >= 1:
+            assert gb.last_step_graph(), it  # the replayed graph, not an eager fallback
+        sg, se = gb.batch_scalars(), eb.batch_scalars()
+        assert np.array_equal(sg, se), it
+        for i in range(B_):
+            for w in range(3):
+                assert np.array_equal(gb.state(i, w), eb.state(i, w)), (it, i, w)
+        for i, o in orcs.items():
+            if conv[i]:
+                o.set_vars(init[i])
+                restarts += 1
+            else:
+                o.set_vars(pre[i])
+            done, rec = o.iterate()
+            assert done == 0, (it, i)
+            for which, ref in ((1, o.daff()), (2, o.dir())):
+                got = gb.state(i, which)
+                assert np.abs(got[:N_] - ref[:N_]).max() < DX_TOL, (it, i, which)
+                assert np.abs(got - ref).max() < 1e-9 * max(1.0, np.abs(ref).max()), (it, i, which)
+            for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+                assert abs(sg[i, I.SC[k]] - rec[k]) <= 1e-9 * max(1.0, abs(rec[k])), (it, i, k)
+    assert restarts >= len(sample), restarts  # every sampled QP restarted inside the replay
+    gb.close()
+    eb.close()
+
+
 def _run(ctx, B, seed0, steps, kernel=None):
     bt = I.Batch(N_, M_, 0, B, ctx)
     if kernel is not None:

@@ -41,6 +41,7 @@ def _pair(ctx, n, m, p, mode):
     (1024, 256, 128, "augmented", True),    # on torch's (legacy default) stream: captured on the context's own
     (2048, 512, 0, "normal", False),        # C2's shape: the pipelined normal-equations factor, 5 panels of 512
     (1536, 0, 0, "mixed", False),           # fp32 factor + fp64 refinement, 6 panels
+    (5120, 0, 0, "mixed", False),           # 10 panels of 512: the 128 x 128 f32 trailing tiles too
 ])
 def test_captured_forked_step_equals_eager(n, m, p, mode, torch_stream):
     ctx = I.Context(0, stream=torch.cuda.current_stream().cuda_stream) if torch_stream else I.Context(0)
@@ -56,6 +57,41 @@ def test_captured_forked_step_equals_eager(n, m, p, mode, torch_stream):
             ctx.sync()
             assert graph.last_step_graph() == 1 and eager.last_step_graph() == 0
             for which in (1, 2):  # affine and corrector directions
+                assert np.array_equal(eager._state(which), graph._state(which)), (it, which)
+            assert np.array_equal(eager.vars(), graph.vars()), it
+        eager.close()
+        graph.close()
+    finally:
+        ctx.close()
+
+
+@pytest.mark.parametrize("n,m,p,mode", [
+    (1024, 256, 128, "augmented"),  # N = 1408, 6 outer panels: the forked factor
+    (1536, 0, 0, "mixed"),          # the mixed solve enqueues every refinement pass inside a capture
+])
+def test_step_inside_callers_torch_graph_capture(n, m, p, mode):
+    """A caller that captures step() itself (torch.cuda.graph on the
+    context's stream): the step goes into the caller's capture on that
+    stream -- no hop to the context's own stream, no host wait -- and each
+    replay equals an eager step bit for bit."""
+    s = torch.cuda.Stream()
+    ctx = I.Context(0, stream=s.cuda_stream)
+    try:
+        eager, graph = _pair(ctx, n, m, p, mode)
+        flags = I.STEP_RESTART_IF_CONVERGED
+        eager.step(flags)  # first steps eager: workspaces exist before the capture
+        graph.step(flags)
+        ctx.sync()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
+            graph.step(flags)
+        for it in range(3):
+            eager.step(flags)
+            with torch.cuda.stream(s):
+                g.replay()
+            s.synchronize()
+            ctx.sync()
+            for which in (1, 2):
                 assert np.array_equal(eager._state(which), graph._state(which)), (it, which)
             assert np.array_equal(eager.vars(), graph.vars()), it
         eager.close()

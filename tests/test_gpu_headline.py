@@ -102,6 +102,35 @@ def test_c5_mixed_newton_step_vs_oracle(ctx):
           f"{s['ir_iters_aff']:.0f} / {s['ir_iters']:.0f} corrections", flush=True)
 
 
+def test_c5_mixed_bench_setting_vs_oracle(ctx):
+    """C5 at the setting bench.py times (refinement tolerance 1e-12, at most
+    20 corrections, bench.py --ir-tol default): the same parity bar as the
+    fp64 path, ||dx_gpu - dx_cpu||_inf < 1e-10, at iterate 0 and at the
+    GPU's iterate after 3 steps."""
+    n, seed = 16384, 1234
+    qp = oracle.gen_qp(n, 0, 0, seed)
+    o = oracle.OracleQP(qp)
+    g = I.Optimizer(n, 0, 0, ctx)
+    g.generate(seed)
+    g.set_mixed_precision(True, 1e-12, 20)
+    assert np.array_equal(g.vars(), o.vars())
+    for label, warm in (("C5@1e-12 iterate 0", 0), ("C5@1e-12 iterate 3", 3)):
+        for _ in range(warm):
+            g.step()
+        if warm:
+            o.set_vars(g.vars())
+        g.step()
+        done, rec = o.iterate()
+        assert done == 0
+        _check_scalars(g, rec, label)
+        _check_step(o, g, label)
+        s = g.scalars()
+        assert s["ir_ratio"] <= 1e-12 and s["ir_ratio_aff"] <= 1e-12, s
+        print(f"{label}: refinement ratio {s['ir_ratio_aff']:.2e} / {s['ir_ratio']:.2e} after "
+              f"{s['ir_iters_aff']:.0f} / {s['ir_iters']:.0f} corrections", flush=True)
+        g.set_vars(o.vars())
+
+
 def test_c2_normal_newton_steps_vs_oracle(ctx):
     """C2 (BASELINE.json configs[1]): n=2048, m=512, the normal-equations
     reduction (Cholesky of H, TRSM, SYRK, Cholesky of S as one pipelined

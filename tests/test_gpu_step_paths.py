@@ -2,10 +2,11 @@
 path it replaced on the same iterate (one Newton step of Optimizer::solve,
 Optimizer.cpp:127-219):
 
-* the fp32 trailing update (mixed precision, C5) as a halving tree of
-  strided-batched SGEMMs + one batched diagonal launch vs one rocBLAS SSYRKX
-  (debug bit 1024): the same directions to refinement tolerance, and two
-  runs of the tree bitwise equal (every element of C written by one launch);
+* the fp32 trailing and strip updates (mixed precision, C5) on the
+  32 x 32 x 2 f32 MFMA kernel (gemm32.h) vs the gemm.h engine's fp32
+  instance (debug bit 128): the same directions to refinement tolerance, and
+  two runs bitwise equal (every element of C written by one launch, in a
+  fixed k order);
 * the eager refinement loop that stops on a host-mapped stop test vs all
   max_refine + 1 passes enqueued (debug bit 512): bitwise equal (the passes
   after convergence return at once);
@@ -19,7 +20,7 @@ pytestmark = pytest.mark.gpu
 I = pytest.importorskip("ipmz_amd")
 torch = pytest.importorskip("torch")
 
-DEBUG_IR_FULL, DEBUG_SYRKX = 512, 1024
+DEBUG_F32_ENGINE, DEBUG_IR_FULL = 128, 512
 
 
 @pytest.fixture(autouse=True)
@@ -44,14 +45,14 @@ def _run(ctx, n, m, p, steps, mixed, mask=0):
     return out
 
 
-def test_halving_tree_vs_syrkx_and_determinism():
+def test_f32_mfma_kernel_vs_gemm_engine_and_determinism():
     ctx = I.Context(0)
     try:
-        n = 6144  # N = 6144, nbo 512: the trailing orders >= 4096 (5120, 4608, 4096) take the tree
-        tree = _run(ctx, n, 0, 0, 2, True)
-        tree2 = _run(ctx, n, 0, 0, 2, True)
-        syrkx = _run(ctx, n, 0, 0, 2, True, DEBUG_SYRKX)
-        for (a1, d1, v1, s1), (a2, d2, v2, _), (a3, d3, v3, s3) in zip(tree, tree2, syrkx):
+        n = 6144  # N = 6144, nbo 512: trailing orders 5120 .. 512 (both tile sizes), strips
+        mf = _run(ctx, n, 0, 0, 2, True)
+        mf2 = _run(ctx, n, 0, 0, 2, True)
+        eng = _run(ctx, n, 0, 0, 2, True, DEBUG_F32_ENGINE)
+        for (a1, d1, v1, s1), (a2, d2, v2, _), (a3, d3, v3, s3) in zip(mf, mf2, eng):
             assert np.array_equal(a1, a2) and np.array_equal(d1, d2) and np.array_equal(v1, v2)
             assert s1["ir_ratio_aff"] <= 1e-12 and s1["ir_ratio"] <= 1e-12
             assert s3["ir_ratio_aff"] <= 1e-12 and s3["ir_ratio"] <= 1e-12

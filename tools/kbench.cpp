@@ -175,6 +175,41 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (mode == "smallv") {  // kbench 320 smallv: the one-workgroup factor with 4 vs 8 waves per QP
+    for (int B : {128, 1024})
+      for (int snw : {8, 4}) {
+        double *Kb, *Db, *Lb, *Wb;
+        const int64_t sK = ld * N, sL = (int64_t)((N + 63) / 64) * 64 * 64;
+        CK(hipMalloc(&Kb, sK * B * 8));
+        CK(hipMalloc(&Db, (int64_t)N * B * 8));
+        CK(hipMalloc(&Lb, sL * B * 8));
+        CK(hipMalloc(&Wb, (int64_t)N * 64 * B * 8));
+        ipmz::BatchStrides bs;
+        bs.B = B;
+        bs.sK = sK;
+        bs.sD = N;
+        bs.sL = sL;
+        bs.sW = (int64_t)N * 64;
+        float best = 1e30f;
+        for (int rep = 0; rep < 4; ++rep) {
+          for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
+          t.start(st);
+          CK(ipmz::ldlt_factor_small_variant(snw, Kb, ld, N, Db, Lb, Wb, info, st, bs));
+          const float ms = t.stop(st);
+          if (rep) best = ms < best ? ms : best;
+        }
+        std::vector<double> hD(N);
+        CK(hipMemcpy(hD.data(), Db + (int64_t)(B - 1) * N, N * 8, hipMemcpyDeviceToHost));
+        double cs = 0;
+        for (double d : hD) cs += d;
+        std::printf("small factor N=%d B=%d waves=%d: %.1f us (D checksum of the last QP %.15e)\n", N, B, snw, best * 1e3, cs);
+        CK(hipFree(Kb));
+        CK(hipFree(Db));
+        CK(hipFree(Lb));
+        CK(hipFree(Wb));
+      }
+    return 0;
+  }
   if (mode == "gvar") {  // trailing-GEMM tile variants: kbench N gvar v1 v2 ...
     for (int a = 3; a < argc; ++a) {
       const int var = std::atoi(argv[a]);
