@@ -271,10 +271,11 @@ def run_single(I, ctx, args, world, dist, torch, workload):
             trk = load_json("profiles/pmc_traffic.json") if workload == "c3" else None
             tach = ph["trailing_flops"] / tr_s / 1e12
             roof["trailing"] = {
-                "kernel": ("trailing orders >= 4096: a halving tree of rocblas_sgemm_strided_batched levels + one "
-                           "batched gemm_nt_kernel<float,64,64> launch for the 512-wide diagonal blocks; "
-                           "gemm_nt_kernel<float,...> below (trailing update A22 -= W21 L21^T)" if mixed else
-                           "gemm_nt_kernel<double,128,128,EPI_SUB,4,4> (trailing update A22 -= W21 L21^T)"),
+                "kernel": ("sgemm_nt_kernel<128,128,...> (csrc/gemm32.h, v_mfma_f32_32x32x2_f32; trailing update "
+                           "A22 -= W21 L21^T of the fp32 factor, one launch over the lower tiles)" if mixed else
+                           "dgemm_nt_glds_kernel<128,128,4,4,8,3> (csrc/gemm64.h, LDS-DMA staging; trailing update "
+                           "A22 -= W21 L21^T; gemm_nt_kernel<double,128,128,EPI_SUB,4,4> for launches with partial "
+                           "tiles)"),
                 "achieved": tach, "peak": peak, "unit": "TFLOP/s", "frac": tach / peak,
                 "traffic": trk.get("traffic_bytes_per_launch") if trk else None,
                 "traffic_unit": "bytes/launch (rocprofv3 FETCH_SIZE x2 + WRITE_SIZE, separate --pmc passes)",

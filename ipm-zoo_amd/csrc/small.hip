@@ -95,7 +95,7 @@ __device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc
 }  // namespace
 
 template <int SNW>
-__global__ __launch_bounds__(64 * SNW) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
+__global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
                                                          double* __restrict__ D, double* __restrict__ Linv,
                                                          double* __restrict__ W, int* __restrict__ info, int64_t sK,
                                                          int64_t sD, int64_t sL, int64_t sW) {

@@ -19,7 +19,7 @@ step() {  # name timeout cmd...
 for s in ${STEPS:-smoke tests bench prof}; do
   case $s in
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
-    tests) step tests 900 python -m pytest tests -m gpu -v --timeout=300 --timeout-method thread -p no:cacheprovider ;;
+    tests) step tests 1000 python -u -m pytest tests -m gpu -v --timeout=400 --timeout-method thread -p no:cacheprovider ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_c2) step bench_c2 300 python bench.py --workload c2 ;;
     bench_c4) step bench_c4 300 python bench.py --workload c4 ;;
@@ -36,6 +36,18 @@ for s in ${STEPS:-smoke tests bench prof}; do
     pmcf_mops) step ${PMCW:-c3}_pmcf_mops 240 rocprofv3 --pmc $([ "${PMCW:-c3}" = c5 ] && echo SQ_INSTS_VALU_MFMA_MOPS_F32 || echo SQ_INSTS_VALU_MFMA_MOPS_F64) -d "$OUT/${PMCW:-c3}_pmcf_mops" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     pmcf_busy) step ${PMCW:-c3}_pmcf_busy 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d "$OUT/${PMCW:-c3}_pmcf_busy" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
+    sgemm) step sgemm 200 ipm-zoo_amd/build/sgemm_bench ${SGEMM_R:-15872} ${SGEMM_V:-} ;;
+    smallv) step smallv 100 ipm-zoo_amd/build/kbench 320 smallv ;;
+    ab64) TORCH_STREAM=1 step ab64 300 python -u tools/mask_ab.py 1024 c3 ;;
+    ab32) TORCH_STREAM=1 step ab32 300 python -u tools/mask_ab.py 128 c5 ;;
+    ab64b) TORCH_STREAM=1 step ab64b 300 python -u tools/mask_ab.py 2048 c3 ;;
+    ab64s) TORCH_STREAM=1 step ab64s 300 python -u tools/mask_ab.py 4096 c3 c2 ;;
+    ab32b) TORCH_STREAM=1 step ab32b 300 python -u tools/mask_ab.py 2048 c5 ;;
+    c2old) TORCH_STREAM=1 IPMZ_PKG_DIR=_old/ipm-zoo_amd step c2old 200 python -u tools/mask_ab.py 0 c2 c3 ;;
+    c2new) TORCH_STREAM=1 step c2new 200 python -u tools/mask_ab.py 0 c2 c3 ;;
+    dgemm) step dgemm 200 ipm-zoo_amd/build/sgemm_bench d ${DGEMM_R:-10752} ${DGEMM_V:-} ;;
+    mixedtests) step mixedtests 400 python -u -m pytest tests/test_gpu_mixed.py tests/test_gpu_step_paths.py tests/test_gpu_graph.py -v --timeout 240 --timeout-method thread -p no:cacheprovider ;;
+    newtests) step newtests 600 python -u -m pytest tests/test_gpu_headline.py tests/test_gpu_c4_batch.py -v --timeout 400 --timeout-method thread -p no:cacheprovider ;;
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;
     counters) step counters 120 rocprofv3 -L ;;
