@@ -755,6 +755,10 @@ struct ipmz_qp {
   // factor storage
   double *K = nullptr, *D = nullptr;
   int64_t sK = 0, sD = 0, sb = 0;
+  // batches of small systems (fused phases, LDL^T): the assembled KKT kept
+  // across steps (off-diagonal part written once per data load, the diagonal
+  // every step); the small factor reads it and writes L to K (strides sK)
+  double* K0 = nullptr;
   char* ws = nullptr;      // B == 1: ws_layout(N) ; B > 1: see batch_ws
   int64_t ws_bytes = 0;
   double *bLinv = nullptr, *bW = nullptr;  // batched factor workspace (B > 1)
@@ -875,6 +879,7 @@ int solve_batch(ipmz_qp* s, hipStream_t st, int which) {
 }
 
 // info_reset: the caller already reset the batched factor's info word
+bool uses_k0(const ipmz_qp* s);
 int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   if (s->eqnone) {  // zero diagonal block: symmetric_indefinite_factorization (reference kp behaviour)
     if (s->bkws) {
@@ -900,6 +905,7 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   bs.sL = s->sL;
   bs.sW = s->sW;
   bs.pflags = s->small_kernel == IPMZ_BATCH_FACTOR_ONE ? nullptr : s->pflags;
+  bs.K0 = info_reset && uses_k0(s) ? s->K0 : nullptr;  // (info_reset: the fused step, whose pre phase assembled into K0)
   if (!info_reset) HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
   HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
                              s->ctx->stream, bs));
@@ -909,6 +915,11 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
 // batches of small systems: the O(N) / O(n^2) phases as three per-QP
 // workgroup kernels (newton.hip k_fused_*)
 bool fused_phases(const ipmz_qp* s) { return s->B > 1 && s->N <= IPMZ_FUSED_NMAX; }
+// the fused step keeps the assembled matrix in K0 when the small batched
+// factor (nbi 64) consumes it; otherwise the whole matrix is assembled into K
+bool uses_k0(const ipmz_qp* s) {
+  return s->K0 && s->ctx->nbi == 64 && s->N <= IPMZ_SMALL_NMAX && !(debug_inject_mask() & IPMZ_DEBUG_NO_K0);
+}
 
 int run_step(ipmz_qp* s, int flags) {
   hipStream_t st = s->ctx->stream;
@@ -929,7 +940,7 @@ int run_step(ipmz_qp* s, int flags) {
     // phases: assemble = pre (restart, assembly, affine rhs); factor;
     // solve = the two solves; eval = mid + post
     mark(0);
-    HIP_OK(qp_fused_pre(qb, restart ? 1 : 0, s->eqnone ? nullptr : s->binfo, st));
+    HIP_OK(qp_fused_pre(qb, restart ? 1 : 0, s->eqnone ? nullptr : s->binfo, st, uses_k0(s) ? KMODE_K0_DIAG : KMODE_K));
     mark(1);
     if ((rc = factor_batch(s, nullptr, true))) return rc;
     mark(2);
@@ -993,6 +1004,7 @@ int run_step(ipmz_qp* s, int flags) {
 
 int evaluate_and_save(ipmz_qp* s) {
   hipStream_t st = s->ctx->stream;
+  if (s->K0) HIP_OK(qp_fused_pre(s->qb, 0, nullptr, st, KMODE_K0_OFFDIAG));  // the data just changed
   HIP_OK(qp_evaluate(s->qb, st));
   HIP_OK(qp_save_initial(s->qb, st));
   s->loaded = true;
@@ -1086,6 +1098,10 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   int64_t sDone;
   double* done = dev_array(s, 1, &sDone);
   s->K = dev_array(s, (int64_t)N * s->ldk, &s->sK);
+  if (B > 1 && N <= IPMZ_FUSED_NMAX && !s->eqnone) {
+    int64_t sK0 = 0;
+    s->K0 = dev_array(s, (int64_t)N * s->ldk, &sK0);
+  }
   s->D = dev_array(s, N, &s->sD);
   s->sb = sNb;
   bool ok = Q && A && C && c && lx && ux && Qx && ATl && CTl && lA && uA && Ax && d && Cx && v && r && da && di &&
@@ -1190,6 +1206,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
     q.part = part + i * sPart;
     q.tpart = tpart + i * sT;
     q.K = s->K + i * s->sK;
+    q.K0 = s->K0 ? s->K0 + i * s->sK : nullptr;
     q.done = reinterpret_cast<unsigned*>(done + i * sDone);
   }
   void* dqp = nullptr;

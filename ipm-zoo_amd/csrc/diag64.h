@@ -146,10 +146,13 @@ using namespace diag64;
 struct NoHook {
   __device__ void operator()() const {}
 };
+// Ksrc (optional): read the block from there instead of K (the batched
+// factor's first touch of the assembled KKT, small.hip); L is written to K.
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
-                                            double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB()) {
+                                            double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
+                                            const TS* __restrict__ Ksrc = nullptr) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
@@ -167,7 +170,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     for (int q = 0; q < NQ; ++q) {
       const int rr = (tid >> 6) + NW * q, cc = tid & 63;
       const int r2 = rr < b ? rr : 0, c2 = cc <= r2 ? cc : 0;
-      const TS* src = &K[(int64_t)(k0 + r2) * ld + k0 + c2];
+      const TS* src = &(Ksrc ? Ksrc : K)[(int64_t)(k0 + r2) * ld + k0 + c2];
       t[q] = (double)(LSC ? ld_sc1(src) : *src);
     }
 #pragma unroll

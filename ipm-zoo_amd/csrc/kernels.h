@@ -25,11 +25,13 @@ namespace ipmz {
 // 256 = the fp32 factor's look-ahead strip on the trailing stream before the trailing update (no fourth stream),
 // 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test),
 // 1024 = the fp64 trailing update on gemm.h's register-staged kernel instead of gemm64.h's LDS-DMA one (A/B),
-// 2048 = the alternative GEMM tiles of ldlt.hip sgemm_sub / dgemm_sub, 4096 = the fp64 strips on gemm.h (A/B)
+// 2048 = the alternative GEMM tiles of ldlt.hip sgemm_sub / dgemm_sub, 4096 = the fp64 strips on gemm.h (A/B),
+// 8192 = batches assemble the whole KKT into K every step (not the kept K0) (A/B)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
-       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_VARIANT_B = 2048, IPMZ_DEBUG_OLD_STRIPS = 4096 };
+       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_VARIANT_B = 2048, IPMZ_DEBUG_OLD_STRIPS = 4096,
+       IPMZ_DEBUG_NO_K0 = 8192 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -59,6 +61,11 @@ struct BatchStrides {
   // small batched factor: B * IPMZ_PAIR_FLAGS + 1 words for the two-workgroup
   // factor (B <= #CU; W then needs 2 x N x 64 per QP), nullptr = one workgroup
   unsigned* pflags = nullptr;
+  // small batched factor: the assembled KKT's first touch (block column 0's
+  // steps) read from K0 (strides sK) instead of K -- the off-diagonal part
+  // kept across Newton steps, only its diagonal rewritten per step; nullptr =
+  // K holds the assembled matrix
+  const double* K0 = nullptr;
 };
 #define IPMZ_PAIR_FLAGS 32  // per QP: LW[16], DONE[16] (N <= IPMZ_SMALL_NMAX)
 // the batched factor of order N runs two workgroups per QP (given flags)
@@ -276,6 +283,7 @@ struct QPDev {
   double* part;   // reduction partials
   double* tpart;  // transposed-GEMV partials
   double* K;      // KKT / factor (N x ldk)
+  double* K0;     // batches of small systems: the assembled KKT kept across steps (the factor reads it, writes L to K); nullptr: none
   double *v0, *r0, *scal0;  // initial iterate snapshot (benchmark restarts)
   unsigned* done;           // fused evaluation: arrival counter of the QP's workgroups (0 between launches)
 };
@@ -310,7 +318,11 @@ hipError_t qp_batch_summary(const QPBatch& qb, double* out, hipStream_t st);
 // mid = predictor back-substitution .. corrector rhs, post = corrector
 // back-substitution + update + evaluation.  N <= IPMZ_FUSED_NMAX.
 #define IPMZ_FUSED_NMAX 1024
-hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st);
+// kmode: 0 = the whole lower triangle into K; 1 = the diagonal into K0 (its
+// off-diagonal part is already there); 2 = only the off-diagonal part into
+// K0 (once per data load; no restart, no rhs)
+enum { KMODE_K = 0, KMODE_K0_DIAG = 1, KMODE_K0_OFFDIAG = 2 };
+hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st, int kmode = KMODE_K);
 hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st);
 hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st);  // (+ the evaluation)
 

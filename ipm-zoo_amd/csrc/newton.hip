@@ -982,10 +982,13 @@ constexpr int FT = 512;  // 8 waves
 // QP (blockIdx.y): the off-diagonal copy (independent of the iterate) is
 // split over all of them; workgroup 0 also restarts, writes the diagonal and
 // the rhs (which read the iterate) in that order.
-__global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, int restart, int* info) {
+// kmode (kernels.h KMODE_*): where the matrix goes -- K whole, or the kept
+// K0 (its off-diagonal part once per data load, its diagonal every step)
+__global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, int restart, int* info, int kmode) {
   const QPDev& q = qs[blockIdx.y];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool lead = blockIdx.x == 0;
+  const bool lead = blockIdx.x == 0 && kmode != KMODE_K0_OFFDIAG;
+  double* const KT = kmode == KMODE_K ? q.K : q.K0;
   if (info && lead && blockIdx.y == 0 && tid == 0) *info = 0x7f7f7f7f;  // the factor's first-failure word
   if (lead && restart && q.scal[SC_CONVERGED] != 0.0) {
     for (int64_t t = tid; t < q.state_len; t += FT) {
@@ -1004,7 +1007,7 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
   // pair per lane), eight units per wave in flight: one workgroup moves the
   // QP's ~0.8 MB only with many loads outstanding
   const int N = q.N, n = q.n, m = q.m, nm = q.n + q.mk;
-  const int nch = (N + 127) / 128, units = N * nch;
+  const int nch = (N + 127) / 128, units = kmode == KMODE_K0_DIAG ? 0 : N * nch;
   for (int u0 = (blockIdx.x * (FT / 64) + wave) * 8; u0 < units; u0 += gridDim.x * (FT / 64) * 8) {
     double v0[8], v1[8];
 #pragma unroll
@@ -1031,7 +1034,7 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
     for (int k = 0; k < 8; ++k) {
       const int u = u0 + k, i = u / nch, j = (u % nch) * 128 + 2 * lane;
       if (u < units) {
-        double* Kr = q.K + (int64_t)i * q.ldk;
+        double* Kr = KT + (int64_t)i * q.ldk;
         if (j + 1 < i) *reinterpret_cast<double2*>(Kr + j) = make_double2(v0[k], v1[k]);  // ldk even
         else if (j < i) Kr[j] = v0[k];
       }
@@ -1039,7 +1042,7 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
   }
   if (!lead) return;
   for (int i = tid; i < N; i += FT) {
-    double* Kd = q.K + (int64_t)i * q.ldk + i;
+    double* Kd = KT + (int64_t)i * q.ldk + i;
     if (i < n) *Kd = kkt_xx(q, i, q.Q[(int64_t)i * q.ldn + i]);
     else if (q.naive && i < n + m) *Kd = -(ipmz_inv(q.v[LG][i - n]) * q.v[G][i - n]);
     else if (q.naive && i < nm) *Kd = -(ipmz_inv(q.v[LH][i - n - m]) * q.v[H][i - n - m]);
@@ -1200,8 +1203,12 @@ static int fused_split(int B) {
   return s < 1 ? 1 : (s > 8 ? 8 : s);
 }
 
-hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st) {
-  hipLaunchKernelGGL(k_fused_pre, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d, restart, info);
+hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st, int kmode) {
+  if (kmode != KMODE_K && !qb.h.K0) return hipErrorInvalidValue;
+  // the diagonal-only mode has no copy to spread: one workgroup per QP
+  const int split = kmode == KMODE_K0_DIAG ? 1 : fused_split(qb.B);
+  hipLaunchKernelGGL(k_fused_pre, dim3(split, qb.B), dim3(FT), 0, st, qb.d, kmode == KMODE_K0_OFFDIAG ? 0 : restart,
+                     kmode == KMODE_K0_OFFDIAG ? nullptr : info, kmode);
   return hipGetLastError();
 }
 hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st) {

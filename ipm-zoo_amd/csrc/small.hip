@@ -98,11 +98,13 @@ template <int SNW>
 __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) void ldlt_small_kernel(double* __restrict__ K, int64_t ld, int N,
                                                          double* __restrict__ D, double* __restrict__ Linv,
                                                          double* __restrict__ W, int* __restrict__ info, int64_t sK,
-                                                         int64_t sD, int64_t sL, int64_t sW) {
+                                                         int64_t sD, int64_t sL, int64_t sW,
+                                                         const double* __restrict__ K0) {
   constexpr int SFR = Cfg<SNW>::SFR, SNN = Cfg<SNW>::SNN;
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   const int64_t qp = blockIdx.x;
   K += qp * sK;
+  if (K0) K0 += qp * sK;  // the assembled matrix: block column 0's steps read it (first touch), L goes to K
   D += qp * sD;
   Linv += qp * sL;
   W += qp * sW;  // N x 64 row-major: the current block column's W = L D
@@ -114,15 +116,16 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
   auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
   for (int J = 0; J < nblk; ++J) {
     const int J0 = 64 * J;
+    const double* KS = (J == 0 && K0) ? K0 : K;  // where this step's not yet updated tiles are read
     diag64_body<false, false, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
-                                                  smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
+                                                  smem + 64 * DS, smem + 2 * 64 * DS, nullptr, NoHook(), KS);
     if (J == nblk - 1) break;
     __syncthreads();  // diag64_body's L, D, L^{-1} stores are visible to the workgroup
     // ---- TRSM of the chunks below (block J is full: J0 + 64 < N), with
     // L_JJ^{-1} and the pivots straight from diag64_body's LDS images (X in
     // Bs, lower part; dsh) -- no global round trip on the chain
     double v[SFR], u[SFR];
-    tile_fetch<SNW>(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    tile_fetch<SNW>(KS + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
     const double* dsh = smem + 2 * 64 * DS;
     double rd[SNN];
 #pragma unroll
@@ -131,7 +134,7 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
       const int rows = nrows(c);
       tile_put<SNW>(As, rows, v);
       __syncthreads();
-      if (c + 1 < nblk) tile_fetch<SNW>(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
+      if (c + 1 < nblk) tile_fetch<SNW>(KS + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
       acc_t acc[SNN];
 #pragma unroll
       for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
@@ -165,8 +168,10 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
       acc_t acc[SNN], cv[SNN];
       const bool diag = q == c;
       // this lane's elements: rows r0 + (lane >> 4) + 4g, columns 16 (n0 + n) + (lane & 15)
-      double* Ct = K + (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
-      const double* Ct0 = K + (int64_t)(64 * c) * ld + 64 * q;
+      const int64_t toff = (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
+      double* Ct = K + toff;
+      const double* Cs = KS + toff;  // (block column 0's step: the assembled matrix)
+      const double* Ct0 = KS + (int64_t)(64 * c) * ld + 64 * q;
       const int64_t ld4 = 4 * ld;
 #pragma unroll
       for (int n = 0; n < SNN; ++n) {
@@ -176,7 +181,7 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
         for (int g = 0; g < 4; ++g) {
           const int row = r0 + MF::row(lane, g);
           const bool in = row < rows && (!diag || col <= row);
-          cv[n][g] = *(in ? Ct + g * ld4 + 16 * n : Ct0);  // (out-of-tile lanes: a valid dummy address)
+          cv[n][g] = *(in ? Cs + g * ld4 + 16 * n : Ct0);  // (out-of-tile lanes: a valid dummy address)
         }
       }
       __syncthreads();
@@ -232,13 +237,15 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
                                                               double* __restrict__ D, double* __restrict__ Linv,
                                                               double* __restrict__ W, int* __restrict__ info,
                                                               int64_t sK, int64_t sD, int64_t sL, int64_t sW,
-                                                              unsigned* __restrict__ flags, unsigned* __restrict__ err) {
+                                                              unsigned* __restrict__ flags, unsigned* __restrict__ err,
+                                                              const double* __restrict__ K0) {
   constexpr int SFR = Cfg<SNW>::SFR, SNN = Cfg<SNW>::SNN;
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
   __shared__ unsigned sh_ok;
   const int64_t qp = blockIdx.x >> 1;
   const int role = blockIdx.x & 1;
   K += qp * sK;
+  if (K0) K0 += qp * sK;  // block column 0's steps read the assembled matrix (not written by this launch)
   D += qp * sD;
   Linv += qp * sL;
   W += qp * sW;  // two N x 64 row-major buffers (parity of J): W = L D of block column J
@@ -268,7 +275,9 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
       tile_put<SNW>(Bs, nrows(q), u);
       acc_t acc[SNN], cv[SNN];
       const bool diag = q == c;
-      double* Ct = K + (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
+      const int64_t toff = (int64_t)(64 * c + r0 + (lane >> 4)) * ld + 64 * q + 16 * n0 + (lane & 15);
+      double* Ct = K + toff;
+      const double* Cs = ((J == 0 && K0) ? K0 : K) + toff;  // block column 0's step: the assembled matrix
       const double* Ct0 = K + (int64_t)(64 * c) * ld + 64 * q;
       const int64_t ld4 = 4 * ld;
 #pragma unroll
@@ -279,7 +288,7 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
         for (int g = 0; g < 4; ++g) {
           const int row = r0 + MF::row(lane, g);
           const bool in = row < rows && (!diag || col <= row);
-          cv[n][g] = ld_sc1(in ? Ct + g * ld4 + 16 * n : Ct0);
+          cv[n][g] = ld_sc1(in ? Cs + g * ld4 + 16 * n : Ct0);
         }
       }
       __syncthreads();
@@ -319,15 +328,16 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
   }
   for (int J = 0; J < nblk; ++J) {
     const int J0 = 64 * J;
+    const double* KS = (J == 0 && K0) ? K0 : K;  // where this step's not yet updated tiles are read
     // block J was last updated by this workgroup (column J+1 of step J-1) or
     // before the DONE[J-2] wait of step J-1 (agent-scope loads: LSC)
     diag64_body<false, true, double, false, SNW>(K, ld, J0, nrows(J), D, Linv + (int64_t)J * 64 * 64, info, smem,
-                                                 smem + 64 * DS, smem + 2 * 64 * DS, nullptr);
+                                                 smem + 64 * DS, smem + 2 * 64 * DS, nullptr, NoHook(), KS);
     if (J == nblk - 1) break;
     __syncthreads();
     // ---- TRSM of every chunk below, published for role 1
     double v[SFR];
-    tile_fetch_sc<SNW>(K + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
+    tile_fetch_sc<SNW>(KS + (int64_t)(J0 + 64) * ld + J0, ld, nrows(J + 1), v);
     const double* dsh = smem + 2 * 64 * DS;
     double* Wb = Wj(J);
     double rd[SNN];
@@ -337,7 +347,7 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
       const int rows = nrows(c);
       tile_put<SNW>(As, rows, v);
       __syncthreads();
-      if (c + 1 < nblk) tile_fetch_sc<SNW>(K + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
+      if (c + 1 < nblk) tile_fetch_sc<SNW>(KS + (int64_t)(64 * (c + 1)) * ld + J0, ld, nrows(c + 1), v);
       acc_t acc[SNN];
 #pragma unroll
       for (int n = 0; n < SNN; ++n) acc[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
@@ -376,13 +386,13 @@ hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, do
     hipError_t e = hipMemsetAsync(bs.pflags, 0, ((size_t)bs.B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ldlt_small_pair_kernel<8>, dim3(2 * bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info,
-                       bs.sK, bs.sD, bs.sL, bs.sW, bs.pflags, bs.pflags + (size_t)bs.B * IPMZ_PAIR_FLAGS);
+                       bs.sK, bs.sD, bs.sL, bs.sW, bs.pflags, bs.pflags + (size_t)bs.B * IPMZ_PAIR_FLAGS, bs.K0);
     return hipGetLastError();
   }
   // 8 waves (two per SIMD) also when the batch leaves a CU per QP: 16 waves
   // measured slower (N = 320, B = 128: 249 vs 190 us)
   hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
-                     bs.sL, bs.sW);
+                     bs.sL, bs.sW, bs.K0);
   return hipGetLastError();
 }
 
@@ -392,10 +402,10 @@ hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, doub
                                      int* info, hipStream_t st, const BatchStrides& bs) {
   if (snw == 4)
     hipLaunchKernelGGL(ldlt_small_kernel<4>, dim3(bs.B), dim3(64 * 4), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
-                       bs.sD, bs.sL, bs.sW);
+                       bs.sD, bs.sL, bs.sW, bs.K0);
   else
     hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
-                       bs.sD, bs.sL, bs.sW);
+                       bs.sD, bs.sL, bs.sW, bs.K0);
   return hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
-"""C4 batches (n = 256, m = 64): the fused step with the KKT's off-diagonal part
-read by the factor from the problem data (default) vs copied into K first
-(debug bit 256): QP-steps/s at B = 1024 and 128, and the phase split."""
+"""C4 batches (n = 256, m = 64): A/B of a debug bit on the fused step (default
+8192: the whole KKT assembled into K every step instead of the kept K0):
+QP-steps/s at B = 1024 and 128, and the phase split.
+    python tools/c4_ab.py [MASK]"""
 import os, sys, time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "ipm-zoo_amd"))
@@ -11,7 +12,8 @@ torch.cuda.set_device(0)
 torch.zeros(1, device="cuda")
 ctx = I.Context(0)
 for B in (1024, 128):
-    for mask in (0, 256, 0, 256):
+    MASK = int(sys.argv[1]) if len(sys.argv) > 1 else 8192
+    for mask in (0, MASK, 0, MASK):
         I.debug_inject(mask)
         b = I.Batch(256, 64, 0, B, ctx)
         b.generate(1)
