@@ -64,13 +64,19 @@ def cpu_start(*args):
                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
 
 
-def cpu_finish(proc):
-    try:
-        out, err = proc.communicate(timeout=900)
-    except subprocess.TimeoutExpired:
-        proc.kill()
-        proc.communicate()
-        return {"error": "timed out after 900 s"}
+def cpu_finish(proc, name=""):
+    t0 = time.perf_counter()
+    while True:  # a progress line on stderr every 30 s (stdout carries only the JSON line)
+        try:
+            out, err = proc.communicate(timeout=30)
+            break
+        except subprocess.TimeoutExpired:
+            el = time.perf_counter() - t0
+            if el > 900:
+                proc.kill()
+                proc.communicate()
+                return {"error": "timed out after 900 s"}
+            print(f"[bench] CPU baseline {name}: running ({el:.0f} s)", file=sys.stderr, flush=True)
     if proc.returncode != 0:
         return {"error": err[-400:]}
     return json.loads(out.strip().splitlines()[-1])
@@ -88,11 +94,13 @@ def cpu_baselines(names):
         else:
             procs[w] = cpu_start("step", wl["n"], wl["m"], wl["p"], wl.get("sample_scale", 4), slot)
         slot += 1
-    out = {w: cpu_finish(p) for w, p in procs.items()}
+    print(f"[bench] CPU baselines {', '.join(names)} on the host cores (a full-size C3 step takes ~3 min)",
+          file=sys.stderr, flush=True)
+    out = {w: cpu_finish(p, w) for w, p in procs.items()}
     for w in names:
         wl = WORKLOADS[w]
         if wl.get("batch"):
-            out[w]["all_cores"] = cpu_finish(cpu_start("batch", wl["n"], wl["m"], 8, 16))
+            out[w]["all_cores"] = cpu_finish(cpu_start("batch", wl["n"], wl["m"], 8, 16), w + " (16 cores)")
     return out
 
 

@@ -27,9 +27,9 @@ import json
 import sys
 from collections import defaultdict
 
-FACTOR_KERNELS = ("gemm_nt_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel",
+FACTOR_KERNELS = ("gemm_nt_kernel", "gemm_nt_glds_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel",
                   "ldlt_small_kernel", "ldlt_small_pair_kernel",  # (these two: C4's batched factor)
-                  "sgemm_nt_kernel")  # C5's fp32 trailing / strip updates (gemm32.h)
+                  )
 
 
 def load(d):

@@ -21,8 +21,8 @@ import json
 import math
 import sys
 
-KERNEL = "gemm_nt_kernel<double, 128, 128, 0, 4, 4, 6>"
-NBO = int(__import__("os").environ.get("IPMZ_PMC_NBO", 384))  # the bench's outer panel width (C3: 384)
+KERNEL = "dgemm_nt_glds_kernel<128, 128, 4, 4, 8, 3, 8, 0>"  # C3's trailing update (gemm64.h)
+NBO = int(__import__("os").environ.get("IPMZ_PMC_NBO", 512))  # the bench's outer panel width (C3: 512)
 
 
 def rows(d):
