@@ -293,30 +293,28 @@ static void launch_diag64(int B, hipStream_t st, float* K, int64_t ld, int j0, i
 // engine; so does debug bit IPMZ_DEBUG_F32_ENGINE (A/B).
 static bool sgemm_sub(GemmArgsT<float>& g, bool square_lower, hipStream_t st, hipError_t& e) {
   if (!sgemm_aligned(g) || (debug_inject_mask() & IPMZ_DEBUG_F32_ENGINE)) return false;
-  const bool vb = debug_inject_mask() & IPMZ_DEBUG_VARIANT_B;  // (experiment: the alternative tiles)
+  // (profiles/r04_s2: the LDS-DMA tiles against the register-staged ones in
+  // the step, C5 44.7 vs 42.7 steps/s)
   if (square_lower) {
     if (g.M <= IPMZ_TRAIL_SMALL_M) e = launch_sgemm<64, 64, 2, 2, 32, 4>(g, st);
-    else if (vb) e = launch_sgemm<128, 128, 2, 2, 16, 4>(g, st);
     else e = launch_sgemm<128, 128, 2, 2, 16, 2, EPI_SUB, 3, true>(g, st);
     return true;
   }
   if (g.M <= 4096) e = launch_sgemm<64, 64, 2, 2, 32, 4, EPI_SUB_STRIP>(g, st);
-  else if (vb) e = launch_sgemm<128, 128, 2, 2, 32, 2, EPI_SUB_STRIP>(g, st);
   else e = launch_sgemm<128, 128, 2, 4, 16, 4, EPI_SUB_STRIP, 2, true>(g, st);
   return true;
 }
 
 // fp64 updates with LDS-DMA staging (gemm64.h) where every tile is full:
 // false -- not launched (partial tiles, debug bit IPMZ_DEBUG_F64_ENGINE): the
-// caller takes gemm.h's kernel
+// caller takes gemm.h's kernel.  In the step: C3 70.7 -> 74.0 steps/s, the
+// strips' share ~1.5 % (profiles/r04_s2/ab64*.log)
 static bool dgemm_sub(GemmArgsT<double>& g, bool square_lower, hipStream_t st, hipError_t& e) {
   if (debug_inject_mask() & IPMZ_DEBUG_F64_ENGINE) return false;
-  const bool vb = debug_inject_mask() & IPMZ_DEBUG_VARIANT_B;
   if (square_lower) {
     if (g.M <= IPMZ_TRAIL_SMALL_M) return false;
-    return vb ? launch_dgemm_glds<128, 128, 2, 4, 16, 2, 4>(g, st, e) : launch_dgemm_glds<128, 128, 4, 4, 8, 3, 8>(g, st, e);
+    return launch_dgemm_glds<128, 128, 4, 4, 8, 3, 8>(g, st, e);
   }
-  if (debug_inject_mask() & IPMZ_DEBUG_OLD_STRIPS) return false;
   if (g.M <= 4096) return launch_dgemm_glds<64, 64, 2, 2, 8, 3, 8, EPI_SUB_STRIP>(g, st, e);
   return launch_dgemm_glds<64, 128, 2, 2, 8, 3, 4, EPI_SUB_STRIP>(g, st, e);
 }

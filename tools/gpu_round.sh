@@ -40,9 +40,6 @@ for s in ${STEPS:-smoke tests bench prof}; do
     smallv) step smallv 100 ipm-zoo_amd/build/kbench 320 smallv ;;
     ab64) TORCH_STREAM=1 step ab64 300 python -u tools/mask_ab.py 1024 c3 ;;
     ab32) TORCH_STREAM=1 step ab32 300 python -u tools/mask_ab.py 128 c5 ;;
-    ab64b) TORCH_STREAM=1 step ab64b 300 python -u tools/mask_ab.py 2048 c3 ;;
-    ab64s) TORCH_STREAM=1 step ab64s 300 python -u tools/mask_ab.py 4096 c3 c2 ;;
-    ab32b) TORCH_STREAM=1 step ab32b 300 python -u tools/mask_ab.py 2048 c5 ;;
     c4ab) step c4ab 300 python -u tools/c4_ab.py 8192 ;;
     batchtests) step batchtests 600 python -u -m pytest tests/test_gpu_batch.py tests/test_gpu_c4_batch.py tests/test_gpu_formulations.py tests/test_gpu_dist.py -v --timeout 300 --timeout-method thread -p no:cacheprovider ;;
     c2old) TORCH_STREAM=1 IPMZ_PKG_DIR=_old/ipm-zoo_amd step c2old 200 python -u tools/mask_ab.py 0 c2 c3 ;;
