@@ -210,8 +210,10 @@ __global__ __launch_bounds__(64 * WGM * WGN) __attribute__((amdgpu_waves_per_eu(
 }
 
 // full tiles only; false: not launched (the caller takes gemm.h's kernel)
+// lds_pad: extra (dynamic, unused) LDS bytes per workgroup -- caps the
+// workgroups per CU by LDS (experiment: room for a panel workgroup beside one)
 template <int BM, int BN, int WGM, int WGN, int BK, int NST, int WPE, int EPI = EPI_SUB>
-static bool launch_dgemm_glds(GemmArgsT<double> g, hipStream_t st, hipError_t& e) {
+static bool launch_dgemm_glds(GemmArgsT<double> g, hipStream_t st, hipError_t& e, unsigned lds_pad = 0) {
   if (g.M % BM || g.N % BN || g.Kd % BK || g.Kd == 0 || g.M == 0 || g.N == 0) return false;
   if (((reinterpret_cast<uintptr_t>(g.A) | reinterpret_cast<uintptr_t>(g.B)) & 15) || (g.lda | g.ldb) & 1) return false;
   g.ntm = g.M / BM;
@@ -222,7 +224,7 @@ static bool launch_dgemm_glds(GemmArgsT<double> g, hipStream_t st, hipError_t& e
     else g.lower = 1;
   }
   hipLaunchKernelGGL((dgemm_nt_glds_kernel<BM, BN, WGM, WGN, BK, NST, WPE, EPI>), dim3((unsigned)nblk),
-                     dim3(64 * WGM * WGN), 0, st, g);
+                     dim3(64 * WGM * WGN), lds_pad, st, g);
   e = hipGetLastError();
   return true;
 }
