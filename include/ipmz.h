@@ -346,15 +346,19 @@ int ipmz_batch_copy_scalars(ipmz_qp* qp, double* dst_device);
 int ipmz_batch_summary(ipmz_qp* qp, double* dst_device);
 /* Step until every QP converged (converged QPs keep their iterate). */
 int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
-/* Which kernel factors a batch of small systems (N <= 1024; same LDL^T,
- * same MFMA tiles in the same order, so both give the same factor):
- * IPMZ_BATCH_FACTOR_AUTO (default: two workgroups per QP when 2 * batch <=
- * #CU, else one), IPMZ_BATCH_FACTOR_ONE (one workgroup per QP),
- * IPMZ_BATCH_FACTOR_PAIR (two per QP; IPMZ_ERR_INVALID unless 2 * batch <=
- * #CU, since both workgroups of a QP must be resident together). */
+/* Which kernel factors a batch of small systems (N <= 1024, 64-column
+ * blocks, one LDL^T): IPMZ_BATCH_FACTOR_AUTO (default: two workgroups per QP
+ * when 2 * batch <= #CU, else the left-looking one), IPMZ_BATCH_FACTOR_ONE
+ * (right-looking, one workgroup per QP), IPMZ_BATCH_FACTOR_PAIR (the same
+ * right-looking factor on two workgroups per QP -- identical results to ONE;
+ * IPMZ_ERR_INVALID unless 2 * batch <= #CU, since both workgroups of a QP
+ * must be resident together), IPMZ_BATCH_FACTOR_LEFT (left-looking, one
+ * workgroup per QP: every L tile formed once in registers; sums in a
+ * different order, so 1e-16-level differences against ONE / PAIR). */
 #define IPMZ_BATCH_FACTOR_AUTO 0
 #define IPMZ_BATCH_FACTOR_ONE 1
 #define IPMZ_BATCH_FACTOR_PAIR 2
+#define IPMZ_BATCH_FACTOR_LEFT 3
 int ipmz_batch_set_factor_kernel(ipmz_qp* qp, int kernel);
 
 /* Phase timing (HIP events on the context stream; eager launches only).

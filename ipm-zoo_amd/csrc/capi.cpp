@@ -904,7 +904,8 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
   bs.sD = s->sD;
   bs.sL = s->sL;
   bs.sW = s->sW;
-  bs.pflags = s->small_kernel == IPMZ_BATCH_FACTOR_ONE ? nullptr : s->pflags;
+  bs.pflags = s->pflags;
+  bs.small_kernel = s->small_kernel;
   bs.K0 = info_reset && uses_k0(s) ? s->K0 : nullptr;  // (info_reset: the fused step, whose pre phase assembled into K0)
   if (!info_reset) HIP_OK(hipMemsetAsync(s->binfo, 0x7f, sizeof(int), s->ctx->stream));
   HIP_OK(ldlt_factor_batched(s->K, s->ldk, s->N, s->D, s->bLinv, s->bW, nbo_for(s->ctx, s->N), s->ctx->nbi, s->binfo,
@@ -1789,7 +1790,7 @@ int ipmz_batch_solve(ipmz_qp* s, int max_iter, int* iterations, int* converged_c
   return IPMZ_OK;
 }
 int ipmz_batch_set_factor_kernel(ipmz_qp* s, int kernel) {
-  if (!s || kernel < IPMZ_BATCH_FACTOR_AUTO || kernel > IPMZ_BATCH_FACTOR_PAIR)
+  if (!s || kernel < IPMZ_BATCH_FACTOR_AUTO || kernel > IPMZ_BATCH_FACTOR_LEFT)
     return fail(IPMZ_ERR_INVALID, "ipmz_batch_set_factor_kernel: bad arguments");
   if (kernel == IPMZ_BATCH_FACTOR_PAIR && !(s->pflags && small_pair_eligible(s->B, s->N)))
     return fail(IPMZ_ERR_INVALID, "ipmz_batch_set_factor_kernel: two workgroups per QP need a batch of small systems "

@@ -148,12 +148,14 @@ struct NoHook {
 };
 // Ksrc (optional): read the block from there instead of K (the batched
 // factor's first touch of the assembled KKT, small.hip); L is written to K.
+// tid_arg (optional): the caller's thread index (small.hip launders it per
+// block column so the body's lane-dependent addresses are not hoisted).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
-                                            const TS* __restrict__ Ksrc = nullptr) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                            const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1) {
+  const int tid = tid_arg < 0 ? (int)threadIdx.x : tid_arg, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
   int nclk = 0;

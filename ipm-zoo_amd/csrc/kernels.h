@@ -64,6 +64,8 @@ struct BatchStrides {
   // kept across Newton steps, only its diagonal rewritten per step; nullptr =
   // K holds the assembled matrix
   const double* K0 = nullptr;
+  // small batched factor: IPMZ_BATCH_FACTOR_* (ipmz.h)
+  int small_kernel = 0;
 };
 #define IPMZ_PAIR_FLAGS 32  // per QP: LW[16], DONE[16] (N <= IPMZ_SMALL_NMAX)
 // the batched factor of order N runs two workgroups per QP (given flags)

@@ -16,6 +16,7 @@
 // waves (two per SIMD) split every 64 x 64 MFMA tile so one wave's LDS and
 // memory waits overlap the other's MFMAs; operand tiles for the next step
 // are loaded into registers while the current one computes.
+#include "ipmz.h"
 #include "common.h"
 #include "kernels.h"
 #include "diag64.h"
@@ -40,8 +41,8 @@ struct Cfg {
 // past nrows read row 0 and are zeroed on the LDS store.
 template <int SNW>
 __device__ __forceinline__ void tile_fetch(const double* __restrict__ src, int64_t lds, int nrows,
-                                           double (&v)[Cfg<SNW>::SFR]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                           double (&v)[Cfg<SNW>::SFR], int tid = threadIdx.x) {
+  const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
   for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
     const int rr = wave + SNW * i;
@@ -60,26 +61,39 @@ __device__ __forceinline__ void tile_fetch_sc(const double* __restrict__ src, in
   }
 }
 template <int SNW>
-__device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&v)[Cfg<SNW>::SFR]) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+__device__ __forceinline__ void tile_put(double* dst, int nrows, const double (&v)[Cfg<SNW>::SFR],
+                                         int tid = threadIdx.x) {
+  const int lane = tid & 63, wave = tid >> 6;
 #pragma unroll
   for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
     const int rr = wave + SNW * i;
     dst[rr * DS + lane] = rr < nrows ? v[i] : 0.0;
   }
 }
+// the same, column `lane` scaled by s (W = L D staged from an L tile)
+template <int SNW>
+__device__ __forceinline__ void tile_put_scaled(double* dst, int nrows, const double (&v)[Cfg<SNW>::SFR], double s,
+                                                int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+  for (int i = 0; i < Cfg<SNW>::SFR; ++i) {
+    const int rr = wave + SNW * i;
+    dst[rr * DS + lane] = rr < nrows ? v[i] * s : 0.0;
+  }
+}
 // this wave's part of the 64 x 64 result: rows 16 (w & 3) .. +15, column
 // blocks n0 + (0 .. SNN-1), n0 = SNN (w >> 2)
-__device__ __forceinline__ int tile_r0() { return 16 * ((threadIdx.x >> 6) & 3); }
+__device__ __forceinline__ int tile_r0(int tid = threadIdx.x) { return 16 * ((tid >> 6) & 3); }
 template <int SNW>
-__device__ __forceinline__ int tile_n0() { return Cfg<SNW>::SNN * (threadIdx.x >> 8); }
+__device__ __forceinline__ int tile_n0(int tid = threadIdx.x) { return Cfg<SNW>::SNN * (tid >> 8); }
 // acc[n] (+)= sgn * As[rows, :] Bs[16 (n0 + n).., :]^T.  LOWER: Bs is
 // lower triangular and only its lower part is meaningful (the diagonal
 // factor's L^{-1} image, left in LDS): entries k > row read as 0.
 template <int SNW, bool NEG, bool LOWER = false>
-__device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[Cfg<SNW>::SNN]) {
-  const int lane = threadIdx.x & 63;
-  const int arow = tile_r0() + (lane & 15), n0 = tile_n0<SNW>();
+__device__ __forceinline__ void tile_mma(const double* As, const double* Bs, acc_t (&acc)[Cfg<SNW>::SNN],
+                                         int tid = threadIdx.x) {
+  const int lane = tid & 63;
+  const int arow = tile_r0(tid) + (lane & 15), n0 = tile_n0<SNW>(tid);
 #pragma unroll 4
   for (int s = 0; s < 16; ++s) {
     const int k = 4 * s + (lane >> 4);
@@ -210,6 +224,193 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
       if (!more) break;
       c = cn;
       q = qn;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Left-looking variant (round 4): every tile of block column J is formed
+// ONCE, in registers, from the assembled matrix and the finished columns,
+//   T(c, J) = A(c, J) - sum_{K<J} L(c, K) (L(J, K) D_K)^T,     c >= J,
+// then factored (c = J: diag64_body, handed over through LDS) or solved
+// (c > J: L(c, J) = T X_J^T / D_J), and L stored once.  Against the
+// right-looking kernel above: no read-modify-write of trailing tiles and no W
+// buffer -- the loads of a step are finished L tiles, independent of the
+// MFMAs, so they are prefetched two tiles ahead.  Same tile MFMAs (16x16x4
+// f64 over 64-wide k blocks); the sums over K are accumulated in registers
+// before the subtraction (1e-16-level rounding differences against the
+// right-looking order).  Columns c > J are formed CM tiles at a time.
+// LDS: P0/P1 A operands (alternating), P2/P3 B operands (P3 doubles as
+// diag64_body's X = L_JJ^{-1}, read by the TRSMs), D of every finished column.
+// EXP (kbench attribution only, results meaningless when set): bit 0 skips
+// the diagonal factors, bit 1 the MFMAs, bit 2 the operand tile loads
+template <int SNW, int CM, int EXP = 0>
+__global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) void ldlt_small_left_kernel(
+    double* __restrict__ K, int64_t ld, int N, double* __restrict__ D, double* __restrict__ Linv,
+    int* __restrict__ info, int64_t sK, int64_t sD, int64_t sL, const double* __restrict__ K0) {
+  constexpr int SFR = Cfg<SNW>::SFR, SNN = Cfg<SNW>::SNN, TB = 64 * DS;
+  __shared__ __attribute__((aligned(16))) double smem[4 * TB + 64 + IPMZ_SMALL_NMAX];
+  const int64_t qp = blockIdx.x;
+  K += qp * sK;
+  D += qp * sD;
+  Linv += qp * sL;
+  const double* KS = K0 ? K0 + qp * sK : K;  // the assembled matrix: every entry read once
+  // buffer offsets opaque to the compiler (uniform SGPRs): every LDS access is
+  // then one base VGPR + an immediate offset; with constant offsets past the
+  // 64 KB immediate range the compiler materialised one VGPR per unrolled
+  // access and spilled
+  int o1 = TB;
+  asm volatile("" : "+s"(o1));
+  double* const P0 = smem;
+  double* const P1 = smem + o1;
+  double* const P2 = smem + 2 * o1;
+  double* const P3 = smem + 3 * o1;
+  double* const dsh = smem + 4 * o1;
+  double* const dall = dsh + 64;
+  const int nblk = (N + 63) / 64;
+  auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
+  auto Lt = [&](int c, int Kb) { return K + (int64_t)(64 * c) * ld + 64 * Kb; };  // tile L(c, Kb)
+  int abuf = 0;  // P0 / P1 alternation of the A operands (one barrier per tile)
+  for (int J = 0; J < nblk; ++J) {
+    const int J0 = 64 * J, b = nrows(J);
+    // the thread index laundered per block column: nothing lane-dependent is
+    // hoisted out of this loop (the hoisted diag64 / tile addresses of all
+    // phases at once spilled)
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));
+    const int lane = tid & 63, r0 = tile_r0(tid), n0 = tile_n0<SNW>(tid);
+    // acc <- this lane's elements of A(c, J) (lower part when c == J; lanes
+    // outside read a valid dummy address and are never used)
+    auto load_a = [&](int c, int J, acc_t(&acc)[SNN], int t) {
+      const int rows = nrows(c), ln = t & 63, rr0 = tile_r0(t), nn0 = tile_n0<SNW>(t);
+      const double* base = KS + (int64_t)(64 * c + rr0 + (ln >> 4)) * ld + 64 * J + 16 * nn0 + (ln & 15);
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (nn0 + n) + (ln & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = rr0 + MF::row(ln, g);
+          const bool in = row < rows && (c != J || col <= row);
+          acc[n][g] = *(in ? base + (int64_t)g * 4 * ld + 16 * n : KS);
+        }
+      }
+    };
+    __syncthreads();  // the previous column's TRSM reads of P0..P3 and its dall store done
+    // ---- T(J, J), then its factor
+    if (J == 0) {
+      if constexpr (!(EXP & 1))
+      diag64_body<false, false, double, false, SNW>(K, ld, 0, b, D, Linv, info, P0, P3, dsh, nullptr, NoHook(), KS, tid);
+    } else {
+      acc_t acc[SNN];
+      load_a(J, J, acc, tid);
+      double va[SFR], vb[SFR];
+      tile_fetch<SNW>(Lt(J, 0), ld, b, va, tid);
+      if (J > 1) tile_fetch<SNW>(Lt(J, 1), ld, b, vb, tid);
+      auto step = [&](int Kb, double(&v)[SFR]) {
+        double* pa = (Kb & 1) ? P1 : P0;
+        double* pb = (Kb & 1) ? P3 : P2;
+        tile_put<SNW>(pa, b, v, tid);
+        tile_put_scaled<SNW>(pb, b, v, dall[64 * Kb + lane], tid);
+        __syncthreads();
+        if (Kb + 2 < J && !(EXP & 4)) tile_fetch<SNW>(Lt(J, Kb + 2), ld, b, v, tid);
+        if constexpr (!(EXP & 2)) tile_mma<SNW, true>(pa, pb, acc, tid);
+      };
+      for (int Kb = 0; Kb < J; Kb += 2) {
+        step(Kb, va);
+        if (Kb + 1 < J) step(Kb + 1, vb);
+      }
+      __syncthreads();  // P0..P3 reads done: T goes to P0 as diag64_body's M
+#pragma unroll
+      for (int n = 0; n < SNN; ++n) {
+        const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = r0 + MF::row(lane, g);
+          P0[row * DS + col] = (row < b && col <= row) ? acc[n][g] : (row == col ? 1.0 : 0.0);
+        }
+      }
+      if constexpr (!(EXP & 1))
+      diag64_body<false, false, double, true, SNW>(K, ld, J0, b, D, Linv + (int64_t)J * 64 * 64, info, P0, P3, dsh,
+                                                   nullptr, NoHook(), nullptr, tid);
+    }
+    if (J == nblk - 1) break;
+    __syncthreads();  // diag64_body's write-back done reading P0; X (P3) and dsh final
+    if (tid < 64) dall[J0 + tid] = dsh[tid];
+    double rd[SNN];
+#pragma unroll
+    for (int n = 0; n < SNN; ++n) rd[n] = 1.0 / dsh[16 * (n0 + n) + (lane & 15)];
+    // ---- T(c, J), c > J, CM tiles at a time: the stream of operand tiles is
+    // (for each K < J) L(J, K) -> P2 scaled by D_K, then L(c, K) for the
+    // chunk's c, each followed by its MFMAs
+    for (int cb = J + 1; cb < nblk; cb += CM) {
+      const int nc = nblk - cb < CM ? nblk - cb : CM;
+      asm volatile("" : "+v"(tid));  // (again: nothing hoisted out of the chunk loop)
+      const int lane = tid & 63, r0 = tile_r0(tid), n0 = tile_n0<SNW>(tid);
+      acc_t acc[CM][SNN];
+#pragma unroll
+      for (int ci = 0; ci < CM; ++ci)
+        if (ci < nc) load_a(cb + ci, J, acc[ci], tid);
+      const int S = J * (nc + 1);
+      auto src = [&](int s, double(&v)[SFR]) {
+        if constexpr ((EXP & 4) != 0) return;
+        const int Kb = s / (nc + 1), t = s - Kb * (nc + 1);
+        if (t == 0) tile_fetch<SNW>(Lt(J, Kb), ld, 64, v, tid);
+        else tile_fetch<SNW>(Lt(cb + t - 1, Kb), ld, nrows(cb + t - 1), v, tid);
+      };
+      auto step = [&](int s, double(&v)[SFR]) {
+        const int Kb = s / (nc + 1), t = s - Kb * (nc + 1);
+        if (t == 0) {
+          __syncthreads();  // the previous K's MFMAs done reading P2
+          tile_put_scaled<SNW>(P2, 64, v, dall[64 * Kb + lane], tid);
+          if (s + 2 < S) src(s + 2, v);
+          return;
+        }
+        double* pa = abuf ? P1 : P0;
+        abuf ^= 1;
+        tile_put<SNW>(pa, nrows(cb + t - 1), v, tid);
+        __syncthreads();
+        if (s + 2 < S) src(s + 2, v);
+#pragma unroll
+        for (int ci = 0; ci < CM; ++ci)
+          if (ci == t - 1 && !(EXP & 2)) tile_mma<SNW, true>(pa, P2, acc[ci], tid);
+      };
+      if (S > 0) {
+        double va[SFR], vb[SFR];
+        src(0, va);
+        src(1, vb);  // S >= 2 (a B tile and at least one A tile per K)
+        for (int s = 0; s < S; s += 2) {
+          step(s, va);
+          if (s + 1 < S) step(s + 1, vb);
+        }
+      }
+      // ---- TRSM: L(c, J) = T(c, J) X_J^T / D_J (T through P0 / P1 as the A operand)
+#pragma unroll
+      for (int ci = 0; ci < CM; ++ci) {
+        if (ci >= nc) break;
+        const int c = cb + ci, rows = nrows(c);
+        double* pa = abuf ? P1 : P0;
+        abuf ^= 1;
+#pragma unroll
+        for (int n = 0; n < SNN; ++n) {
+          const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) pa[(r0 + MF::row(lane, g)) * DS + col] = acc[ci][n][g];
+        }
+        __syncthreads();
+        acc_t l[SNN];
+#pragma unroll
+        for (int n = 0; n < SNN; ++n) l[n] = (acc_t){0.0, 0.0, 0.0, 0.0};
+        if constexpr (!(EXP & 2)) tile_mma<SNW, false, true>(pa, P3, l, tid);
+#pragma unroll
+        for (int n = 0; n < SNN; ++n) {
+          const int col = 16 * (n0 + n) + (lane & 15);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int row = r0 + MF::row(lane, g);
+            if (row < rows) K[(int64_t)(64 * c + row) * ld + J0 + col] = l[n][g] * rd[n];
+          }
+        }
+      }
     }
   }
 }
@@ -381,18 +582,25 @@ bool small_pair_eligible(int B, int N) { return 2 * B <= device_cus() && N > 64 
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs) {
   if (N <= 0 || bs.B <= 0) return hipSuccess;
+  const int kern = bs.small_kernel;
   // a batch that leaves CUs idle: two workgroups per QP (flags zeroed here)
-  if (bs.pflags && small_pair_eligible(bs.B, N)) {
+  const bool pair_ok = bs.pflags && small_pair_eligible(bs.B, N);
+  if (pair_ok && (kern == IPMZ_BATCH_FACTOR_PAIR || kern == IPMZ_BATCH_FACTOR_AUTO)) {
     hipError_t e = hipMemsetAsync(bs.pflags, 0, ((size_t)bs.B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ldlt_small_pair_kernel<8>, dim3(2 * bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info,
                        bs.sK, bs.sD, bs.sL, bs.sW, bs.pflags, bs.pflags + (size_t)bs.B * IPMZ_PAIR_FLAGS, bs.K0);
     return hipGetLastError();
   }
-  // 8 waves (two per SIMD) also when the batch leaves a CU per QP: 16 waves
-  // measured slower (N = 320, B = 128: 249 vs 190 us)
-  hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK, bs.sD,
-                     bs.sL, bs.sW, bs.K0);
+  if (kern == IPMZ_BATCH_FACTOR_ONE) {
+    // 8 waves (two per SIMD) also when the batch leaves a CU per QP: 16 waves
+    // measured slower (N = 320, B = 128: 249 vs 190 us)
+    hipLaunchKernelGGL(ldlt_small_kernel<8>, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
+                       bs.sD, bs.sL, bs.sW, bs.K0);
+    return hipGetLastError();
+  }
+  hipLaunchKernelGGL((ldlt_small_left_kernel<8, 4>), dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info, bs.sK,
+                     bs.sD, bs.sL, bs.K0);
   return hipGetLastError();
 }
 
@@ -400,7 +608,23 @@ hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, do
 // SNW = 4 waves (two workgroups -- two QPs -- per CU) or 8
 hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, double* D, double* Linv, double* W,
                                      int* info, hipStream_t st, const BatchStrides& bs) {
-  if (snw == 4)
+  if (snw >= 100) {  // 100 + EXP: the left-looking kernel's attribution variants
+    auto l = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info, bs.sK, bs.sD, bs.sL, bs.K0);
+    };
+    switch (snw - 100) {
+      case 1: l(ldlt_small_left_kernel<8, 4, 1>); break;
+      case 2: l(ldlt_small_left_kernel<8, 4, 2>); break;
+      case 3: l(ldlt_small_left_kernel<8, 4, 3>); break;
+      case 4: l(ldlt_small_left_kernel<8, 4, 4>); break;
+      case 6: l(ldlt_small_left_kernel<8, 4, 6>); break;
+      case 7: l(ldlt_small_left_kernel<8, 4, 7>); break;
+      default: l(ldlt_small_left_kernel<8, 4, 0>); break;
+    }
+  } else if (snw == 1)
+    hipLaunchKernelGGL((ldlt_small_left_kernel<8, 4>), dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info,
+                       bs.sK, bs.sD, bs.sL, bs.K0);
+  else if (snw == 4)
     hipLaunchKernelGGL(ldlt_small_kernel<4>, dim3(bs.B), dim3(64 * 4), 0, st, K, ld, N, D, Linv, W, info, bs.sK,
                        bs.sD, bs.sL, bs.sW, bs.K0);
   else

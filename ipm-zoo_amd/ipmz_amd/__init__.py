@@ -551,11 +551,12 @@ class Batch(Optimizer):
         if not self.ctx.on_stream(torch.cuda.current_stream(t.device).cuda_stream):
             self.ctx.sync()
 
-    FACTOR_AUTO, FACTOR_ONE, FACTOR_PAIR = 0, 1, 2  # include/ipmz.h IPMZ_BATCH_FACTOR_*
+    FACTOR_AUTO, FACTOR_ONE, FACTOR_PAIR, FACTOR_LEFT = 0, 1, 2, 3  # include/ipmz.h IPMZ_BATCH_FACTOR_*
 
     def set_factor_kernel(self, kernel):
-        """FACTOR_AUTO, FACTOR_ONE (one workgroup per QP) or FACTOR_PAIR (two
-        per QP; needs 2 * batch <= #CU): the small batched LDL^T kernel."""
+        """FACTOR_AUTO, FACTOR_ONE (right-looking, one workgroup per QP),
+        FACTOR_PAIR (right-looking, two per QP; needs 2 * batch <= #CU) or
+        FACTOR_LEFT (left-looking, one per QP): the small batched LDL^T kernel."""
         _check(lib.ipmz_batch_set_factor_kernel(self.h, int(kernel)), "ipmz_batch_set_factor_kernel")
 
     def batch_scalars(self):

@@ -16,10 +16,14 @@ def ctx():
     return I.Context(0)
 
 
+@pytest.mark.parametrize("kernel", ["auto", "one", "left"])
 @pytest.mark.parametrize("n,m,p,B,seed0", [(64, 16, 0, 5, 100), (256, 64, 0, 12, 0), (96, 24, 8, 4, 7),
                                            (300, 60, 0, 3, 50), (700, 90, 10, 2, 60)])
-def test_batch_steps_vs_oracle(ctx, n, m, p, B, seed0):
+def test_batch_steps_vs_oracle(ctx, n, m, p, B, seed0, kernel):
+    """Every small-factor kernel (ragged last blocks: N = 80, 112, 360, 800)."""
     bt = I.Batch(n, m, p, B, ctx)
+    if kernel != "auto":
+        bt.set_factor_kernel({"one": I.Batch.FACTOR_ONE, "left": I.Batch.FACTOR_LEFT}[kernel])
     bt.generate(seed0)
     orcs = [oracle.OracleQP(oracle.gen_qp(n, m, p, seed0 + i)) for i in range(B)]
     for i, o in enumerate(orcs):

@@ -160,9 +160,31 @@ def test_c4_small_factor_kernels_agree_bitwise(ctx):
     assert np.array_equal(auto[0][0], pair[0][0])
 
 
+def test_c4_left_kernel_matches_right_looking(ctx):
+    """B = 1024: the left-looking factor (every L tile formed once in
+    registers; the sums over earlier block columns in another order) against
+    the right-looking one-workgroup factor -- the same steps to rounding."""
+    left = _run(ctx, B_, 900, 3, I.Batch.FACTOR_LEFT)
+    one = _run(ctx, B_, 900, 3, I.Batch.FACTOR_ONE)
+    for it in range(3):
+        scl, dl = left[it]
+        sco, do = one[it]
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            a, b = scl[:, I.SC[k]], sco[:, I.SC[k]]
+            assert np.all(np.abs(a - b) <= 1e-9 * np.maximum(1.0, np.abs(b))), (it, k)
+        for i in range(B_):
+            for w in range(2):
+                g, r = dl[i][w], do[i][w]
+                assert np.abs(g[:N_] - r[:N_]).max() < DX_TOL, (it, i, w)
+                assert np.abs(g - r).max() < 1e-9 * max(1.0, np.abs(r).max()), (it, i, w)
+
+
 def test_c4_pair_kernel_rejected_when_not_coresident(ctx):
     bt = I.Batch(N_, M_, 0, B_, ctx)
     with pytest.raises(I.IpmzError, match="2 \\* batch <= #CU"):
         bt.set_factor_kernel(I.Batch.FACTOR_PAIR)
     bt.set_factor_kernel(I.Batch.FACTOR_ONE)
+    bt.set_factor_kernel(I.Batch.FACTOR_LEFT)
+    with pytest.raises(I.IpmzError):
+        bt.set_factor_kernel(4)
     bt.close()

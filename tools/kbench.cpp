@@ -5,6 +5,8 @@
 // outside the product library.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <string>
@@ -175,9 +177,12 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
-  if (mode == "smallv") {  // kbench 320 smallv: the one-workgroup factor with 4 vs 8 waves per QP
+  if (mode == "smallv") {  // kbench 320 smallv: the one-workgroup factors: right-looking (8 waves) vs left-looking
+    std::vector<double> refK, refD;
+    std::vector<int> vars = {8, 1};
+    for (int a = 3; a < argc; ++a) vars.push_back(std::atoi(argv[a]));  // e.g. 101 102 104 (attribution)
     for (int B : {128, 1024})
-      for (int snw : {8, 4}) {
+      for (int snw : vars) {
         double *Kb, *Db, *Lb, *Wb;
         const int64_t sK = ld * N, sL = (int64_t)((N + 63) / 64) * 64 * 64;
         CK(hipMalloc(&Kb, sK * B * 8));
@@ -198,11 +203,26 @@ int main(int argc, char** argv) {
           const float ms = t.stop(st);
           if (rep) best = ms < best ? ms : best;
         }
-        std::vector<double> hD(N);
+        std::vector<double> hD(N), hK(sK);
         CK(hipMemcpy(hD.data(), Db + (int64_t)(B - 1) * N, N * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hK.data(), Kb + (int64_t)(B - 1) * sK, sK * 8, hipMemcpyDeviceToHost));
         double cs = 0;
         for (double d : hD) cs += d;
-        std::printf("small factor N=%d B=%d waves=%d: %.1f us (D checksum of the last QP %.15e)\n", N, B, snw, best * 1e3, cs);
+        // the variants against the first (right-looking) one: D and the strict lower L
+        double dD = 0, dL = 0;
+        if (snw == 8) {
+          refD = hD;
+          refK = hK;
+        } else {
+          for (int i = 0; i < N; ++i) {
+            dD = std::max(dD, std::fabs(hD[i] - refD[i]) / std::max(1.0, std::fabs(refD[i])));
+            for (int j = 0; j < i; ++j) dL = std::max(dL, std::fabs(hK[i * ld + j] - refK[i * ld + j]));
+          }
+        }
+        std::printf("small factor N=%d B=%d variant=%s: %.1f us (D checksum of the last QP %.15e; vs right-looking: "
+                    "max rel dD %.2e, max dL %.2e)\n",
+                    N, B, snw >= 100 ? ("left-exp" + std::to_string(snw - 100)).c_str() : snw == 1 ? "left" : snw == 4 ? "right-4w" : "right",
+                    best * 1e3, cs, dD, dL);
         CK(hipFree(Kb));
         CK(hipFree(Db));
         CK(hipFree(Lb));
