@@ -16,6 +16,8 @@
 // waves (two per SIMD) split every 64 x 64 MFMA tile so one wave's LDS and
 // memory waits overlap the other's MFMAs; operand tiles for the next step
 // are loaded into registers while the current one computes.
+#include <cstdio>
+
 #include "ipmz.h"
 #include "common.h"
 #include "kernels.h"
@@ -416,6 +418,306 @@ __global__ __launch_bounds__(64 * SNW) __attribute__((amdgpu_waves_per_eu(2))) v
 }
 
 // ---------------------------------------------------------------------------
+// Wave-specialized left-looking factor, N <= 64 NB <= 320 (C4's N = 320:
+// NB = 5).  The kernel above runs the diagonal factors -- the chain, ~14 us
+// per 64 x 64 block, one wave busy -- with the other seven waves waiting.
+// Here waves 0..3 (the chain group) only factor diagonal blocks (diag64_body,
+// NW = 4), while waves 4..7 (the bulk group) form the next tiles in the
+// chain's shadow:
+//   window J   chain: diag(J) (WS_NBAR barriers)
+//              bulk : TRSM(c, J-1) of the chunks c > J (X_{J-1} is still in
+//                     LDS until diag(J) writes X, after its third barrier),
+//                     then T(c, J) = A(c, J) - sum_{K<J} L(c, K) W(J, K)^T,
+//                     c > J, and the next diagonal tile minus its terms K < J,
+//                     one tile of MFMAs per barrier interval, padded to WS_NBAR
+//   transition bulk : TRSM(J+1, J) -> L(J+1, J), its W = L D into LDS (T1),
+//                     the last term of T(J+1, J+1) -> LDS as the next M (T2)
+// Both groups run the same barriers (raw counts match by construction; see
+// ws_window_bars).  The bulk group keeps its tiles TRANSPOSED in registers --
+// wave 4 + w owns columns 16 w .. 16 w + 15 of every T^T (rows of L) -- so a
+// TRSM reads its T straight from registers (the accumulator layout of a
+// 16 x 16 block is the B fragment of the next NN product) and its L operand
+// rows come from global memory into registers (k order permuted so each lane
+// loads 32 contiguous bytes); only W = L D is staged in LDS.
+constexpr int WS_NBAR = 10;  // barriers of one diag64_body call (clkbuf == nullptr)
+// kbench attribution (CLK instantiation only): s_memtime stamps of QP 0,
+// chain group [0, 64), bulk group [64, 128)
+__device__ unsigned long long ws_clk[128];
+__host__ __device__ constexpr int ws_window_bars(int NB, int J) {
+  // leftover TRSMs + per K < J: a staging interval and one per tile c > J
+  // (the next diagonal tile shares tile J+1's interval: the same L rows)
+  return J == 0 || J + 1 >= NB ? 0 : (NB - J - 1) + J * (1 + (NB - J - 1));
+}
+__host__ __device__ constexpr bool ws_schedule_fits(int NB) {
+  for (int J = 0; J < NB; ++J)
+    if (ws_window_bars(NB, J) > WS_NBAR || (J >= 1 && NB - J - 1 > 3)) return false;  // leftovers before diag's X write
+  return true;
+}
+static_assert(ws_schedule_fits(2) && ws_schedule_fits(3) && ws_schedule_fits(4) && ws_schedule_fits(5), "WS schedule");
+
+template <int NB, bool CLK = false>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void ldlt_small_ws_kernel(
+    double* __restrict__ K, int64_t ld, int N, double* __restrict__ D, double* __restrict__ Linv,
+    int* __restrict__ info, int64_t sK, int64_t sD, int64_t sL, const double* __restrict__ K0) {
+  constexpr int TB = 64 * DS;
+  __shared__ __attribute__((aligned(16))) double smem[4 * TB + 64 + 64 * NB];
+  const int64_t qp = blockIdx.x;
+  K += qp * sK;
+  D += qp * sD;
+  Linv += qp * sL;
+  const double* KS = K0 ? K0 + qp * sK : K;  // the assembled matrix: every entry read once
+  int o1 = TB;  // (opaque offsets: one base VGPR + immediates per LDS access, see above)
+  asm volatile("" : "+s"(o1));
+  double* const M = smem;             // the next diagonal tile (chain input)
+  double* const W1 = smem + o1;       // W(J+1, K) = L(J+1, K) D_K (bulk; the transition's W(J+1, J))
+  double* const W0 = smem + 2 * o1;   // W(J, K) (bulk)
+  double* const X = smem + 3 * o1;    // L_JJ^{-1} (chain output, read by the TRSMs)
+  double* const dsh = smem + 4 * o1;  // D_J (chain)
+  double* const dall = dsh + 64;      // D of every finished column
+  auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
+  auto stamp = [&](int slot) {
+    if constexpr (CLK)
+      if (blockIdx.x == 0 && (threadIdx.x & 255) == 0) ws_clk[slot] = __builtin_amdgcn_s_memtime();
+  };
+  if ((threadIdx.x >> 6) < 4) {
+    // ---- chain group: diag(J), then the two transition barriers
+    for (int J = 0; J < NB; ++J) {
+      int tid = threadIdx.x;
+      asm volatile("" : "+v"(tid));
+      const int b = nrows(J);
+      stamp(3 * J);
+      if (J == 0)
+        diag64_body<false, false, double, false, 4>(K, ld, 0, b, D, Linv, info, M, X, dsh, nullptr, NoHook(), KS, tid);
+      else
+        diag64_body<false, false, double, true, 4>(K, ld, 64 * J, b, D, Linv + (int64_t)J * 64 * 64, info, M, X, dsh,
+                                                   nullptr, NoHook(), nullptr, tid);
+      stamp(3 * J + 1);
+      if (J == NB - 1) break;
+      if (tid < 64) dall[64 * J + tid] = dsh[tid];
+      __syncthreads();  // T1
+      __syncthreads();  // T2: M holds T(J+1, J+1)
+      stamp(3 * J + 2);
+    }
+    return;
+  }
+  // ---- bulk group: wave 4 + w owns rows r = 16 w .. 16 w + 15 of every L
+  // tile, i.e. columns r of every T^T
+  acc_t T[NB - 1][4];  // T^T(c, .), slot c - 1: blocks jb (rows j = 16 jb + q + 4 g)
+  acc_t PT[4];         // the next diagonal tile, transposed
+  // A(c, J)^T (lower part for the diagonal tile c == J); rows r past the matrix read as 0
+  // (32-bit element offsets from the QP's base: one VGPR per address, immediate column offsets)
+  const unsigned ldu = (unsigned)ld;
+  auto load_at = [&](int c, int J, acc_t(&a)[4], int tid) {
+    const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), rows = nrows(c);
+    const unsigned o = (unsigned)(64 * c + (r < rows ? r : 0)) * ldu + 64 * J + q;
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int j = 16 * jb + q + 4 * g;
+        const bool in = r < rows && (c != J || j <= r);  // (the upper part of A(J, J) is read, not used)
+        const double v = KS[o + 16 * jb + 4 * g];
+        a[jb][g] = in ? v : 0.0;
+      }
+  };
+  // this lane's L(c, Kb) row r, columns 16 u + 4 q + t (the k order of the
+  // accumulation MFMAs): 32 contiguous bytes per u
+  auto load_bf = [&](int c, int Kb, double(&bf)[16], int tid) {
+    const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), rows = nrows(c);
+    const double2* src =
+        reinterpret_cast<const double2*>(K + ((unsigned)(64 * c + (r < rows ? r : 0)) * ldu + 64 * Kb + 4 * q));
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const double2 x0 = src[8 * u], x1 = src[8 * u + 1];
+      bf[4 * u] = x0.x;
+      bf[4 * u + 1] = x0.y;
+      bf[4 * u + 2] = x1.x;
+      bf[4 * u + 3] = x1.y;
+    }
+  };
+  // a^T -= Ls (bf D_Kb)^T over one 64-wide k block: the plain L copy in LDS
+  // (rows j) against this lane's L rows scaled by the pivots (W = L D)
+  auto mma_acc = [&](acc_t(&a)[4], const double* Ls, const double(&bf)[16], int Kb, int tid) {
+    const int l = tid & 63, q = l >> 4;
+    const double* base = Ls + (l & 15) * DS + 4 * q;
+    const double* dk = dall + 64 * Kb + 4 * q;
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const double b = bf[4 * u + t] * dk[16 * u + t];
+#pragma unroll
+        for (int jb = 0; jb < 4; ++jb) a[jb] = MF::mma(-base[16 * jb * DS + 16 * u + t], b, a[jb]);
+        __builtin_amdgcn_sched_barrier(0);  // (bounds the LDS operands in flight: registers)
+      }
+  };
+  // L^T = diag(1 / d) X T^T: X (lower, LDS) against T^T's blocks as B
+  // fragments; lt[ib] rows i = 16 ib + q + 4 g; d: the pivots in LDS
+  auto trsm = [&](const acc_t(&a)[4], acc_t(&lt)[4], const double* d, int tid) {
+    const int l = tid & 63, q = l >> 4;
+    const double* xr = X + (l & 15) * DS + q;
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib) lt[ib] = (acc_t){0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+#pragma unroll
+        for (int ib = jb; ib < 4; ++ib) lt[ib] = MF::mma(xr[16 * ib * DS + 16 * jb + 4 * g], a[jb][g], lt[ib]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) lt[ib][g] *= fast_rcp(d[16 * ib + q + 4 * g]);
+  };
+  // L(c, J) rows r of this wave: transposed through the wave's own rows of a
+  // free LDS tile, then stored a whole 512-byte row per instruction (the
+  // register layout would store 32-byte pieces of 16 rows per instruction)
+  auto store_l = [&](int c, int J, const acc_t(&lt)[4], double* buf, int tid) {
+    const int l = tid & 63, q = l >> 4, w = (tid >> 6) - 4, r = 16 * w + (l & 15), rows = nrows(c);
+#pragma unroll
+    for (int ib = 0; ib < 4; ++ib)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) buf[r * DS + 16 * ib + q + 4 * g] = lt[ib][g];
+    unsigned o = (unsigned)(64 * c + 16 * w) * ldu + 64 * J + l;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      if (16 * w + i < rows) K[o] = buf[(16 * w + i) * DS + l];
+      o += ldu;
+      if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // plain copies of L(J, Kb) -> W0 and L(J+1, Kb) -> W1 (256 threads; rows
+  // past the matrix zero): loads into v, then the LDS stores
+  // (W1P = false: only the W0 part -- W1 already holds its tile)
+  auto stage_load = [&](int J, int Kb, double(&v)[32], bool w1p, int tid) {
+    const int t = tid - 256, col = t & 63, rows1 = nrows(J + 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = (t >> 6) + 4 * i;
+      v[i] = K[(unsigned)(64 * J + r) * ldu + 64 * Kb + col];  // (block J < NB - 1: full)
+      if (w1p) v[16 + i] = K[(unsigned)(64 * (J + 1) + (r < rows1 ? r : 0)) * ldu + 64 * Kb + col];
+    }
+  };
+  auto stage_put = [&](const double(&v)[32], int J, bool w1p, int tid) {
+    const int t = tid - 256, col = t & 63, rows1 = nrows(J + 1);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int r = (t >> 6) + 4 * i;
+      W0[r * DS + col] = v[i];
+      if (w1p) W1[r * DS + col] = r < rows1 ? v[16 + i] : 0.0;
+    }
+  };
+  static_for<NB>([&](auto jc) {
+    constexpr int J = decltype(jc)::value;
+    int tid = threadIdx.x;
+    asm volatile("" : "+v"(tid));  // nothing lane-dependent hoisted across windows
+    int nb = 0;
+    // raw barrier: this wave's LDS operations retired, its global loads and
+    // stores stay in flight; FULL (__syncthreads): the stores complete too,
+    // where another interval reads them next
+    auto bar = [&](bool full) {
+      if (full) {
+        __syncthreads();
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+        asm volatile("" ::: "memory");
+      }
+      __builtin_amdgcn_sched_barrier(0);  // (nothing scheduled across intervals: registers)
+      ++nb;
+      stamp(64 + 13 * J + nb);
+    };
+    stamp(64 + 13 * J);
+    // ======== window J (the chain factors block J)
+    if constexpr (J == 0) {
+      static_for<NB - 1>([&](auto cc) { load_at(decltype(cc)::value + 1, 0, T[decltype(cc)::value], tid); });
+      if constexpr (NB > 1) load_at(1, 1, PT, tid);
+    } else if constexpr (J + 1 < NB) {
+      constexpr int NL = NB - J - 1;  // leftover TRSMs of column J-1 = tiles c = J+1 .. NB-1 per K
+      // the first K step's operands, loaded under the leftovers: L(J, 0)
+      // (earlier windows) and L(J+1, 0) -- for J = 1 that tile is the first
+      // leftover's own result, transposed straight into W1 below
+      double stg[32], bfa[16], bfb[16];
+      stage_load(J, 0, stg, J > 1, tid);
+      // X_{J-1} stays intact until diag(J)'s 4th interval (NL <= 3)
+      static_for<NL>([&](auto cc) {
+        constexpr int c = J + 1 + decltype(cc)::value;
+        acc_t lt[4];
+        trsm(T[c - 1], lt, dall + 64 * (J - 1), tid);
+        // (W0 is restaged after the leftovers; W1 then holds L(2, 0) for J = 1)
+        store_l(c, J - 1, lt, (J == 1 && c == 2) ? W1 : W0, tid);
+        __builtin_amdgcn_sched_barrier(0);  // (register pressure: the next loads stay here)
+        load_at(c, J, T[c - 1], tid);  // T(c, J) starts from A(c, J)
+        bar(decltype(cc)::value == NL - 1);  // the K loop reads these L rows
+      });
+      asm volatile("" ::: "memory");
+      load_at(J + 1, J + 1, PT, tid);
+      // K loop, per Kb: S (W0, W1 staged), M1 (tile J+1 and the diagonal
+      // tile: the same L rows), Mc (c = J+2 ..); each item's global operand is
+      // loaded one interval ahead
+      static_for<J>([&](auto kc) {
+        constexpr int Kb = decltype(kc)::value;
+        stage_put(stg, J, J > 1 || Kb > 0, tid);
+        asm volatile("" ::: "memory");
+        load_bf(J + 1, Kb, bfa, tid);
+        bar(false);
+        if constexpr (NL >= 2) load_bf(J + 2, Kb, bfb, tid);
+        else if constexpr (Kb + 1 < J) stage_load(J, Kb + 1, stg, true, tid);
+        mma_acc(T[J], W0, bfa, Kb, tid);
+        mma_acc(PT, W1, bfa, Kb, tid);
+        bar(false);
+        static_for<NL - 1>([&](auto cc) {
+          constexpr int ci = decltype(cc)::value, c = J + 2 + ci;
+          auto& cur = (ci % 2 == 0) ? bfb : bfa;
+          auto& nxt = (ci % 2 == 0) ? bfa : bfb;
+          if constexpr (c + 1 < NB) load_bf(c + 1, Kb, nxt, tid);
+          else if constexpr (Kb + 1 < J) stage_load(J, Kb + 1, stg, true, tid);
+          mma_acc(T[c - 1], W0, cur, Kb, tid);
+          bar(false);
+        });
+      });
+    }
+    while (nb < WS_NBAR) bar(false);
+    // ======== transition: L(J+1, J) and the last term of T(J+1, J+1) -> M
+    if constexpr (J + 1 < NB) {
+      const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), b = nrows(J + 1);
+      acc_t lt[4];
+      trsm(T[J], lt, dsh, tid);  // X_J, D_J final after diag(J)'s last barrier
+      store_l(J + 1, J, lt, W0, tid);
+#pragma unroll
+      for (int ib = 0; ib < 4; ++ib)  // W(J+1, J) = L(J+1, J) D_J: this wave's rows r
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int i = 16 * ib + q + 4 * g;
+          W1[r * DS + i] = lt[ib][g] * dsh[i];
+        }
+      stamp(64 + 13 * J + 11);
+      __syncthreads();  // T1 (the chain's write-back of diag(J) done with M)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) {
+        const double* wr = W1 + (16 * jb + (l & 15)) * DS + q;
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) PT[jb] = MF::mma(-wr[16 * kb + 4 * g], lt[kb][g], PT[jb]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int j = 16 * jb + q + 4 * g;
+          M[r * DS + j] = (r < b && j <= r) ? PT[jb][g] : (r == j ? 1.0 : 0.0);
+        }
+      __syncthreads();  // T2 (also: L(J+1, J) stored before the next window reads it)
+      stamp(64 + 13 * J + 12);
+    }
+  });
+}
+
+// ---------------------------------------------------------------------------
 // The same factor with TWO workgroups per QP, for batches that leave CUs
 // idle (2B <= #CU: C4's 128 QPs per GPU at 8 GPUs; N = 320, B = 128: 194 ->
 // 177 us -- the five 64-column diagonal blocks, ~15 us each, stay on one
@@ -585,7 +887,8 @@ hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, do
   const int kern = bs.small_kernel;
   // a batch that leaves CUs idle: two workgroups per QP (flags zeroed here)
   const bool pair_ok = bs.pflags && small_pair_eligible(bs.B, N);
-  if (pair_ok && (kern == IPMZ_BATCH_FACTOR_PAIR || kern == IPMZ_BATCH_FACTOR_AUTO)) {
+  const bool ws_ok = N > 64 && N <= 320;  // the wave-specialized left-looking factor beats the pair
+  if (pair_ok && (kern == IPMZ_BATCH_FACTOR_PAIR || (kern == IPMZ_BATCH_FACTOR_AUTO && !ws_ok))) {
     hipError_t e = hipMemsetAsync(bs.pflags, 0, ((size_t)bs.B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ldlt_small_pair_kernel<8>, dim3(2 * bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info,
@@ -599,8 +902,19 @@ hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, do
                        bs.sD, bs.sL, bs.sW, bs.K0);
     return hipGetLastError();
   }
-  hipLaunchKernelGGL((ldlt_small_left_kernel<8, 4>), dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info, bs.sK,
-                     bs.sD, bs.sL, bs.K0);
+  // left-looking: wave-specialized up to N = 320 (C4: 1024 QPs 854 -> 706 us,
+  // 128 QPs 195 -> 156 us against the right-looking factor), else the plain one
+  const int nb = (N + 63) / 64;
+  auto ws = [&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(bs.B), dim3(512), 0, st, K, ld, N, D, Linv, info, bs.sK, bs.sD, bs.sL, bs.K0);
+  };
+  if (nb == 5) ws(ldlt_small_ws_kernel<5>);
+  else if (nb == 4) ws(ldlt_small_ws_kernel<4>);
+  else if (nb == 3) ws(ldlt_small_ws_kernel<3>);
+  else if (nb == 2) ws(ldlt_small_ws_kernel<2>);
+  else
+    hipLaunchKernelGGL((ldlt_small_left_kernel<8, 4>), dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info,
+                       bs.sK, bs.sD, bs.sL, bs.K0);
   return hipGetLastError();
 }
 
@@ -621,6 +935,29 @@ hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, doub
       case 7: l(ldlt_small_left_kernel<8, 4, 7>); break;
       default: l(ldlt_small_left_kernel<8, 4, 0>); break;
     }
+  } else if (snw == 2) {  // the wave-specialized left-looking factor (N <= 320)
+    const int nb = (N + 63) / 64;
+    auto l = [&](auto kern) {
+      hipLaunchKernelGGL(kern, dim3(bs.B), dim3(512), 0, st, K, ld, N, D, Linv, info, bs.sK, bs.sD, bs.sL, bs.K0);
+    };
+    if (nb == 5 && (debug_inject_mask() & IPMZ_DEBUG_TRACE)) {
+      l(ldlt_small_ws_kernel<5, true>);
+      unsigned long long h[128];
+      hipError_t e = hipMemcpyFromSymbol(h, HIP_SYMBOL(ws_clk), sizeof(h), 0, hipMemcpyDeviceToHost);
+      if (e != hipSuccess) return e;
+      const unsigned long long t0 = h[0];
+      for (int J = 0; J < 5; ++J) {
+        std::printf("ws J=%d chain: diag %llu..%llu T2 %llu | bulk: start %llu bars", J, h[3 * J] - t0, h[3 * J + 1] - t0,
+                    J < 4 ? h[3 * J + 2] - t0 : 0ull, h[64 + 13 * J] - t0);
+        for (int k = 1; k <= 10; ++k) std::printf(" %llu", h[64 + 13 * J + k] - t0);
+        if (J < 4) std::printf(" | pre-T1 %llu T2 %llu", h[64 + 13 * J + 11] - t0, h[64 + 13 * J + 12] - t0);
+        std::printf("\n");
+      }
+    } else if (nb == 5) l(ldlt_small_ws_kernel<5>);
+    else if (nb == 4) l(ldlt_small_ws_kernel<4>);
+    else if (nb == 3) l(ldlt_small_ws_kernel<3>);
+    else if (nb == 2) l(ldlt_small_ws_kernel<2>);
+    else return hipErrorInvalidValue;
   } else if (snw == 1)
     hipLaunchKernelGGL((ldlt_small_left_kernel<8, 4>), dim3(bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, info,
                        bs.sK, bs.sD, bs.sL, bs.K0);

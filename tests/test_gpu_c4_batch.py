@@ -148,16 +148,28 @@ def test_c4_batch1024_matches_pair_kernel_runs(ctx):
 
 def test_c4_small_factor_kernels_agree_bitwise(ctx):
     """B = 128: the one-workgroup factor and the two-workgroup factor forced on
-    the same batch (same MFMA tiles in the same order) give the same steps."""
+    the same batch (same MFMA tiles in the same order) give the same steps;
+    the default (the wave-specialized left-looking factor at N = 320) and the
+    explicit left-looking choice agree bitwise, and with the pair to rounding."""
     one = _run(ctx, 128, 500, 3, I.Batch.FACTOR_ONE)
     pair = _run(ctx, 128, 500, 3, I.Batch.FACTOR_PAIR)
-    auto = _run(ctx, 128, 500, 1)
+    auto = _run(ctx, 128, 500, 2)
+    left = _run(ctx, 128, 500, 2, I.Batch.FACTOR_LEFT)
     for it in range(3):
         assert np.array_equal(one[it][0], pair[it][0]), it
         for i in range(128):
             for w in range(2):
                 assert np.array_equal(one[it][1][i][w], pair[it][1][i][w]), (it, i, w)
-    assert np.array_equal(auto[0][0], pair[0][0])
+    for it in range(2):
+        assert np.array_equal(auto[it][0], left[it][0]), it
+        for k in ("alpha_aff", "mu_aff", "sigma", "alpha"):
+            a, b = auto[it][0][:, I.SC[k]], pair[it][0][:, I.SC[k]]
+            assert np.all(np.abs(a - b) <= 1e-9 * np.maximum(1.0, np.abs(b))), (it, k)
+        for i in range(128):
+            for w in range(2):
+                assert np.array_equal(auto[it][1][i][w], left[it][1][i][w]), (it, i, w)
+                g, r = auto[it][1][i][w], pair[it][1][i][w]
+                assert np.abs(g[:N_] - r[:N_]).max() < DX_TOL, (it, i, w)
 
 
 def test_c4_left_kernel_matches_right_looking(ctx):

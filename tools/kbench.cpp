@@ -221,7 +221,7 @@ int main(int argc, char** argv) {
         }
         std::printf("small factor N=%d B=%d variant=%s: %.1f us (D checksum of the last QP %.15e; vs right-looking: "
                     "max rel dD %.2e, max dL %.2e)\n",
-                    N, B, snw >= 100 ? ("left-exp" + std::to_string(snw - 100)).c_str() : snw == 1 ? "left" : snw == 4 ? "right-4w" : "right",
+                    N, B, snw >= 100 ? ("left-exp" + std::to_string(snw - 100)).c_str() : snw == 2 ? "left-ws" : snw == 1 ? "left" : snw == 4 ? "right-4w" : "right",
                     best * 1e3, cs, dD, dL);
         CK(hipFree(Kb));
         CK(hipFree(Db));
