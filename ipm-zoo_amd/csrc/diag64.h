@@ -150,11 +150,16 @@ struct NoHook {
 // factor's first touch of the assembled KKT, small.hip); L is written to K.
 // tid_arg (optional): the caller's thread index (small.hip launders it per
 // block column so the body's lane-dependent addresses are not hoisted).
-template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook>
+// WB_LINV = false: L^{-1} is not written back (the caller writes it from X
+// later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
+// column pass (the batched factor writes the previous block's L^{-1} there).
+template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
+          bool WB_LINV = true, typename IDLE0 = NoHook>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
-                                            const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1) {
+                                            const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1,
+                                            IDLE0 idle0 = IDLE0()) {
   const int tid = tid_arg < 0 ? (int)threadIdx.x : tid_arg, lane = tid & 63, wave = tid >> 6;
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
@@ -209,6 +214,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   };
   auto xoff = [&](int p, int j) { xmul(p, j, xsum(p, j)); };  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
   if (wave == 0) colpass16(M, dsh, 0, lane);
+  else idle0();
   __syncthreads();
   clk();
   for (int p = 0; p < 3; ++p) {
@@ -256,9 +262,11 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   for (int idx = tid; idx < 64 * 64; idx += 64 * NW) {
     const int rr = idx >> 6, cc = idx & 63;
     if (rr < b && cc < rr) K[(int64_t)(k0 + rr) * ld + k0 + cc] = (TS)M[rr * DS + cc];
-    const TS x = (TS)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc]));
-    if constexpr (COH) __hip_atomic_store(&Linv[idx], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else Linv[idx] = x;
+    if constexpr (WB_LINV) {
+      const TS x = (TS)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc]));
+      if constexpr (COH) __hip_atomic_store(&Linv[idx], x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else Linv[idx] = x;
+    }
   }
   if (tid < b) {
     const double dk = dsh[tid];

@@ -475,9 +475,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
   double* const dsh = smem + 4 * o1;  // D_J (chain)
   double* const dall = dsh + 64;      // D of every finished column
   auto nrows = [&](int c) { return N - 64 * c < 64 ? N - 64 * c : 64; };
+  __shared__ unsigned long long clk_sh[CLK ? 128 : 1];  // (stamps in LDS: no registers held)
   auto stamp = [&](int slot) {
     if constexpr (CLK)
-      if (blockIdx.x == 0 && (threadIdx.x & 255) == 0) ws_clk[slot] = __builtin_amdgcn_s_memtime();
+      clk_sh[slot] = __builtin_amdgcn_s_memtime();  // (every lane: no branch)
   };
   if ((threadIdx.x >> 6) < 4) {
     // ---- chain group: diag(J), then the two transition barriers
@@ -486,11 +487,24 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       asm volatile("" : "+v"(tid));
       const int b = nrows(J);
       stamp(3 * J);
+      // L^{-1} of block J-1 (still in X) is written by waves 1..3 while wave 0
+      // runs diag(J)'s first column pass -- off the transition's critical path
+      auto linv_prev = [&]() {
+        double* dst = Linv + (int64_t)(J - 1) * 64 * 64;
+        for (int idx = tid - 64; idx < 64 * 64; idx += 192) {
+          const int rr = idx >> 6, cc = idx & 63;
+          dst[idx] = cc > rr ? 0.0 : X[rr * DS + cc];  // (block J-1 < NB-1: full)
+        }
+      };
       if (J == 0)
-        diag64_body<false, false, double, false, 4>(K, ld, 0, b, D, Linv, info, M, X, dsh, nullptr, NoHook(), KS, tid);
-      else
-        diag64_body<false, false, double, true, 4>(K, ld, 64 * J, b, D, Linv + (int64_t)J * 64 * 64, info, M, X, dsh,
-                                                   nullptr, NoHook(), nullptr, tid);
+        diag64_body<false, false, double, false, 4, NoHook, false>(K, ld, 0, b, D, Linv, info, M, X, dsh, nullptr,
+                                                                   NoHook(), KS, tid);
+      else if (J < NB - 1)
+        diag64_body<false, false, double, true, 4, NoHook, false>(K, ld, 64 * J, b, D, Linv, info, M, X, dsh,
+                                                                  nullptr, NoHook(), nullptr, tid, linv_prev);
+      else  // the last block writes its own L^{-1}
+        diag64_body<false, false, double, true, 4, NoHook, true>(K, ld, 64 * J, b, D, Linv + (int64_t)J * 64 * 64, info,
+                                                                 M, X, dsh, nullptr, NoHook(), nullptr, tid, linv_prev);
       stamp(3 * J + 1);
       if (J == NB - 1) break;
       if (tid < 64) dall[64 * J + tid] = dsh[tid];
@@ -498,6 +512,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       __syncthreads();  // T2: M holds T(J+1, J+1)
       stamp(3 * J + 2);
     }
+    if constexpr (CLK)
+      if (blockIdx.x == 0 && threadIdx.x < 64) ws_clk[threadIdx.x] = clk_sh[threadIdx.x];
     return;
   }
   // ---- bulk group: wave 4 + w owns rows r = 16 w .. 16 w + 15 of every L
@@ -574,12 +590,15 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
   // L(c, J) rows r of this wave: transposed through the wave's own rows of a
   // free LDS tile, then stored a whole 512-byte row per instruction (the
   // register layout would store 32-byte pieces of 16 rows per instruction)
-  auto store_l = [&](int c, int J, const acc_t(&lt)[4], double* buf, int tid) {
-    const int l = tid & 63, q = l >> 4, w = (tid >> 6) - 4, r = 16 * w + (l & 15), rows = nrows(c);
+  auto put_l = [&](const acc_t(&lt)[4], double* buf, int tid) {
+    const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15);
 #pragma unroll
     for (int ib = 0; ib < 4; ++ib)
 #pragma unroll
       for (int g = 0; g < 4; ++g) buf[r * DS + 16 * ib + q + 4 * g] = lt[ib][g];
+  };
+  auto rows_out = [&](int c, int J, const double* buf, int tid) {  // this wave's rows of buf -> L(c, J)
+    const int l = tid & 63, w = (tid >> 6) - 4, rows = nrows(c);
     unsigned o = (unsigned)(64 * c + 16 * w) * ldu + 64 * J + l;
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
@@ -587,6 +606,10 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       o += ldu;
       if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
     }
+  };
+  auto store_l = [&](int c, int J, const acc_t(&lt)[4], double* buf, int tid) {
+    put_l(lt, buf, tid);
+    rows_out(c, J, buf, tid);
   };
   // plain copies of L(J, Kb) -> W0 and L(J+1, Kb) -> W1 (256 threads; rows
   // past the matrix zero): loads into v, then the LDS stores
@@ -631,6 +654,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
     };
     stamp(64 + 13 * J);
     // ======== window J (the chain factors block J)
+    if constexpr (J >= 1) rows_out(J, J - 1, W0, tid);  // the transition's L(J, J-1), transposed into W0
     if constexpr (J == 0) {
       static_for<NB - 1>([&](auto cc) { load_at(decltype(cc)::value + 1, 0, T[decltype(cc)::value], tid); });
       if constexpr (NB > 1) load_at(1, 1, PT, tid);
@@ -646,10 +670,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
         constexpr int c = J + 1 + decltype(cc)::value;
         acc_t lt[4];
         trsm(T[c - 1], lt, dall + 64 * (J - 1), tid);
+        if constexpr (J == 1) stamp(20 + 3 * decltype(cc)::value);
         // (W0 is restaged after the leftovers; W1 then holds L(2, 0) for J = 1)
         store_l(c, J - 1, lt, (J == 1 && c == 2) ? W1 : W0, tid);
+        if constexpr (J == 1) stamp(21 + 3 * decltype(cc)::value);
         __builtin_amdgcn_sched_barrier(0);  // (register pressure: the next loads stay here)
         load_at(c, J, T[c - 1], tid);  // T(c, J) starts from A(c, J)
+        if constexpr (J == 1) stamp(22 + 3 * decltype(cc)::value);
         bar(decltype(cc)::value == NL - 1);  // the K loop reads these L rows
       });
       asm volatile("" ::: "memory");
@@ -665,8 +692,11 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
         bar(false);
         if constexpr (NL >= 2) load_bf(J + 2, Kb, bfb, tid);
         else if constexpr (Kb + 1 < J) stage_load(J, Kb + 1, stg, true, tid);
+        if constexpr (J == 1) stamp(30);
         mma_acc(T[J], W0, bfa, Kb, tid);
+        if constexpr (J == 1) stamp(31);
         mma_acc(PT, W1, bfa, Kb, tid);
+        if constexpr (J == 1) stamp(32);
         bar(false);
         static_for<NL - 1>([&](auto cc) {
           constexpr int ci = decltype(cc)::value, c = J + 2 + ci;
@@ -685,7 +715,9 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), b = nrows(J + 1);
       acc_t lt[4];
       trsm(T[J], lt, dsh, tid);  // X_J, D_J final after diag(J)'s last barrier
-      store_l(J + 1, J, lt, W0, tid);
+      if constexpr (J == 1) stamp(33);
+      put_l(lt, W0, tid);  // L(J+1, J) -> global from W0 in the next window's first interval
+      if constexpr (J == 1) stamp(34);
 #pragma unroll
       for (int ib = 0; ib < 4; ++ib)  // W(J+1, J) = L(J+1, J) D_J: this wave's rows r
 #pragma unroll
@@ -715,6 +747,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       stamp(64 + 13 * J + 12);
     }
   });
+  if constexpr (CLK)
+    if (blockIdx.x == 0 && threadIdx.x >= 256 && threadIdx.x < 320) ws_clk[threadIdx.x - 192] = clk_sh[threadIdx.x - 192];
 }
 
 // ---------------------------------------------------------------------------
@@ -953,6 +987,10 @@ hipError_t ldlt_factor_small_variant(int snw, double* K, int64_t ld, int N, doub
         if (J < 4) std::printf(" | pre-T1 %llu T2 %llu", h[64 + 13 * J + 11] - t0, h[64 + 13 * J + 12] - t0);
         std::printf("\n");
       }
+      std::printf("ws J=1 leftovers (trsm, store, load_at):");
+      for (int k = 20; k < 29; ++k) std::printf(" %llu", h[k] - t0);
+      std::printf(" | M1 %llu %llu %llu | transition trsm %llu store %llu\n", h[30] - t0, h[31] - t0, h[32] - t0,
+                  h[33] - t0, h[34] - t0);
     } else if (nb == 5) l(ldlt_small_ws_kernel<5>);
     else if (nb == 4) l(ldlt_small_ws_kernel<4>);
     else if (nb == 3) l(ldlt_small_ws_kernel<3>);
