@@ -28,7 +28,7 @@ import sys
 from collections import defaultdict
 
 FACTOR_KERNELS = ("gemm_nt_kernel", "gemm_nt_glds_kernel", "panel_kernel", "panel_chain_kernel", "panel_rows_kernel", "solve_prep_kernel",
-                  "ldlt_small_kernel", "ldlt_small_pair_kernel",  # (these two: C4's batched factor)
+                  "ldlt_small_kernel", "ldlt_small_pair_kernel", "ldlt_small_ws_kernel", "ldlt_small_left_kernel",  # (the small.hip kernels: C4's batched factor)
                   )
 
 
