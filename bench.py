@@ -175,8 +175,9 @@ def run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch):
                              "summary kernel + the all-reduce; phases from a second, instrumented pass"},
         "phase_ms_per_step": ({k: ph[k] / args.steps for k in ("step", "assemble", "factor", "solve", "eval")}
                               if ph else None),
-        "roofline": {"bound": "mfma", "kernel": "batched factor phase (whole LDL^T of each QP in one 8-wave "
-                                                "workgroup, fp64 MFMA)",
+        "roofline": {"bound": "mfma", "kernel": "batched factor phase (whole left-looking LDL^T of each QP in "
+                                                "one 8-wave workgroup: diagonal chain on waves 0-3, tiles on "
+                                                "4-7; fp64 MFMA)",
                      "achieved": fac, "peak": FP64_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": fac / FP64_MFMA_PEAK_TFLOPS if fac else None, "traffic": None,
                      "note": "B * N^3/3 over the factor phase (HIP events), rank 0"},
