@@ -523,18 +523,46 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
   // A(c, J)^T (lower part for the diagonal tile c == J); rows r past the matrix read as 0
   // (32-bit element offsets from the QP's base: one VGPR per address, immediate column offsets)
   const unsigned ldu = (unsigned)ld;
+  // 4 x 4 transpose across the lane groups q = l >> 4 (v_permlane32_swap,
+  // then v_permlane16_swap, per 32-bit half): u[t] of group q -> u[q] of group t
+  auto transpose4 = [&](double(&u)[4]) {
+    unsigned lo[4], hi[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      lo[t] = __double2loint(u[t]);
+      hi[t] = __double2hiint(u[t]);
+    }
+    auto sw = [](unsigned(&v)[4], int i, int j, bool s32) {
+      const auto r = s32 ? __builtin_amdgcn_permlane32_swap(v[i], v[j], false, false)
+                         : __builtin_amdgcn_permlane16_swap(v[i], v[j], false, false);
+      v[i] = r[0];
+      v[j] = r[1];
+    };
+    sw(lo, 0, 2, true), sw(lo, 1, 3, true), sw(lo, 0, 1, false), sw(lo, 2, 3, false);
+    sw(hi, 0, 2, true), sw(hi, 1, 3, true), sw(hi, 0, 1, false), sw(hi, 2, 3, false);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) u[t] = __hiloint2double(hi[t], lo[t]);
+  };
+  // A(c, J)^T (lower part for the diagonal tile c == J); rows r past the
+  // matrix read as 0.  Each lane loads 32 contiguous bytes per 16-column
+  // block (two 16-byte loads instead of four 8-byte ones) and the lane groups
+  // exchange them into the accumulator layout.
   auto load_at = [&](int c, int J, acc_t(&a)[4], int tid) {
     const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), rows = nrows(c);
-    const unsigned o = (unsigned)(64 * c + (r < rows ? r : 0)) * ldu + 64 * J + q;
+    const double* src = KS + ((unsigned)(64 * c + (r < rows ? r : 0)) * ldu + 64 * J + 4 * q);
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
+    for (int jb = 0; jb < 4; ++jb) {
+      const double2 x0 = *reinterpret_cast<const double2*>(src + 16 * jb);
+      const double2 x1 = *reinterpret_cast<const double2*>(src + 16 * jb + 2);
+      double u[4] = {x0.x, x0.y, x1.x, x1.y};  // A[r][16 jb + 4 q + t]
+      transpose4(u);                           // A[r][16 jb + q + 4 g]
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int j = 16 * jb + q + 4 * g;
         const bool in = r < rows && (c != J || j <= r);  // (the upper part of A(J, J) is read, not used)
-        const double v = KS[o + 16 * jb + 4 * g];
-        a[jb][g] = in ? v : 0.0;
+        a[jb][g] = in ? u[g] : 0.0;
       }
+    }
   };
   // this lane's L(c, Kb) row r, columns 16 u + 4 q + t (the k order of the
   // accumulation MFMAs): 32 contiguous bytes per u
@@ -598,13 +626,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       for (int g = 0; g < 4; ++g) buf[r * DS + 16 * ib + q + 4 * g] = lt[ib][g];
   };
   auto rows_out = [&](int c, int J, const double* buf, int tid) {  // this wave's rows of buf -> L(c, J)
-    const int l = tid & 63, w = (tid >> 6) - 4, rows = nrows(c);
-    unsigned o = (unsigned)(64 * c + 16 * w) * ldu + 64 * J + l;
+    // two rows per instruction, 16 bytes per lane (half the memory instructions)
+    const int l = tid & 63, w = (tid >> 6) - 4, rows = nrows(c), h = l >> 5, col = 2 * (l & 31);
+    unsigned o = (unsigned)(64 * c + 16 * w + h) * ldu + 64 * J + col;
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (16 * w + i < rows) K[o] = buf[(16 * w + i) * DS + l];
-      o += ldu;
-      if ((i & 3) == 3) __builtin_amdgcn_sched_barrier(0);
+    for (int i = 0; i < 16; i += 2) {
+      const int r = 16 * w + i + h;
+      if (r < rows) {
+        double2 x;
+        x.x = buf[r * DS + col];
+        x.y = buf[r * DS + col + 1];
+        *reinterpret_cast<double2*>(K + o) = x;
+      }
+      o += 2 * ldu;
+      if ((i & 7) == 6) __builtin_amdgcn_sched_barrier(0);
     }
   };
   auto store_l = [&](int c, int J, const acc_t(&lt)[4], double* buf, int tid) {
@@ -614,22 +649,29 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
   // plain copies of L(J, Kb) -> W0 and L(J+1, Kb) -> W1 (256 threads; rows
   // past the matrix zero): loads into v, then the LDS stores
   // (W1P = false: only the W0 part -- W1 already holds its tile)
-  auto stage_load = [&](int J, int Kb, double(&v)[32], bool w1p, int tid) {
-    const int t = tid - 256, col = t & 63, rows1 = nrows(J + 1);
+  // (16 bytes per lane: two rows per instruction)
+  auto stage_load = [&](int J, int Kb, double2(&v)[16], bool w1p, int tid) {
+    const int t = tid - 256, col = 2 * (t & 31), rows1 = nrows(J + 1);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = (t >> 6) + 4 * i;
-      v[i] = K[(unsigned)(64 * J + r) * ldu + 64 * Kb + col];  // (block J < NB - 1: full)
-      if (w1p) v[16 + i] = K[(unsigned)(64 * (J + 1) + (r < rows1 ? r : 0)) * ldu + 64 * Kb + col];
+    for (int i = 0; i < 8; ++i) {
+      const int r = (t >> 5) + 8 * i;
+      v[i] = *reinterpret_cast<const double2*>(K + ((unsigned)(64 * J + r) * ldu + 64 * Kb + col));  // (J < NB-1: full)
+      if (w1p)
+        v[8 + i] = *reinterpret_cast<const double2*>(
+            K + ((unsigned)(64 * (J + 1) + (r < rows1 ? r : 0)) * ldu + 64 * Kb + col));
     }
   };
-  auto stage_put = [&](const double(&v)[32], int J, bool w1p, int tid) {
-    const int t = tid - 256, col = t & 63, rows1 = nrows(J + 1);
+  auto stage_put = [&](const double2(&v)[16], int J, bool w1p, int tid) {
+    const int t = tid - 256, col = 2 * (t & 31), rows1 = nrows(J + 1);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      const int r = (t >> 6) + 4 * i;
-      W0[r * DS + col] = v[i];
-      if (w1p) W1[r * DS + col] = r < rows1 ? v[16 + i] : 0.0;
+    for (int i = 0; i < 8; ++i) {
+      const int r = (t >> 5) + 8 * i;
+      W0[r * DS + col] = v[i].x;
+      W0[r * DS + col + 1] = v[i].y;
+      if (w1p) {
+        W1[r * DS + col] = r < rows1 ? v[8 + i].x : 0.0;
+        W1[r * DS + col + 1] = r < rows1 ? v[8 + i].y : 0.0;
+      }
     }
   };
   static_for<NB>([&](auto jc) {
@@ -663,7 +705,8 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       // the first K step's operands, loaded under the leftovers: L(J, 0)
       // (earlier windows) and L(J+1, 0) -- for J = 1 that tile is the first
       // leftover's own result, transposed straight into W1 below
-      double stg[32], bfa[16], bfb[16];
+      double2 stg[16];
+      double bfa[16], bfb[16];
       stage_load(J, 0, stg, J > 1, tid);
       // X_{J-1} stays intact until diag(J)'s 4th interval (NL <= 3)
       static_for<NL>([&](auto cc) {
