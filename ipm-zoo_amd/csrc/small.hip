@@ -17,6 +17,7 @@
 // memory waits overlap the other's MFMAs; operand tiles for the next step
 // are loaded into registers while the current one computes.
 #include <cstdio>
+#include <type_traits>
 
 #include "ipmz.h"
 #include "common.h"
@@ -450,7 +451,8 @@ __host__ __device__ constexpr int ws_window_bars(int NB, int J) {
 }
 __host__ __device__ constexpr bool ws_schedule_fits(int NB) {
   for (int J = 0; J < NB; ++J)
-    if (ws_window_bars(NB, J) > WS_NBAR || (J >= 1 && NB - J - 1 > 3)) return false;  // leftovers before diag's X write
+    // (two intervals left for the transition's first TRSM rows; leftovers before diag's X write)
+    if (ws_window_bars(NB, J) > WS_NBAR - 2 || (J >= 1 && NB - J - 1 > 3)) return false;
   return true;
 }
 static_assert(ws_schedule_fits(2) && ws_schedule_fits(3) && ws_schedule_fits(4) && ws_schedule_fits(5), "WS schedule");
@@ -597,23 +599,30 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
   };
   // L^T = diag(1 / d) X T^T: X (lower, LDS) against T^T's blocks as B
   // fragments; lt[ib] rows i = 16 ib + q + 4 g; d: the pivots in LDS
-  auto trsm = [&](const acc_t(&a)[4], acc_t(&lt)[4], const double* d, int tid) {
+  // rows [ib0, ib1) of it only (the transition's TRSM starts in the window,
+  // as soon as those rows of X_J are final)
+  auto trsm_rows = [&](const acc_t(&a)[4], acc_t(&lt)[4], const double* d, int tid, auto ib0c, auto ib1c) {
+    constexpr int IB0 = decltype(ib0c)::value, IB1 = decltype(ib1c)::value;
     const int l = tid & 63, q = l >> 4;
     const double* xr = X + (l & 15) * DS + q;
 #pragma unroll
-    for (int ib = 0; ib < 4; ++ib) lt[ib] = (acc_t){0.0, 0.0, 0.0, 0.0};
+    for (int ib = IB0; ib < IB1; ++ib) lt[ib] = (acc_t){0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int jb = 0; jb < 4; ++jb)
+    for (int jb = 0; jb < IB1; ++jb)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
 #pragma unroll
-        for (int ib = jb; ib < 4; ++ib) lt[ib] = MF::mma(xr[16 * ib * DS + 16 * jb + 4 * g], a[jb][g], lt[ib]);
+        for (int ib = (jb > IB0 ? jb : IB0); ib < IB1; ++ib)
+          lt[ib] = MF::mma(xr[16 * ib * DS + 16 * jb + 4 * g], a[jb][g], lt[ib]);
         __builtin_amdgcn_sched_barrier(0);
       }
 #pragma unroll
-    for (int ib = 0; ib < 4; ++ib)
+    for (int ib = IB0; ib < IB1; ++ib)
 #pragma unroll
       for (int g = 0; g < 4; ++g) lt[ib][g] *= fast_rcp(d[16 * ib + q + 4 * g]);
+  };
+  auto trsm = [&](const acc_t(&a)[4], acc_t(&lt)[4], const double* d, int tid) {
+    trsm_rows(a, lt, d, tid, std::integral_constant<int, 0>{}, std::integral_constant<int, 4>{});
   };
   // L(c, J) rows r of this wave: transposed through the wave's own rows of a
   // free LDS tile, then stored a whole 512-byte row per instruction (the
@@ -752,12 +761,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
         });
       });
     }
+    // rows 0..47 of L(J+1, J) in the window's 9th interval: X_J's block rows
+    // 0..2 are final after diag(J)'s 8th barrier (its inverse tiles X_22,
+    // X_20, X_21 in the 8th interval), D_J after the third column pass
+    acc_t lt[4];
+    if constexpr (J + 1 < NB) {
+      while (nb < WS_NBAR - 2) bar(false);
+      trsm_rows(T[J], lt, dsh, tid, std::integral_constant<int, 0>{}, std::integral_constant<int, 3>{});
+    }
     while (nb < WS_NBAR) bar(false);
     // ======== transition: L(J+1, J) and the last term of T(J+1, J+1) -> M
     if constexpr (J + 1 < NB) {
       const int l = tid & 63, q = l >> 4, r = 16 * ((tid >> 6) - 4) + (l & 15), b = nrows(J + 1);
-      acc_t lt[4];
-      trsm(T[J], lt, dsh, tid);  // X_J, D_J final after diag(J)'s last barrier
+      // its last block row (X_J final after diag(J)'s last barrier)
+      trsm_rows(T[J], lt, dsh, tid, std::integral_constant<int, 3>{}, std::integral_constant<int, 4>{});
       if constexpr (J == 1) stamp(33);
       put_l(lt, W0, tid);  // L(J+1, J) -> global from W0 in the next window's first interval
       if constexpr (J == 1) stamp(34);
