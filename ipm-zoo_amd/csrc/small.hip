@@ -614,7 +614,7 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
 #pragma unroll
         for (int ib = (jb > IB0 ? jb : IB0); ib < IB1; ++ib)
           lt[ib] = MF::mma(xr[16 * ib * DS + 16 * jb + 4 * g], a[jb][g], lt[ib]);
-        __builtin_amdgcn_sched_barrier(0);
+        if (g == 3) __builtin_amdgcn_sched_barrier(0);  // (per block column: registers; chains interleave)
       }
 #pragma unroll
     for (int ib = IB0; ib < IB1; ++ib)
