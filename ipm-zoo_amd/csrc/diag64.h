@@ -104,6 +104,47 @@ __device__ __forceinline__ void colpass16(double* M, double* dsh, int p, int lan
   }
   if (lane < 16) dsh[16 * p + lane] = dreg;
 }
+// The same pass with the pivot's reciprocal off the critical chain: every
+// lane computes the (zero-rule) reciprocal of its own v[k+1] as soon as step
+// k has updated it -- lane k+1's value is the next pivot -- so the v_rcp +
+// Newton chain runs beside step k's remaining updates, and step k+1 starts
+// from two readlanes.  The same operations on the same values: bitwise the
+// same factor.
+__device__ __forceinline__ void colpass16_spec(double* M, double* dsh, int p, int lane) {
+  const int row = 16 * p + lane;
+  const bool act = row < 64;
+  const int rr = act ? row : 63;
+  double v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = M[rr * DS + 16 * p + j];
+  double dreg = 1.0, dl, rl;
+  auto piv = [&](double x) {
+    dl = x == 0.0 ? 1e-8 : x;  // LinearSolvers.cpp:26-28
+    rl = fast_rcp(dl);
+  };
+  piv(v[0]);
+  static_for<16>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const double dk = readlane_t(dl, k);
+    const double rdk = readlane_t(rl, k);
+    dreg = lane == k ? dk : dreg;
+    const double l = lane > k ? v[k] * rdk : 0.0;
+    if constexpr (k + 1 < 16) {
+      v[k + 1] = fma(-l, readlane_t(v[k], k + 1), v[k + 1]);
+      piv(v[k + 1]);
+    }
+    static_for<(k + 2 < 16 ? 14 - k : 0)>([&](auto jc) {
+      constexpr int j = k + 2 + decltype(jc)::value;
+      v[j] = fma(-l, readlane_t(v[k], j), v[j]);  // w_j = A[j][k], row j = lane j
+    });
+    v[k] = lane > k ? l : v[k];
+  });
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) M[rr * DS + 16 * p + j] = v[j];
+  }
+  if (lane < 16) dsh[16 * p + lane] = dreg;
+}
 // X_pp = L_pp^{-1} of a unit-lower 16 x 16 tile: lane c (mod 16) solves
 // L x = e_c right-looking (L entries are wave-uniform LDS broadcasts)
 __device__ __forceinline__ void inv16(const double* Lt, double* Xt, int lane) {
@@ -154,7 +195,7 @@ struct NoHook {
 // later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
 // column pass (the batched factor writes the previous block's L^{-1} there).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
-          bool WB_LINV = true, typename IDLE0 = NoHook>
+          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 0>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
@@ -213,7 +254,11 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     tile_store(Xt(p, j), acc, lane);
   };
   auto xoff = [&](int p, int j) { xmul(p, j, xsum(p, j)); };  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
-  if (wave == 0) colpass16(M, dsh, 0, lane);
+  auto colpass = [&](int p) {
+    if constexpr (CPV == 1) colpass16_spec(M, dsh, p, lane);
+    else colpass16(M, dsh, p, lane);
+  };
+  if (wave == 0) colpass(0);
   else idle0();
   __syncthreads();
   clk();
@@ -226,7 +271,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     // with block column p, and the inverse tiles of block row p (X_pp, then
     // X_pj, j < p, on one wave: they depend on X_pp) -- all in the pass's shadow
     if (wave == 0) {
-      colpass16(M, dsh, p + 1, lane);
+      colpass(p + 1);
     } else if (wave < 4) {
       if (p == 0) {  // tiles (2,2), (3,2), (3,3) on waves 1..3; X_00 after wave 1's tile
         const int i = wave == 1 ? 2 : 3, j = wave == 3 ? 3 : 2;

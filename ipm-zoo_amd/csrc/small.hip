@@ -499,13 +499,13 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
         }
       };
       if (J == 0)
-        diag64_body<false, false, double, false, 4, NoHook, false>(K, ld, 0, b, D, Linv, info, M, X, dsh, nullptr,
+        diag64_body<false, false, double, false, 4, NoHook, false, NoHook, 1>(K, ld, 0, b, D, Linv, info, M, X, dsh, nullptr,
                                                                    NoHook(), KS, tid);
       else if (J < NB - 1)
-        diag64_body<false, false, double, true, 4, NoHook, false>(K, ld, 64 * J, b, D, Linv, info, M, X, dsh,
+        diag64_body<false, false, double, true, 4, NoHook, false, decltype(linv_prev), 1>(K, ld, 64 * J, b, D, Linv, info, M, X, dsh,
                                                                   nullptr, NoHook(), nullptr, tid, linv_prev);
       else  // the last block writes its own L^{-1}
-        diag64_body<false, false, double, true, 4, NoHook, true>(K, ld, 64 * J, b, D, Linv + (int64_t)J * 64 * 64, info,
+        diag64_body<false, false, double, true, 4, NoHook, true, decltype(linv_prev), 1>(K, ld, 64 * J, b, D, Linv + (int64_t)J * 64 * 64, info,
                                                                  M, X, dsh, nullptr, NoHook(), nullptr, tid, linv_prev);
       stamp(3 * J + 1);
       if (J == NB - 1) break;

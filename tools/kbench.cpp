@@ -139,15 +139,31 @@ int main(int argc, char** argv) {
       }
     return 0;
   }
-  if (mode == "diagclk") {  // stage clocks of the 64 x 64 diagonal factor
-    unsigned long long clk[32];
-    for (int rep = 0; rep < 3; ++rep) {
-      CK(ipmz::diag_clock_probe(K, ld, D, Linv, info, clk, st));
-      CK(hipStreamSynchronize(st));
+  if (mode == "diagclk") {  // stage clocks of the 64 x 64 diagonal factor; column passes 0 (as shipped), 1 (variant)
+    std::vector<double> ref;
+    for (int cpv : {0, 1, 0, 1}) {
+      unsigned long long clk[32];
+      for (int rep = 0; rep < 3; ++rep) {
+        hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+        CK(ipmz::diag_clock_probe(K, ld, D, Linv, info, clk, st, cpv));
+        CK(hipStreamSynchronize(st));
+      }
+      std::vector<double> hk(64 * ld), hd(64), hl(64 * 64);
+      CK(hipMemcpy(hk.data(), K, 64 * ld * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hd.data(), D, 64 * 8, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hl.data(), Linv, 64 * 64 * 8, hipMemcpyDeviceToHost));
+      std::vector<double> cur(hd);
+      for (int i = 0; i < 64; ++i)
+        for (int j = 0; j < i; ++j) cur.push_back(hk[i * ld + j]);
+      cur.insert(cur.end(), hl.begin(), hl.end());
+      double dmax = 0;
+      if (ref.empty()) ref = cur;
+      else
+        for (size_t i = 0; i < cur.size(); ++i) dmax = std::max(dmax, std::fabs(cur[i] - ref[i]));
+      std::printf("diag64 cpv=%d stage clocks (s_memtime ticks from start):", cpv);
+      for (unsigned i = 1; i < clk[31] && i < 31; ++i) std::printf(" %llu", clk[i] - clk[0]);
+      std::printf("  (max |d| vs the first: %.2e)\n", dmax);
     }
-    std::printf("diag64 stage clocks (s_memtime ticks from start):");
-    for (unsigned i = 1; i < clk[31] && i < 31; ++i) std::printf(" %llu", clk[i] - clk[0]);
-    std::printf("\n");
     return 0;
   }
   if (mode == "small") {  // batched one-workgroup factor (C4)

@@ -108,13 +108,16 @@ hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc,
 
 // stage clocks (s_memtime) of one diag64_body run: entries [0, clk[31]) of out
 __device__ unsigned long long g_diag_clk[32];
+template <int CPV>
 __global__ __launch_bounds__(256) void diag_clock_kernel(double* K, int64_t ld, double* D, double* Linv, int* info) {
   __shared__ double M[64 * DS], X[64 * DS], dsh[64];
-  diag64_body<false>(K, ld, 0, 64, D, Linv, info, M, X, dsh, g_diag_clk);
+  diag64_body<false, false, double, false, 4, NoHook, true, NoHook, CPV>(K, ld, 0, 64, D, Linv, info, M, X, dsh,
+                                                                        g_diag_clk);
 }
 hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,
-                            hipStream_t st) {
-  hipLaunchKernelGGL(diag_clock_kernel, dim3(1), dim3(256), 0, st, K, ld, D, Linv, info);
+                            hipStream_t st, int cpv) {
+  if (cpv == 1) hipLaunchKernelGGL(diag_clock_kernel<1>, dim3(1), dim3(256), 0, st, K, ld, D, Linv, info);
+  else hipLaunchKernelGGL(diag_clock_kernel<0>, dim3(1), dim3(256), 0, st, K, ld, D, Linv, info);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_diag_clk), sizeof(unsigned long long) * 32, 0,
