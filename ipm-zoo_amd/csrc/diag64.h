@@ -104,7 +104,7 @@ __device__ __forceinline__ void colpass16(double* M, double* dsh, int p, int lan
   }
   if (lane < 16) dsh[16 * p + lane] = dreg;
 }
-// The same pass with the pivot's reciprocal off the critical chain: every
+// The pass every factor uses (CPV = 1): the pivot's reciprocal off the critical chain: every
 // lane computes the (zero-rule) reciprocal of its own v[k+1] as soon as step
 // k has updated it -- lane k+1's value is the next pivot -- so the v_rcp +
 // Newton chain runs beside step k's remaining updates, and step k+1 starts
@@ -195,7 +195,7 @@ struct NoHook {
 // later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
 // column pass (the batched factor writes the previous block's L^{-1} there).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
-          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 0>
+          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
