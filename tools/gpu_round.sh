@@ -35,6 +35,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     # panel path's cross-launch hand-offs can time out under the profiler)
     pmcf_mops) step ${PMCW:-c3}_pmcf_mops 240 rocprofv3 --pmc $([ "${PMCW:-c3}" = c5 ] && echo SQ_INSTS_VALU_MFMA_MOPS_F32 || echo SQ_INSTS_VALU_MFMA_MOPS_F64) -d "$OUT/${PMCW:-c3}_pmcf_mops" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
     pmcf_busy) step ${PMCW:-c3}_pmcf_busy 240 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CU_CYCLES -d "$OUT/${PMCW:-c3}_pmcf_busy" -o run --output-format csv -- python bench.py --workload ${PMCW:-c3} --steps 1 --warmup 0 --no-cpu-baseline --no-instrumented --no-batched --no-configs ;;
+    # (kbench / sgemm_bench are listed in .gpurunignore: drop those lines to run the experiment steps)
     kbench) step kbench 300 ipm-zoo_amd/build/kbench 11264 ;;
     sgemm) step sgemm 200 ipm-zoo_amd/build/sgemm_bench ${SGEMM_R:-15872} ${SGEMM_V:-} ;;
     smallv) step smallv 100 ipm-zoo_amd/build/kbench 320 smallv ;;
