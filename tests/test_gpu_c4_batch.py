@@ -191,6 +191,35 @@ def test_c4_left_kernel_matches_right_looking(ctx):
                 assert np.abs(g - r).max() < 1e-9 * max(1.0, np.abs(r).max()), (it, i, w)
 
 
+@pytest.mark.parametrize("n,m", [(52, 13), (100, 28), (103, 26), (150, 42), (205, 51), (256, 1), (255, 64),
+                                 (256, 64), (257, 64)])
+def test_left_factor_block_counts_vs_right_looking(ctx, n, m):
+    """The wave-specialized factor for every block count it handles (N = 65 ..
+    320: 2..5 blocks, ragged and full last blocks) and the plain left-looking
+    one just past it (N = 321), against the right-looking factor on the same
+    batch: the same Newton directions to rounding."""
+    B = 6
+
+    def run(kernel):
+        bt = I.Batch(n, m, 0, B, ctx)
+        bt.set_factor_kernel(kernel)
+        bt.generate(4000 + n)
+        out = []
+        for _ in range(2):
+            bt.step()
+            out.append([(bt.state(i, 1), bt.state(i, 2)) for i in range(B)])
+        bt.close()
+        return out
+
+    left, one = run(I.Batch.FACTOR_LEFT), run(I.Batch.FACTOR_ONE)
+    for it in range(2):
+        for i in range(B):
+            for w in range(2):
+                g, r = left[it][i][w], one[it][i][w]
+                assert np.abs(g[:n] - r[:n]).max() < DX_TOL, (it, i, w)
+                assert np.abs(g - r).max() < 1e-9 * max(1.0, np.abs(r).max()), (it, i, w)
+
+
 def test_c4_pair_kernel_rejected_when_not_coresident(ctx):
     bt = I.Batch(N_, M_, 0, B_, ctx)
     with pytest.raises(I.IpmzError, match="2 \\* batch <= #CU"):
