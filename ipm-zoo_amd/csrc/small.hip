@@ -716,7 +716,20 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       // leftover's own result, transposed straight into W1 below
       double2 stg[16];
       double bfa[16], bfb[16];
-      stage_load(J, 0, stg, J > 1, tid);
+      if constexpr (J == 1) {
+        // L(1, 0) is the tile the other waves are storing just above (no
+        // barrier in between: a global load here could return the old
+        // contents of K); W0 still holds it in the staging layout
+        const int t = tid - 256, col = 2 * (t & 31);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int r = (t >> 5) + 8 * i;
+          stg[i].x = W0[r * DS + col];
+          stg[i].y = W0[r * DS + col + 1];
+        }
+      } else {
+        stage_load(J, 0, stg, true, tid);
+      }
       // X_{J-1} stays intact until diag(J)'s 4th interval (NL <= 3)
       static_for<NL>([&](auto cc) {
         constexpr int c = J + 1 + decltype(cc)::value;

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -244,6 +245,62 @@ int main(int argc, char** argv) {
         CK(hipFree(Lb));
         CK(hipFree(Wb));
       }
+    return 0;
+  }
+  if (mode == "smalldet") {  // kbench 320 smalldet v1 v2 ...: run-to-run bitwise determinism of the small factors
+    const int B = 1024, R = 40;
+    for (int a = 3; a < argc; ++a) {
+      const int snw = std::atoi(argv[a]);
+      double *Kb, *Db, *Lb, *Wb;
+      const int64_t sK = ld * N, sL = (int64_t)((N + 63) / 64) * 64 * 64;
+      CK(hipMalloc(&Kb, sK * B * 8));
+      CK(hipMalloc(&Db, (int64_t)N * B * 8));
+      CK(hipMalloc(&Lb, sL * B * 8));
+      CK(hipMalloc(&Wb, (int64_t)N * 64 * B * 8));
+      ipmz::BatchStrides bs;
+      bs.B = B;
+      bs.sK = sK;
+      bs.sD = N;
+      bs.sL = sL;
+      bs.sW = (int64_t)N * 64;
+      std::vector<double> rK(sK * B), rD((int64_t)N * B), hK(sK * B), hD((int64_t)N * B);
+      int bad_runs = 0;
+      for (int rep = 0; rep <= R; ++rep) {
+        for (int q = 0; q < B; ++q) hipLaunchKernelGGL(fill_qd, dim3(64), dim3(256), 0, st, Kb + q * sK, ld, N, 7ull + q);
+        CK(ipmz::ldlt_factor_small_variant(snw, Kb, ld, N, Db, Lb, Wb, info, st, bs));
+        CK(hipStreamSynchronize(st));
+        std::vector<double>& K_ = rep ? hK : rK;
+        std::vector<double>& D_ = rep ? hD : rD;
+        CK(hipMemcpy(K_.data(), Kb, sK * B * 8, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(D_.data(), Db, (int64_t)N * B * 8, hipMemcpyDeviceToHost));
+        if (!rep) continue;
+        int badq = 0, first = -1, fi = -1, fj = -1;
+        for (int q = 0; q < B; ++q) {
+          bool bad = std::memcmp(&hD[(int64_t)q * N], &rD[(int64_t)q * N], N * 8) != 0;
+          for (int i = 0; i < N && !bad; ++i)
+            for (int j = 0; j < i; ++j)
+              if (std::memcmp(&hK[q * sK + i * ld + j], &rK[q * sK + i * ld + j], 8)) {
+                bad = true;
+                if (first < 0) { fi = i; fj = j; }
+                break;
+              }
+          if (bad) {
+            ++badq;
+            if (first < 0) first = q;
+          }
+        }
+        if (badq) {
+          ++bad_runs;
+          std::printf("smalldet variant %d run %d: %d QPs differ (first QP %d, first L entry (%d,%d))\n", snw, rep, badq,
+                      first, fi, fj);
+        }
+      }
+      std::printf("smalldet variant %d: %d of %d runs differ bitwise from run 0\n", snw, bad_runs, R);
+      CK(hipFree(Kb));
+      CK(hipFree(Db));
+      CK(hipFree(Lb));
+      CK(hipFree(Wb));
+    }
     return 0;
   }
   if (mode == "gvar") {  // trailing-GEMM tile variants: kbench N gvar v1 v2 ...
