@@ -112,6 +112,32 @@ def test_c4_graph_replay_vs_eager_and_oracle(ctx):
     eb.close()
 
 
+def test_c4_eager_steps_run_to_run_bitwise(ctx):
+    """Three batches from the same seed, 400 eager steps each (restarting
+    converged QPs, so every QP is factored ~60 times from ever new iterates):
+    the scalars of all three agree bitwise after every step.  A guard against
+    a race between the waves of the small factor: the wave-specialized kernel
+    once restaged L(1, 0) from global memory with no barrier after the other
+    waves' stores of it, and a QP now and then picked up the previous step's
+    tile (tools/det_graph.py: 1 of 10 twelve-step trials differed before the
+    fix, 0 of 30 after; this test at 200 steps failed at step 91 on the
+    library built before the fix and passed after it; profiles/r04_race/)."""
+    steps = 400
+    bats = [I.Batch(N_, M_, 0, B_, ctx) for _ in range(3)]
+    for b in bats:
+        b.generate(0)
+    for it in range(steps):
+        sc = []
+        for b in bats:
+            b.step(I.STEP_RESTART_IF_CONVERGED)
+            sc.append(b.batch_scalars())
+        for r in (1, 2):
+            bad = np.unique(np.nonzero(sc[0] != sc[r])[0])
+            assert bad.size == 0, (it, r, bad[:8])
+    for b in bats:
+        b.close()
+
+
 def _run(ctx, B, seed0, steps, kernel=None):
     bt = I.Batch(N_, M_, 0, B, ctx)
     if kernel is not None:
