@@ -1,6 +1,6 @@
 """Config C4 on the path bench.py times: a batch of 1024 QPs (n = 256, m = 64,
 KKT N = 320), where every batch > #CU / 2 runs the one-workgroup-per-QP factor
-(ldlt_small_kernel<8>, small.hip) and the 8-wave one-workgroup solve
+(ldlt_small_ws_kernel<5>, small.hip) and the 8-wave one-workgroup solve
 (trsv_small_kernel<8>, trsv.hip) -- the kernels of the `batched` bench line.
 
 Each QP is one Optimizer::solve_quasi_definite_ body
