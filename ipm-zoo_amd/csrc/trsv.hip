@@ -334,12 +334,13 @@ __global__ __launch_bounds__(64 * NW) void trsv_small_kernel(const double* __res
   const int Np = (N + 63) & ~63;
   double* bv = sm;                 // rhs, then x
   double* yv = sm + Np;            // y, then z
-  // the 16-wave kernel (a CU per QP) loads K 16 bytes per lane: 2-3 % off its
-  // solve (B = 128: 0.070 -> 0.068 ms); the 8-wave one (QPs sharing CUs) was
-  // 3 % slower so (0.333 -> 0.343 ms at B = 1024, profiles/r04_race/solve16_*)
+  // K is read 16 bytes per lane in the backward sweep (two rows per
+  // instruction) and, in the 16-wave kernel (a CU per QP), the forward one:
+  // B = 128 solve 0.070 -> 0.068 ms, B = 1024 0.334 -> 0.332 ms; the 8-wave
+  // forward sweep was slower so (0.344 ms; profiles/r04_race/solve16_*)
   constexpr bool W16 = NW >= 16;
-  double* part = yv + Np;                     // (W16 ? 2 : 1) NW x 64 partial sums
-  double* ub = part + (W16 ? 2 : 1) * NW * 64; // 64: the block's u
+  double* part = yv + Np;          // 2 NW x 64 partial sums
+  double* ub = part + 2 * NW * 64; // 64: the block's u
   const int64_t q = blockIdx.x;
   K += q * sK;
   D += q * sD;
@@ -413,31 +414,24 @@ __global__ __launch_bounds__(64 * NW) void trsv_small_kernel(const double* __res
     double lv[RW];
 #pragma unroll
     for (int k = 0; k < RW; ++k) lv[k] = Lb[(wave * RW + k) * 64 + lane];
-    if constexpr (W16) {
-      // two rows per load instruction: half-wave h takes rows i = J0 + 64 +
-      // 2 wave + h (+ 2 NW), lane l & 31 columns 2 (l & 31), + 1 (16 bytes)
-      const int h = lane >> 5, c2 = 2 * (lane & 31);
-      double2 acc = {0.0, 0.0};
+    // two rows per load instruction: half-wave h takes rows i = J0 + 64 +
+    // 2 wave + h (+ 2 NW), lane l & 31 columns 2 (l & 31), + 1 (16 bytes)
+    const int h = lane >> 5, c2 = 2 * (lane & 31);
+    double2 acc = {0.0, 0.0};
 #pragma unroll 4
-      for (int i = J0 + 64 + 2 * wave + h; i < N; i += 2 * NW) {
-        const double2 kv = *reinterpret_cast<const double2*>(&K[(int64_t)i * ld + J0 + c2]);
-        const double xb = bv[i];
-        acc.x = fma(kv.x, xb, acc.x);
-        acc.y = fma(kv.y, xb, acc.y);
-      }
-      part[(2 * wave + h) * 64 + c2] = acc.x;
-      part[(2 * wave + h) * 64 + c2 + 1] = acc.y;
-    } else {
-      double acc = 0.0;
-#pragma unroll 8
-      for (int i = J0 + 64 + wave; i < N; i += NW) acc = fma(K[(int64_t)i * ld + J0 + lane], bv[i], acc);
-      part[wave * 64 + lane] = acc;
+    for (int i = J0 + 64 + 2 * wave + h; i < N; i += 2 * NW) {
+      const double2 kv = *reinterpret_cast<const double2*>(&K[(int64_t)i * ld + J0 + c2]);
+      const double xb = bv[i];
+      acc.x = fma(kv.x, xb, acc.x);
+      acc.y = fma(kv.y, xb, acc.y);
     }
+    part[(2 * wave + h) * 64 + c2] = acc.x;
+    part[(2 * wave + h) * 64 + c2 + 1] = acc.y;
     __syncthreads();
     if (wave == 0) {
       double s = 0.0;
 #pragma unroll
-      for (int w = 0; w < (W16 ? 2 : 1) * NW; ++w) s += part[w * 64 + lane];
+      for (int w = 0; w < 2 * NW; ++w) s += part[w * 64 + lane];
       ub[lane] = lane < bj ? yv[J0 + lane] - s : 0.0;
     }
     __syncthreads();
@@ -463,9 +457,9 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
   if (nbi == 64 && N <= TRSV_SMALL_NMAX) {
     // 16 waves when the batch leaves a CU per QP, 8 when QPs share CUs
     const bool wide = B <= device_cus();
-    if (wide && (ld & 1)) return hipErrorInvalidValue;  // (16-byte row loads: an even leading dimension)
+    if (ld & 1) return hipErrorInvalidValue;  // (16-byte row loads: an even leading dimension)
     const int NW = wide ? 16 : 8;
-    const size_t lds = (2 * (size_t)((N + 63) & ~63) + (wide ? 2 : 1) * NW * 64 + 64) * sizeof(double);
+    const size_t lds = (2 * (size_t)((N + 63) & ~63) + 2 * NW * 64 + 64) * sizeof(double);
     if (wide)
       hipLaunchKernelGGL((trsv_small_kernel<16>), dim3(B), dim3(64 * 16), lds, st, K, ld, N, D, Linv, b, sK, sD, sL,
                          sb);
