@@ -9,9 +9,11 @@ A "step" is one Newton iteration of Optimizer::solve_quasi_definite_
 (rhs + triangular solves + back-substitution), two ratio tests, mu_aff/sigma,
 update, and the next iterate's residuals/objective/mu.  A converged iterate
 is reset to the initial point on the device (no host round trip), so every
-timed step is a full Newton step.  The timed steps replay the step as a HIP
-graph (the production path); a second, instrumented pass with per-phase HIP
-events gives the phase split and the roofline numbers.
+timed step is a full Newton step.  The timed steps run the production path:
+HIP-graph replay for steps whose factor does not fork (C4's batches), eager
+launches with at most one step in flight for the look-ahead factor (C3, C2,
+C5) -- each line's config.timing says which; a second, instrumented pass with
+per-phase HIP events gives the phase split and the roofline numbers.
 
 Multi-GPU (torchrun, one process per GPU):
   * headline (C3): each rank solves its own independent QP -- the path does
@@ -20,6 +22,8 @@ Multi-GPU (torchrun, one process per GPU):
     (n=256, m=64) sharded over the ranks, strong scaling, with ONE all-reduce
     (MAX) of the device-computed convergence summary per step -- the only
     collective (SURVEY.md §8e);
+  * "batched_shard" sub-object (one GPU only): C4 at 128 QPs, the shard one
+    rank holds in the 8-GPU job, measured alone;
   * "configs" sub-object (default c3 run): C2 (normal equations, n=2048) and
     C5 (n=16384, fp32 factor + fp64 refinement), replicas like the headline,
     each with its own roofline and CPU baseline (--no-configs skips them).
@@ -90,7 +94,7 @@ def cpu_baselines(names):
     for w in names:
         wl = WORKLOADS[w]
         if wl.get("batch"):
-            procs[w] = cpu_start("batch", wl["n"], wl["m"], 10, 1)
+            procs[w] = cpu_start("batch", wl["n"], wl["m"], 10, 1, slot)  # its own core, like the step legs
         else:
             procs[w] = cpu_start("step", wl["n"], wl["m"], wl["p"], wl.get("sample_scale", 4), slot)
         slot += 1
@@ -189,6 +193,17 @@ def run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch):
         out["roofline"]["mfma"] = ftr.get("mfma")
     qp.close()
     return out
+
+
+def shard_line(I, ctx, args, dist, torch):
+    """C4 at one rank's shard of the 8-GPU job (1024 / 8 = 128 QPs), on this
+    one GPU: the per-GPU regime an 8-GPU run times (128 workgroups on 256
+    CUs, the 16-wave solve), graph-replayed like the 1024-QP line."""
+    sub = run_batched(I, ctx, args, 1, 0, dist, torch, WORKLOADS["c4"], 128)
+    sub["metric"] = "QP Newton steps/sec, one rank's C4 shard (128 of 1024 QPs, n=256) on one MI355X"
+    sub["config"]["note"] = ("the shard each rank holds when the 1024-QP batch runs on 8 GPUs, measured alone "
+                             "(no collective); 8 x this value bounds the 8-GPU C4 line")
+    return sub
 
 
 def run_single(I, ctx, args, world, dist, torch, workload):
@@ -364,6 +379,8 @@ def main():
     if nbatch:  # C4 as the headline
         head = run_batched(I, ctx, args, world, rank, dist, torch, wl, nbatch)
         out = dict(head)
+        if world == 1 and nbatch != 128 and not args.no_batched:
+            out["batched_shard"] = shard_line(I, ctx, args, dist, torch)
         out.update({"steps": args.steps, "warmup": args.warmup, "vs_baseline": None, "dtype": "f64",
                     "data": "synthetic (SURVEY.md §8d splitmix64 generator, generated in HBM; QP i: seed i)"})
         out["config"]["description"] = wl["desc"]
@@ -372,6 +389,8 @@ def main():
         out = run_single(I, ctx, args, world, dist, torch, args.workload)
         if not args.no_batched:
             out["batched"] = run_batched(I, ctx, args, world, rank, dist, torch, WORKLOADS["c4"], 1024)
+            if world == 1:
+                out["batched_shard"] = shard_line(I, ctx, args, dist, torch)
         if args.workload == "c3" and not args.no_configs:
             # the other single-GPU configs of BASELINE.json, each its own line item
             out["configs"] = {w: run_single(I, ctx, args, world, dist, torch, w) for w in ("c2", "c5")}

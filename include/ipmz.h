@@ -325,7 +325,11 @@ int ipmz_qp_set_reduction(ipmz_qp* qp, int reduction);
 int ipmz_batch_create(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int batch, ipmz_qp** out);
 int ipmz_batch_size(ipmz_qp* qp);
 /* Copy QP `index`'s data (build_environment's validation); call
- * ipmz_batch_initialize once every QP is loaded. */
+ * ipmz_batch_initialize once every QP is loaded.  A load leaves the batch
+ * uninitialized: ipmz_qp_step / ipmz_batch_solve return IPMZ_ERR_STATE until
+ * ipmz_batch_initialize has rebuilt the kept KKT matrix and the residuals
+ * from the new data (a step on the previous data's matrix would be silent
+ * corruption). */
 int ipmz_batch_load_host(ipmz_qp* qp, int index, const double* Q, const double* c, const double* A,
                          const double* l_A, const double* u_A, const double* C, const double* d, const double* l_x,
                          const double* u_x);
@@ -347,7 +351,8 @@ int ipmz_batch_summary(ipmz_qp* qp, double* dst_device);
 /* Step until every QP converged (converged QPs keep their iterate). */
 int ipmz_batch_solve(ipmz_qp* qp, int max_iter, int* iterations, int* converged_count);
 /* Which kernel factors a batch of small systems (N <= 1024, 64-column
- * blocks, one LDL^T): IPMZ_BATCH_FACTOR_AUTO (default: two workgroups per QP
+ * blocks, one LDL^T): IPMZ_BATCH_FACTOR_AUTO (default: the wave-specialized
+ * left-looking kernel for 64 < N <= 320; above that two workgroups per QP
  * when 2 * batch <= #CU, else the left-looking one), IPMZ_BATCH_FACTOR_ONE
  * (right-looking, one workgroup per QP), IPMZ_BATCH_FACTOR_PAIR (the same
  * right-looking factor on two workgroups per QP -- identical results to ONE;

@@ -1392,7 +1392,10 @@ int qp_status(ipmz_qp* s) {
     return ws_status(st, w.wsK, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step (normal equations)");
   }
   if (s->B == 1 && !s->eqnone) return ws_status(st, s->ws, s->N, nbo_for(s->ctx, s->N), s->ctx->nbi, "Newton step");
-  if (s->pflags && small_pair_eligible(s->B, s->N)) {
+  // only a step whose factor ran the two-workgroup kernel has a word to read
+  // (that kernel's launch zeroes it; the default wave-specialized factor at
+  // C4's N = 320 has no cross-workgroup hand-off and needs no sync here)
+  if (!s->eqnone && s->ctx->nbi == 64 && small_pair_used(s->small_kernel, s->pflags != nullptr, s->B, s->N)) {
     unsigned e = 0;
     HIP_OK(hipMemcpyAsync(&e, s->pflags + (size_t)s->B * IPMZ_PAIR_FLAGS, 4, hipMemcpyDeviceToHost, st));
     HIP_OK(hipStreamSynchronize(st));
@@ -1726,6 +1729,10 @@ int ipmz_batch_load_host(ipmz_qp* s, int index, const double* Q, const double* c
   int rc = check_index(s, index);
   if (rc) return rc;
   if ((rc = load_one(s, index, Q, c, A, lA, uA, C, d, lx, ux))) return rc;
+  // the kept KKT matrix K0 (off-diagonal part written only by
+  // evaluate_and_save) and the residuals still hold the old data: no step
+  // until ipmz_batch_initialize rebuilds them
+  s->loaded = false;
   return IPMZ_OK;
 }
 int ipmz_batch_initialize(ipmz_qp* s) {

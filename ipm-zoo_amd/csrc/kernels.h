@@ -70,6 +70,7 @@ struct BatchStrides {
 #define IPMZ_PAIR_FLAGS 32  // per QP: LW[16], DONE[16] (N <= IPMZ_SMALL_NMAX)
 // the batched factor of order N runs two workgroups per QP (given flags)
 bool small_pair_eligible(int B, int N);
+bool small_pair_used(int kern, bool have_flags, int B, int N);
 // small.hip: whole factor per workgroup (N <= IPMZ_SMALL_NMAX, nbi = 64;
 // W: N x 64 per QP)
 #define IPMZ_SMALL_NMAX 1024

@@ -988,14 +988,20 @@ __global__ __launch_bounds__(64 * SNW) void ldlt_small_pair_kernel(double* __res
 // waves fill a CU, so one workgroup per CU -- 2B <= #CU (B = 128 at 8 GPUs)
 bool small_pair_eligible(int B, int N) { return 2 * B <= device_cus() && N > 64 && N <= IPMZ_SMALL_NMAX; }
 
+// Does ldlt_factor_small_batched launch the two-workgroup kernel (the only
+// small factor with a cross-workgroup hand-off and an error word)?
+bool small_pair_used(int kern, bool have_flags, int B, int N) {
+  // a batch that leaves CUs idle: two workgroups per QP
+  const bool pair_ok = have_flags && small_pair_eligible(B, N);
+  const bool ws_ok = N > 64 && N <= 320;  // the wave-specialized left-looking factor beats the pair
+  return pair_ok && (kern == IPMZ_BATCH_FACTOR_PAIR || (kern == IPMZ_BATCH_FACTOR_AUTO && !ws_ok));
+}
+
 hipError_t ldlt_factor_small_batched(double* K, int64_t ld, int N, double* D, double* Linv, double* W, int* info,
                                      hipStream_t st, const BatchStrides& bs) {
   if (N <= 0 || bs.B <= 0) return hipSuccess;
   const int kern = bs.small_kernel;
-  // a batch that leaves CUs idle: two workgroups per QP (flags zeroed here)
-  const bool pair_ok = bs.pflags && small_pair_eligible(bs.B, N);
-  const bool ws_ok = N > 64 && N <= 320;  // the wave-specialized left-looking factor beats the pair
-  if (pair_ok && (kern == IPMZ_BATCH_FACTOR_PAIR || (kern == IPMZ_BATCH_FACTOR_AUTO && !ws_ok))) {
+  if (small_pair_used(kern, bs.pflags != nullptr, bs.B, N)) {  // flags and error word zeroed here
     hipError_t e = hipMemsetAsync(bs.pflags, 0, ((size_t)bs.B * IPMZ_PAIR_FLAGS + 1) * sizeof(unsigned), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(ldlt_small_pair_kernel<8>, dim3(2 * bs.B), dim3(64 * 8), 0, st, K, ld, N, D, Linv, W, info,

@@ -10,8 +10,10 @@ blocked form the parity tests use.
     python oracle/cpu_bench.py step  N_n N_m N_p SCALE [SLOT]  one Newton step at dims/SCALE, pinned to one core
                                                           (the SLOT-th available one), extrapolated per phase to
                                                           the full dims (N^3 / N^2); SCALE 1 = measured as is
-    python oracle/cpu_bench.py batch n m SECONDS WORKERS   QP-steps/s of WORKERS single-core processes (one QP
-                                                          per process at a time, 3 steps each, seeds disjoint)
+    python oracle/cpu_bench.py batch n m SECONDS WORKERS [START]  QP-steps/s of WORKERS single-core processes
+                                                          (one QP per process at a time, 3 steps each, seeds
+                                                          disjoint), worker i pinned to the (START+i)-th
+                                                          available core
 Prints one JSON object.
 """
 import json
@@ -87,10 +89,10 @@ def _batch_worker(args):
     return steps, wall
 
 
-def batch(n, m, seconds, workers):
+def batch(n, m, seconds, workers, start=0):
     model, nproc, avail = cpu_info()
     workers = max(1, min(workers, len(avail)))
-    jobs = [(avail[i], i, workers, n, m, seconds) for i in range(workers)]
+    jobs = [(avail[(start + i) % len(avail)], i, workers, n, m, seconds) for i in range(workers)]
     if workers == 1:
         res = [_batch_worker(jobs[0])]
     else:
@@ -109,7 +111,7 @@ def main():
     if mode == "step":
         out = step(*(int(a) for a in sys.argv[2:7]))
     elif mode == "batch":
-        out = batch(int(sys.argv[2]), int(sys.argv[3]), float(sys.argv[4]), int(sys.argv[5]))
+        out = batch(*(int(a) if i != 2 else float(a) for i, a in enumerate(sys.argv[2:7])))
     else:
         sys.exit(f"unknown mode {mode}")
     print(json.dumps(out))

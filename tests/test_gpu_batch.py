@@ -66,3 +66,38 @@ def test_batch_solve_all_matches_single(ctx):
         g.generate(300 + i)
         g.solve(100)
         assert np.abs(bt.state(i, 0) - g.vars()).max() < 1e-7, i
+
+
+def _data(q):
+    return I.Data(q["Q"], q["c"], q["lx"], q["ux"], q["A"], q["lA"], q["uA"], q["C"], q["d"])
+
+
+def test_batch_reload_host_needs_initialize(ctx):
+    """ipmz_batch_load_host leaves the batch uninitialized: the kept KKT matrix
+    K0 (off-diagonal part written once per data load) still holds the old data,
+    so a step before ipmz_batch_initialize is refused (IPMZ_ERR_STATE) instead
+    of factoring the old matrix; after it, every QP -- the reloaded one with
+    data the batch never saw -- steps like its own oracle run."""
+    n, m, B = 96, 24, 3
+    bt = I.Batch(n, m, 0, B, ctx)
+    qps = [oracle.gen_qp(n, m, 0, 700 + i) for i in range(B)]
+    for i, q in enumerate(qps):
+        bt.load_one(i, _data(q))
+    bt.initialize()
+    bt.step()
+    qps[1] = oracle.gen_qp(n, m, 0, 9999)  # new data for QP 1
+    bt.load_one(1, _data(qps[1]))
+    with pytest.raises(I.IpmzError):
+        bt.step()
+    bt.initialize()
+    orcs = [oracle.OracleQP(q) for q in qps]
+    for it in range(2):
+        for o in orcs:
+            o.iterate()
+        bt.step()
+        for i, o in enumerate(orcs):
+            for which, ref in ((1, o.daff()), (2, o.dir())):
+                got = bt.state(i, which)
+                assert np.abs(got[:n] - ref[:n]).max() < DX_TOL, (it, i, which)
+            bt.set_state(i, o.vars())
+    bt.close()
