@@ -6,6 +6,7 @@
 
 #define IPMZ_NBO_MAX 512
 #define IPMZ_PANEL_CTRL_WORDS 256
+#define IPMZ_CHAIN_STAMP_BLOCKS 512  // (debug stamps: N <= 32768)
 #define IPMZ_SOLVE_BLOCK 128     // rows per block of the persistent solve
 #define IPMZ_SOLVE_CTRL_WORDS 8  // its control words (error, tickets, sweep counters)
 
@@ -153,6 +154,7 @@ int64_t solve_prep_elems(int N);
 // launches keep it so for the next solve
 hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st);
 hipError_t solve_stamps(unsigned long long* out);  // DEBUG
+hipError_t chain_stamps(unsigned long long* c, unsigned long long* h);  // DEBUG (-DIPMZ_CHAIN_STAMPS)
 hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, double* P, hipStream_t st);
 hipError_t solve_prep(const float* K, int64_t ld, int N, const float* Linv, float* P, hipStream_t st);
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* P, double* b,

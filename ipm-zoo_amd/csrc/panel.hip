@@ -39,6 +39,28 @@
 
 namespace ipmz {
 
+// -DIPMZ_CHAIN_STAMPS (tools/kbench "chainclk" only): s_memrealtime stamps of
+// the chain role per 64-column block (k0 / 64 + j): 0 diag start, 1 READY[c]
+// seen, 2 diag done (write-back included), 3 operands loaded, 4 TRSM done,
+// 5 own update done (REG published); helpers: READY[c] published; rows role
+// 0: start, end; launches: first workgroup start per launch.
+__device__ unsigned long long g_cstamp[IPMZ_CHAIN_STAMP_BLOCKS][8];
+__device__ unsigned long long g_hstamp[IPMZ_CHAIN_STAMP_BLOCKS][4];
+#ifdef IPMZ_CHAIN_STAMPS
+#define CSTAMP(jb, i) \
+  if (threadIdx.x == 0 && (jb) < IPMZ_CHAIN_STAMP_BLOCKS) g_cstamp[jb][i] = __builtin_amdgcn_s_memrealtime()
+#define HSTAMP(jb, i) \
+  if (threadIdx.x == 0 && (jb) < IPMZ_CHAIN_STAMP_BLOCKS) g_hstamp[jb][i] = __builtin_amdgcn_s_memrealtime()
+#else
+#define CSTAMP(jb, i)
+#define HSTAMP(jb, i)
+#endif
+hipError_t chain_stamps(unsigned long long* c, unsigned long long* h) {  // DEBUG
+  hipError_t e = hipMemcpyFromSymbol(c, HIP_SYMBOL(g_cstamp), sizeof(g_cstamp));
+  if (e != hipSuccess) return e;
+  return hipMemcpyFromSymbol(h, HIP_SYMBOL(g_hstamp), sizeof(g_hstamp));
+}
+
 namespace {
 enum { OP_TICKET = 0, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128 };
 constexpr int OP_NBMAX = IPMZ_NBO_MAX / 64;
@@ -301,6 +323,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
     }
     for (int j = 0; j < nb; ++j) {
       const int j0 = k0 + 64 * j, bj = bsz(j);
+      CSTAMP(j0 / 64, 0);
       T* Lb = Lb0 + (int64_t)j * 64 * 64;
       // ---- block row c = j + 1: (c, j) and (c, c) from helper c.  Once the
       // diagonal block is final in LDS and before its write-back, one load
@@ -314,6 +337,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
       auto next_prefetch = [&]() {
         if (!more) return;
         ok = wait_flag(&area[OP_READY + c], err, sh_ok);  // (uniform)
+        CSTAMP(j0 / 64, 1);
         if (!ok) return;
         const int line = threadIdx.x, rr = line >> 2, cc = (line & 3) * (128 / (int)sizeof(T));
         if (rr < rows) {
@@ -325,6 +349,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
         diag64_body<true, false, T, false>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr, next_prefetch);
       else
         diag64_body<true, false, T, true>(K, ld, j0, bj, D, Lb, a.info, M, X, dsh, nullptr, next_prefetch);
+      CSTAMP(j0 / 64, 2);
       if (!more) {
         if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
         break;
@@ -339,6 +364,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
       // them instead of on the chain (nothing this workgroup waits for needs
       // DIAG[j]: helper c only uses blocks <= c - 2).  inject: timeout tests only
       if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
+      CSTAMP(j0 / 64, 3);
       T rd[4];
 #pragma unroll
       for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
@@ -350,6 +376,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
       mma_tile_lower<T>(reinterpret_cast<const T*>(M), [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); },
                         acc);
       __syncthreads();  // M and X reads done
+      CSTAMP(j0 / 64, 4);
       T* Lrow = K + (int64_t)r0 * ld + j0;
       T* Wrow = Wp + (int64_t)r0 * ldw + 64 * j;
       acc_t lacc[4];
@@ -371,6 +398,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
       // the update, so the stores drain beside its MFMAs (publish's barrier
       // also ends every wave's reads of M and X)
       publish(&area[OP_REG + j * OP_NBMAX + c]);
+      CSTAMP(j0 / 64, 5);
       // the next diagonal block, straight into diag64_body's image
 #pragma unroll
       for (int n = 0; n < 4; ++n) {
@@ -462,6 +490,7 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
     }
   }
   publish(&area[OP_READY + c]);
+  HSTAMP(r0 / 64, 0);
 }
 
 // ---- a rows role (rows ticket r): the 64 rows from ce + 64 r.  Every
@@ -505,6 +534,7 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
   // first 64 rows) also accumulates that panel's block (0, 0) look-ahead
   // update W(rows, j) L(rows, j)^T over j -- exactly the chunks prev_update
   // would sum in the next chain role -- and leaves it in pre00_out.
+  if (r == 0) HSTAMP(k0 / 64, 1);
   T* const p00 = r == 0 ? a.pre00_out : nullptr;
   acc_t a00[4];
   zero_acc<T>(a00);
@@ -555,6 +585,7 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
     }
   }
   if (p00 && ok) store_acc<T, false, false>(a00, p00, 64, 64, 64);  // consumed by a later launch
+  if (r == 0) HSTAMP(k0 / 64, 2);
 }
 }  // namespace
 
@@ -574,6 +605,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   const unsigned tu = sh_ticket;
   if (tu == ~0u) return;
   const int t = (int)tu;
+  if (t == 0) HSTAMP(a.k0 / 64 + 1, 3);  // the chain role's workgroup starts
+  if (t == a.nchain) HSTAMP(a.k0 / 64 + 2, 3);  // the first rows role starts
   if (t < a.nchain) {
     // s_setprio 3: the chain roles' waves win issue arbitration (matrix pipe
     // included) against the GEMM waves that share the CU

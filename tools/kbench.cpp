@@ -377,6 +377,45 @@ int main(int argc, char** argv) {
     }
     return 0;
   }
+  if (mode == "chainclk") {  // kbench_chain N chainclk NBO: per-block clocks of the panel chain (IPMZ_CHAIN_STAMPS)
+    const int nbo = argc > 3 ? std::atoi(argv[3]) : 512;
+    std::vector<hipEvent_t> ev(5 * (N / 64 + 2) + 8);
+    for (auto& evi : ev) CK(hipEventCreateWithFlags(&evi, hipEventDisableTiming));
+    int lo = 0, hi = 0;
+    CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    hipStream_t sA, sB, sC;
+    CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+    CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+    CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
+    static unsigned long long cs[IPMZ_CHAIN_STAMP_BLOCKS][8], hs[IPMZ_CHAIN_STAMP_BLOCKS][4];
+    for (int rep = 0; rep < 4; ++rep) {
+      hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, sA, K, ld, N, 7ull);
+      CK(hipMemsetAsync(pctrl, 0, ipmz::panel_ctrl_words(N, nbo) * 4, sA));
+      CK(hipStreamSynchronize(sA));
+      t.start(sA);
+      CK(hipEventRecord(ev.back(), sA));
+      CK(hipStreamWaitEvent(sB, ev.back(), 0));
+      CK(hipStreamWaitEvent(sC, ev.back(), 0));
+      CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, nbo, 64, info, sA, nullptr, sB, sC, ev.data(), (int)ev.size() - 1,
+                           pctrl));
+      const float fms = t.stop(sA);
+      CK(hipDeviceSynchronize());
+      std::printf("factor N=%d nbo=%d: %.3f ms\n", N, nbo, fms);
+    }
+    CK(ipmz::chain_stamps(&cs[0][0], &hs[0][0]));
+    const double t0 = (double)cs[0][0];
+    auto us = [&](unsigned long long v) { return v ? (v - t0) / 100.0 : -1.0; };
+    std::printf("block: diag_start ready_seen diag_done ops_loaded trsm_done own_done | helper_ready(blk) | "
+                "rows0 start end | launch starts (us from block 0's diag start); dur = next diag start - this\n");
+    const int nblk = (N + 63) / 64;
+    for (int b = 0; b < nblk && b < IPMZ_CHAIN_STAMP_BLOCKS; ++b) {
+      const double nx = b + 1 < nblk ? us(cs[b + 1][0]) : -1.0;
+      std::printf("%3d %9.2f %9.2f %9.2f %9.2f %9.2f %9.2f | %9.2f | %9.2f %9.2f | %9.2f %9.2f | dur %6.2f\n", b,
+                  us(cs[b][0]), us(cs[b][1]), us(cs[b][2]), us(cs[b][3]), us(cs[b][4]), us(cs[b][5]), us(hs[b][0]),
+                  us(hs[b][1]), us(hs[b][2]), us(hs[b][3]), -1.0, nx > 0 ? nx - us(cs[b][0]) : 0.0);
+    }
+    return 0;
+  }
   // factor: the look-ahead factor (panel path on a high-priority stream,
   // trailing updates on a low-priority one) and the persistent solve.
   // (Measured and dropped: CU masks reserving 8 / 16 / 32 CUs for the panel
