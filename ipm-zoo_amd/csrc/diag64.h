@@ -194,14 +194,22 @@ struct NoHook {
 // WB_LINV = false: L^{-1} is not written back (the caller writes it from X
 // later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
 // column pass (the batched factor writes the previous block's L^{-1} there).
+// DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
+// the barrier after the first column pass -- wave 0 after its pass, so the
+// wait is off its chain (the 8-wave panel chain publishes the previous
+// block's write-back behind that barrier).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
-          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1>
+          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1, bool DRAIN0 = false>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
                                             const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1,
                                             IDLE0 idle0 = IDLE0()) {
-  const int tid = tid_arg < 0 ? (int)threadIdx.x : tid_arg, lane = tid & 63, wave = tid >> 6;
+  // wave: readfirstlane makes the wave roles below uniform branches for the
+  // compiler (threadIdx.x-derived values are divergent to it), so the roles'
+  // register live ranges do not overlap
+  const int tid = tid_arg < 0 ? (int)threadIdx.x : tid_arg, lane = tid & 63,
+            wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   auto Mt = [&](int i, int j) { return &M[(16 * i) * DS + 16 * j]; };
   auto Xt = [&](int i, int j) { return &X[(16 * i) * DS + 16 * j]; };
   int nclk = 0;
@@ -260,6 +268,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   };
   if (wave == 0) colpass(0);
   else idle0();
+  if constexpr (DRAIN0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   clk();
   for (int p = 0; p < 3; ++p) {
