@@ -196,10 +196,11 @@ struct NoHook {
 // column pass (the batched factor writes the previous block's L^{-1} there).
 // DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
 // the barrier after the first column pass -- wave 0 after its pass, so the
-// wait is off its chain (the 8-wave panel chain publishes the previous
-// block's write-back behind that barrier).
+// wait is off its chain.  WB_D = false: D (and the non-finite pivot check)
+// is left to the caller too (the 8-wave panel chain writes D and L^{-1} from
+// its other wave group, off the critical path).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
-          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1, bool DRAIN0 = false>
+          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1, bool DRAIN0 = false, bool WB_D = true>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
@@ -322,7 +323,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
       else Linv[idx] = x;
     }
   }
-  if (tid < b) {
+  if (WB_D && tid < b) {
     const double dk = dsh[tid];
     if constexpr (COH) __hip_atomic_store(&D[k0 + tid], (TS)dk, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else D[k0 + tid] = (TS)dk;

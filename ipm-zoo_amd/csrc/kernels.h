@@ -26,14 +26,14 @@ namespace ipmz {
 // 256 = the fp32 factor's look-ahead strip on the trailing stream before the trailing update (no fourth stream),
 // 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test),
 // 1024 = the fp64 trailing and strip updates on gemm.h's register-staged kernel instead of gemm64.h's (A/B),
-// 2048 = the panel's chain launch runs the 256-thread kernel with the 4-wave chain roles (round 4, A/B),
+// 2048 = the panel's chain launch runs the 512-thread kernel with the 8-wave chain roles (chain8, A/B),
 // 4096 = the chain launch draws no ticket: the rows launch runs every chain role in its 4-wave form
 //        (what a serialized dispatch order can produce; the forms must factor bitwise alike),
 // 8192 = batches assemble the whole KKT into K every step (not the kept K0) (A/B)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
-       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_CHAIN4 = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
+       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_CHAIN8 = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
        IPMZ_DEBUG_NO_K0 = 8192 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \

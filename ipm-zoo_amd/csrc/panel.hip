@@ -14,13 +14,14 @@
 //       diagonal block (diag64_body), publish DIAG[j], the TRSM of the next
 //       region block (j+1, j) and that block's own diagonal update; the
 //       result IS the next diagonal block.  The whole critical path of the
-//       panel lives on one CU.  In the chain launch it runs on 8 waves
-//       (chain8): waves 0-3 factor the diagonal block, waves 4-7 form the TRSM
-//       and the next diagonal block in its shadow, column block by column
-//       block as the pivots and the rows of L_jj^{-1} become final, so only
-//       the last 16 columns' TRSM and update stay between two diagonal
-//       factors.  In the rows launch (drawn first only when the launches are
-//       serialized) it runs on 4 waves (chain4), one step after the other.
+//       panel lives on one CU.  chain4 (4 waves, the default): one step
+//       after the other.  chain8 (the 512-thread chain launch, debug bit
+//       IPMZ_DEBUG_CHAIN8): waves 0-3 factor the diagonal block, waves 4-7
+//       form the TRSM and the next diagonal block in its shadow, column block
+//       by column block as the pivots and the rows of L_jj^{-1} become final
+//       -- measured slower so far (27 vs 24 us per 64-column block at
+//       N = 2560): it waits for helper c's READY, which follows the chain's
+//       own REG[c-2][c-1] by ~11 us of hand-offs.
 //     tickets nb.. = TILE WORKERS: one region block (c, q), c >= 1, each,
 //       updated with the previous panel (flag TILE[c][q]); the chain updates
 //       block (0, 0) itself, straight into its LDS image.
@@ -37,7 +38,7 @@
 // column blocks over two waves per row block; chain8's bulk waves run chain4's
 // MFMA sequences per column block), so the factor is bitwise the same
 // whichever launch holds a role (tests/test_gpu_panel_forms.py, debug bits
-// IPMZ_DEBUG_CHAIN4 / IPMZ_DEBUG_ROWS_CHAIN).
+// IPMZ_DEBUG_CHAIN8 / IPMZ_DEBUG_ROWS_CHAIN).
 //
 // Flags: one area of IPMZ_PANEL_CTRL_WORDS words per outer panel (zeroed by
 // one memset when the factorization starts); the sticky error word is shared.
@@ -707,18 +708,21 @@ __device__ __forceinline__ void helper(const PanelArgs<T>& a, int c, double* sme
     store_acc<T, true, false, NW>(m, acc, a.Wp + (int64_t)r0 * ldw + 64 * j, ldw, rows, 64);
     publish(&area[OP_REG + j * OP_NBMAX + c]);
     put_acc<T, NW>(m, As, lacc);
-    // strips: (c, q) -= L(c, j) W(q, j)^T, q = j+1 .. c
-    for (int q = j + 1; q <= c; ++q) {
+    // strips: (c, q) -= L(c, j) W(q, j)^T, q = c, c-1 .. j+1: the own tile
+    // (its W in registers) first, the tile whose W the chain publishes
+    // (q = c-1 for j = c-2) last, its tile loaded before that wait -- so
+    // READY[c] follows REG[c-2][c-1] by one strip
+    for (int q = c; q > j; --q) {
       const int q0 = k0 + 64 * q, qrows = panel_bsz(a, q);
+      Acc<T> tile[NN];
+      if (q == c) load_acc<T, true, true, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
+      else load_acc<T, true, false, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
       if (q == c) {
         put_acc<T, NW>(m, Bs, acc);
       } else {
         if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], a.err, sh_ok)) return;
         stage_tile<T, true, NW>(tid, Bs, a.Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, 64);
       }
-      Acc<T> tile[NN];
-      if (q == c) load_acc<T, true, true, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
-      else load_acc<T, true, false, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
       __syncthreads();
       mma_tile<T, true, NW>(m, As, [&](int r, int k) { return Bs[r * DS + k]; }, tile);
       if (q == c) store_acc<T, true, true, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
@@ -855,7 +859,7 @@ __device__ __forceinline__ unsigned draw_ticket(const PanelArgs<T>& a, bool chai
 }
 }  // namespace
 
-// The rows launch (and the chain launch under IPMZ_DEBUG_CHAIN4): 256 threads.
+// The rows launch and, by default, the chain launch: 256 threads.
 // amdgpu_waves_per_eu(2): <= 256 registers per lane (VGPR + AGPR), so a
 // panel workgroup fits beside a trailing-GEMM workgroup (64 per lane at 4
 // waves per SIMD) -- with more it waits for a CU with no GEMM at all.
@@ -939,11 +943,13 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   a.nchain = nb + (Wprev ? nb * (nb + 1) / 2 - 1 : 0);
   a.nrows = ce < N ? (N - ce + 63) / 64 : 0;
   const int dbg = debug_inject_mask();
-  if (dbg & IPMZ_DEBUG_CHAIN4)  // round 4's chain launch: the 256-thread kernel, 4-wave chain roles
-    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, 0, rows_prev ? 1 : 0);
-  else
+  if (dbg & IPMZ_DEBUG_CHAIN8)  // the 512-thread chain launch, 8-wave chain roles
     hipLaunchKernelGGL(panel_chain_kernel<T>, dim3(a.nchain), dim3(512), chain_lds_bytes<T>(), st_chain, a,
                        (dbg & IPMZ_DEBUG_ROWS_CHAIN) ? 0 : 1);
+  else if (dbg & IPMZ_DEBUG_ROWS_CHAIN)  // no chain ticket drawn: the rows launch runs every chain role
+    hipLaunchKernelGGL(panel_chain_kernel<T>, dim3(a.nchain), dim3(512), chain_lds_bytes<T>(), st_chain, a, 0);
+  else
+    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, 0, rows_prev ? 1 : 0);
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   // the rows launch: every chain role and every rows role, should it run first

@@ -1,6 +1,6 @@
 """The panel's chain roles in both of their forms factor bitwise alike
-(panel.hip): the 8-wave chain of the chain launch (production), the 4-wave
-chain of round 4's 256-thread chain launch (debug bit IPMZ_DEBUG_CHAIN4), and
+(panel.hip): the 4-wave chain of the 256-thread chain launch (production),
+the 8-wave chain of the 512-thread chain launch (debug bit IPMZ_DEBUG_CHAIN8), and
 every chain role run by the rows launch in its 4-wave form (debug bit
 IPMZ_DEBUG_ROWS_CHAIN -- what a serialized dispatch order, e.g. under
 rocprofv3 --pmc, produces).  A role may land in either launch, so the forms
@@ -15,8 +15,8 @@ pytestmark = pytest.mark.gpu
 I = pytest.importorskip("ipmz_amd")
 torch = pytest.importorskip("torch")
 
-CHAIN4, ROWS_CHAIN = 2048, 4096  # kernels.h IPMZ_DEBUG_CHAIN4 / IPMZ_DEBUG_ROWS_CHAIN
-MODES = [0, CHAIN4, ROWS_CHAIN]
+CHAIN8, ROWS_CHAIN = 2048, 4096  # kernels.h IPMZ_DEBUG_CHAIN8 / IPMZ_DEBUG_ROWS_CHAIN
+MODES = [0, CHAIN8, ROWS_CHAIN]
 
 
 @pytest.fixture(scope="module")
