@@ -194,7 +194,7 @@ struct NoHook {
 // WB_LINV = false: L^{-1} is not written back (the caller writes it from X
 // later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
 // column pass (the batched factor writes the previous block's L^{-1} there).
-// DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
+// abort8: see the loop below.  DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
 // the barrier after the first column pass -- wave 0 after its pass, so the
 // wait is off its chain.  WB_D = false: D (and the non-finite pivot check)
 // is left to the caller too (the 8-wave panel chain writes D and L^{-1} from
@@ -205,7 +205,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
                                             const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1,
-                                            IDLE0 idle0 = IDLE0()) {
+                                            IDLE0 idle0 = IDLE0(), const volatile unsigned* abort8 = nullptr) {
   // wave: readfirstlane makes the wave roles below uniform branches for the
   // compiler (threadIdx.x-derived values are divergent to it), so the roles'
   // register live ranges do not overlap
@@ -301,6 +301,9 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
     }
     __syncthreads();
     clk();
+    // abort8 (LDS, set before the 8th barrier): the caller gives the block up
+    // (the 8-wave panel chain's launch found itself alone, panel.hip)
+    if (p == 2 && abort8 && *abort8) return;
   }
   // ---- the last row of inverse tiles: X_33 on wave 0 while waves 1..3 sum
   // S_3j = sum_k L_3k X_kj (X_33 is not needed for those), then X_3j = -X_33 S_3j

@@ -387,7 +387,7 @@ int main(int argc, char** argv) {
     CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
     CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
     CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
-    static unsigned long long cs[IPMZ_CHAIN_STAMP_BLOCKS][8], hs[IPMZ_CHAIN_STAMP_BLOCKS][4];
+    static unsigned long long cs[IPMZ_CHAIN_STAMP_BLOCKS][16], hs[IPMZ_CHAIN_STAMP_BLOCKS][4];
     for (int rep = 0; rep < 4; ++rep) {
       hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, sA, K, ld, N, 7ull);
       CK(hipMemsetAsync(pctrl, 0, ipmz::panel_ctrl_words(N, nbo) * 4, sA));
@@ -410,9 +410,14 @@ int main(int argc, char** argv) {
     const int nblk = (N + 63) / 64;
     for (int b = 0; b < nblk && b < IPMZ_CHAIN_STAMP_BLOCKS; ++b) {
       const double nx = b + 1 < nblk ? us(cs[b + 1][0]) : -1.0;
-      std::printf("%3d %9.2f %9.2f %9.2f %9.2f %9.2f %9.2f | %9.2f | %9.2f %9.2f | %9.2f %9.2f | dur %6.2f\n", b,
+      std::printf("%3d %9.2f %9.2f %9.2f %9.2f %9.2f %9.2f | %9.2f | %9.2f %9.2f | %9.2f %9.2f | dur %6.2f", b,
                   us(cs[b][0]), us(cs[b][1]), us(cs[b][2]), us(cs[b][3]), us(cs[b][4]), us(cs[b][5]), us(hs[b][0]),
                   us(hs[b][1]), us(hs[b][2]), us(hs[b][3]), -1.0, nx > 0 ? nx - us(cs[b][0]) : 0.0);
+      if (cs[b][4] && cs[b][6]) {  // chain8: the bulk group's barrier clocks, relative to the window start
+        std::printf(" | bars");
+        for (int k = 4; k < 16; ++k) std::printf(" %.2f", cs[b][k] ? us(cs[b][k]) - us(cs[b][0]) : -1.0);
+      }
+      std::printf("\n");
     }
     return 0;
   }
