@@ -664,7 +664,10 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
     }
     return __builtin_amdgcn_readfirstlane(ok) != 0;
   };
-  for (int j = 0; j < nb; ++j) {
+  // one window; FIRST: window 0 (its own code, so the two paths' registers
+  // are not merged through the loop)
+  auto window = [&](const int j, auto firstc) __attribute__((always_inline)) {
+    constexpr bool FIRST = decltype(firstc)::value;
     const int j0 = k0 + 64 * j;
     int nbar = 0;
     auto bar = [&]() __attribute__((always_inline)) {
@@ -689,7 +692,7 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
       bar();  // #4
       publish_prev(false);
       for (int b = 5; b <= 10; ++b) bar();
-      break;
+      return;
     }
     const int c = j + 1, r0 = k0 + 64 * c, rows = panel_bsz(a, c);
     // ---- I8 .. T2: (4) T(c, j) column block by column block, (5) the own
@@ -747,7 +750,7 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
         }
       bar();  // T2
     };
-    if (j == 0) {
+    if constexpr (FIRST) {
       // ---- window 0: row 1 waits for the tile workers' look-ahead update, so
       // its READY is looked at (no wait) in I4 and waited for in I8 -- a wait
       // at #1 would hold the diagonal factor; no block column before 0
@@ -777,8 +780,8 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
         }
       }
       tail(t1, pt);
-      continue;
-    }
+      return;
+    } else {
     // ---- window j >= 1
     Acc<T> w2[4], t1[4], pt[4];  // W^T(c, j-1) (TRSM (1)), A(c, j)^T, A(c, c)^T
     // I1: block row c's operands (helper c: block columns <= c - 3)
@@ -811,7 +814,11 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
     bar();  // #6
     bar();  // #7
     tail(t1, pt);
-  }
+    }
+  };
+  window(0, std::true_type{});
+  if (*(volatile unsigned*)sh_abort) return;
+  for (int j = 1; j < nb; ++j) window(j, std::false_type{});
   // the last block's L^{-1} and D, then its DIAG
   if (threadIdx.x < 256 + 64) dsave = dsh[threadIdx.x - 256];
   put_linv_d(nb - 1);
