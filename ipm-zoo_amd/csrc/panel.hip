@@ -544,18 +544,16 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
   double dsave = 0.0;         // D of the block last factored (lanes < 64 of wave 4)
   // slab <- tile (rows r0.. of this lane's row r; rows >= rows read as 0;
   // diagt: columns past the diagonal read as 0)
-  auto load_slab = [&](Acc<T>(&y)[4], const T* src, int rows, bool diagt) {
-    const bool in_r = r < rows;
-    const T* row = src + (int64_t)(in_r ? r : 0) * ld + q;
+  // (no masking: a select would wait for the load; the elements of rows >=
+  // rows (read from row 0) and above the diagonal only reach outputs that
+  // are never stored or used -- each output element sums its own row and
+  // column only)
+  auto load_slab = [&](Acc<T>(&y)[4], const T* src, int rows) {
+    const T* row = src + (int64_t)(r < rows ? r : 0) * ld + q;
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int col = 16 * kb + q + 4 * g;
-        const bool in = in_r && (!diagt || col <= r);
-        const T v = ld_sc1(row + 16 * kb + 4 * g);
-        y[kb][g] = in ? v : T(0);
-      }
+      for (int g = 0; g < 4; ++g) y[kb][g] = ld_sc1(row + 16 * kb + 4 * g);
   };
   // TRSM of column block IB: y[IB] = sum_{kb <= IB, g} X[16 IB + p][16 kb + 4 g + q] t[kb][g]
   // (X lower triangular, masked): chain4's mma_tile_lower sequence for acc[IB]
@@ -586,8 +584,8 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
         const T bl = w[kb][g] * rd[16 * kb + MF::row(lane, g)];
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) y[jb] = MF::mma(-A[(16 * jb + p) * DS + k], bl, y[jb]);
-        __builtin_amdgcn_sched_barrier(0);
       }
+      __builtin_amdgcn_sched_barrier(0);  // (per k block: 16 LDS operands in flight)
     });
   };
   // slab column blocks [KB0, KB1) -> rows r of an LDS tile (row-major, DS)
@@ -748,6 +746,18 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
           const int i = 16 * jb + MF::row(lane, g);
           M[r * DS + i] = (r < rows && i <= r) ? (double)pt[jb][g] : (r == i ? 1.0 : 0.0);
         }
+      // block row c + 1, if it is ready already: one load per 128-byte line
+      // of its three tiles pulls them into this XCD's L2, so the next
+      // window's slab loads do not pay the far latency
+      if (c + 1 < nb && __builtin_amdgcn_readfirstlane(ld_sc1(&area[OP_READY + c + 1])) != 0u) {
+        const int r1 = r0 + 64, rows1 = panel_bsz(a, c + 1), tb = threadIdx.x - 256;
+        const int rr = tb >> 2, cc = (tb & 3) * 16;
+        if (rr < rows1) {
+          const T* src = K + (int64_t)(r1 + rr) * ld + cc;
+          T tv = ld_sc1(src + j0) + ld_sc1(src + r0) + ld_sc1(src + r1);
+          asm volatile("" ::"v"(tv));
+        }
+      }
       bar();  // T2
     };
     if constexpr (FIRST) {
@@ -760,8 +770,8 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
       bar();  // #3
       bool loaded = false;
       if (__builtin_amdgcn_readfirstlane(ld_sc1(&area[OP_READY + c])) != 0u) {
-        load_slab(t1, K + (int64_t)r0 * ld + j0, rows, false);
-        load_slab(pt, K + (int64_t)r0 * ld + r0, rows, true);
+        load_slab(t1, K + (int64_t)r0 * ld + j0, rows);
+        load_slab(pt, K + (int64_t)r0 * ld + r0, rows);
         loaded = true;
       }
       bar();  // #4
@@ -770,8 +780,8 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
       bar();  // #7
       if (!loaded) {  // wait for row 1, or give the panel up
         if (wait_ready(c, 100000ull)) {  // 1 ms
-          load_slab(t1, K + (int64_t)r0 * ld + j0, rows, false);
-          load_slab(pt, K + (int64_t)r0 * ld + r0, rows, true);
+          load_slab(t1, K + (int64_t)r0 * ld + j0, rows);
+          load_slab(pt, K + (int64_t)r0 * ld + r0, rows);
         }
         CSTAMP_T(256, j0 / 64, 1);
         if (*(volatile unsigned*)sh_abort) {
@@ -787,9 +797,9 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
     // I1: block row c's operands (helper c: block columns <= c - 3)
     wait_ready(c, 0);
     CSTAMP_T(256, j0 / 64, 1);
-    load_slab(w2, K + (int64_t)r0 * ld + j0 - 64, rows, false);
-    load_slab(t1, K + (int64_t)r0 * ld + j0, rows, false);
-    load_slab(pt, K + (int64_t)r0 * ld + r0, rows, true);
+    load_slab(w2, K + (int64_t)r0 * ld + j0 - 64, rows);
+    load_slab(t1, K + (int64_t)r0 * ld + j0, rows);
+    load_slab(pt, K + (int64_t)r0 * ld + r0, rows);
     bar();  // #1
     // I2 (column pass 0): L^{-1} and D of block j-1; (1) T(c, j-1) with
     // X_{j-1} (in place, last column block first), its L / W stored
