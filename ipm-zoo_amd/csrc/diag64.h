@@ -194,18 +194,23 @@ struct NoHook {
 // WB_LINV = false: L^{-1} is not written back (the caller writes it from X
 // later, small.hip); IDLE0: called by waves 1.. while wave 0 runs the first
 // column pass (the batched factor writes the previous block's L^{-1} there).
-// abort8: see the loop below.  DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
+// abort8: see the loop below.  POST2: called by every thread after the
+// barrier that follows the first column pass (with DRAIN0: every earlier
+// store of the workgroup is complete there -- the 4-wave panel chain raises
+// the previous block's flags in it).  DRAIN0: every wave drains its outstanding global stores (vmcnt(0)) before
 // the barrier after the first column pass -- wave 0 after its pass, so the
 // wait is off its chain.  WB_D = false: D (and the non-finite pivot check)
 // is left to the caller too (the 8-wave panel chain writes D and L^{-1} from
 // its other wave group, off the critical path).
 template <bool COH, bool LSC = false, typename TS = double, bool PRE = false, int NW = 4, typename PRE_WB = NoHook,
-          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1, bool DRAIN0 = false, bool WB_D = true>
+          bool WB_LINV = true, typename IDLE0 = NoHook, int CPV = 1, bool DRAIN0 = false, bool WB_D = true,
+          typename POST2 = NoHook>
 __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int k0, int b, TS* __restrict__ D,
                                             TS* __restrict__ Linv, int* __restrict__ info, double* M, double* X,
                                             double* dsh, unsigned long long* clkbuf, PRE_WB pre_wb = PRE_WB(),
                                             const TS* __restrict__ Ksrc = nullptr, int tid_arg = -1,
-                                            IDLE0 idle0 = IDLE0(), const volatile unsigned* abort8 = nullptr) {
+                                            IDLE0 idle0 = IDLE0(), const volatile unsigned* abort8 = nullptr,
+                                            POST2 post2 = POST2()) {
   // wave: readfirstlane makes the wave roles below uniform branches for the
   // compiler (threadIdx.x-derived values are divergent to it), so the roles'
   // register live ranges do not overlap
@@ -271,6 +276,7 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   else idle0();
   if constexpr (DRAIN0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  post2();  // (every thread, after the barrier that follows the first column pass)
   clk();
   for (int p = 0; p < 3; ++p) {
     // ---- A(p): the critical tiles (i, p+1), i > p, with block column p

@@ -122,14 +122,18 @@ __device__ __forceinline__ int launder(int v) {
 // acc[i] (+)= sgn * A[16 wr.., :] B[16 n.., :]^T over k in [0, 64), n = n0 + i:
 // A, B row-major 64 x DS tiles in LDS (B read through bf: (row, k) -> T).
 // Per element: the MFMAs of k = 4s .. 4s+3, s = 0..15, in order.
+// ascale (optional, LDS): A's element (r, k) is As[r][k] * ascale[k] (one
+// rounding: the L = W / d tile read from the W tile)
 template <typename T, bool NEG, int NW, typename BF>
-__device__ __forceinline__ void mma_tile(const TMap<NW>& m, const T* As, BF bf, Acc<T> (&acc)[TMap<NW>::NN]) {
+__device__ __forceinline__ void mma_tile(const TMap<NW>& m, const T* As, BF bf, Acc<T> (&acc)[TMap<NW>::NN],
+                                         const T* ascale = nullptr) {
   typedef Mfma<T> MF;
   const int arow = 16 * m.wr + (m.lane & 15);
 #pragma unroll 4
   for (int s = 0; s < 16; ++s) {
     const int k = 4 * s + (m.lane >> 4);
-    const T a = NEG ? -As[arow * DS + k] : As[arow * DS + k];
+    const T av = ascale ? As[arow * DS + k] * ascale[k] : As[arow * DS + k];
+    const T a = NEG ? -av : av;
 #pragma unroll
     for (int i = 0; i < TMap<NW>::NN; ++i) acc[i] = MF::mma(a, bf(16 * (m.n0 + i) + (m.lane & 15), k), acc[i]);
   }
@@ -358,8 +362,17 @@ __device__ __forceinline__ void chain_block00(const PanelArgs<T>& a, double* M, 
   // (diag64_body's first barrier orders these stores before its reads)
 }
 
-// ---- CHAIN, 4 waves (a 256-thread workgroup of either launch): one step
-// after the other, every step on the critical path
+// ---- CHAIN, 4 waves (a 256-thread workgroup of either launch).  Per block
+// j: the diagonal factor (diag64_body), then -- on the critical path -- the
+// write-back of L_jj, the TRSM of block (c, j), c = j + 1, and the own update
+// of (c, c), which is the next diagonal block.  Everything else is moved off
+// that path: the operands of block row c are loaded before the write-back
+// (their latency overlaps it); L_jj^{-1} and D_j are written by waves 1..3
+// while wave 0 runs the next block's first column pass (X and a copy of D
+// are intact until then); the L / W stores of (c, j) are not drained on the
+// path -- the flags DIAG[j] and REG[j][c] are raised after that pass's
+// barrier, every store drained (diag64_body's DRAIN0 / POST2); the own
+// update reads L = W / d from the W tile in LDS (X stays intact).
 template <typename T>
 __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsigned* sh_ok) {
   T* const K = a.K;
@@ -370,66 +383,87 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
   double* M = smem;
   double* X = smem + 64 * DS;
   double* dsh = smem + 2 * 64 * DS;  // 64 doubles (diag64_body's pivots)
+  double* dsv = dsh + 64;            // 64: D of the block last factored (its write-back is deferred)
+  T* rdv = reinterpret_cast<T*>(dsv + 64);  // 64: 1 / d of the block in dsh
   if (a.Wprev) chain_block00<T, 4>(a, M, X);
+  // L^{-1} (identity-padded past b) and D of block jb (X, dsv); threads
+  // [t0, 256) -- waves 1..3 in the next block's first column pass
+  auto put_linv_d = [&](int jb, int tid, int t0) __attribute__((always_inline)) {
+    const int jp0 = k0 + 64 * jb, b = panel_bsz(a, jb);
+    T* Lb = a.Lb0 + (int64_t)jb * 64 * 64;
+    for (int idx = tid - t0; idx < 64 * 64; idx += 256 - t0) {
+      const int rr = idx >> 6, cc = idx & 63;
+      st_sc1(&Lb[idx], (T)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc])));
+    }
+    for (int t = tid - t0; t < b; t += 256 - t0) {
+      const double dk = dsv[t];
+      st_sc1(&a.D[jp0 + t], (T)dk);
+      if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(a.info, jp0 + t + 1);  // first non-finite pivot
+    }
+  };
   for (int j = 0; j < nb; ++j) {
     const int tid = launder((int)threadIdx.x), lane = tid & 63;
     const TMap<4> m(tid);
     const int j0 = k0 + 64 * j, bj = panel_bsz(a, j);
     CSTAMP(j0 / 64, 0);
     T* Lb = a.Lb0 + (int64_t)j * 64 * 64;
-    // ---- block row c = j + 1: (c, j) and (c, c) from helper c.  Once the
-    // diagonal block is final in LDS and before its write-back, one load
-    // per 128-byte line of both tiles pulls them into this XCD's L2 (the
-    // helper stored them write-through): the operand loads after the
-    // write-back then hit L2 instead of paying the HBM latency on the chain
     const bool more = j + 1 < nb;
     const int c = j + 1, r0 = k0 + 64 * c, rows = more ? panel_bsz(a, c) : 0;
+    // block j-1's L^{-1} / D (waves 1..3 during the first column pass) and
+    // flags (after its barrier: every store of this workgroup is complete)
+    auto idle0 = [&]() __attribute__((always_inline)) {
+      if (j >= 1) put_linv_d(j - 1, tid, 64);
+    };
+    auto post2 = [&]() __attribute__((always_inline)) {
+      if (j >= 1 && tid == 0) {
+        if (!(a.inject && j == 1)) st_sc1(&area[OP_DIAG + j - 1], 1u);
+        st_sc1(&area[OP_REG + (j - 1) * OP_NBMAX + j], 1u);
+      }
+    };
+    // block row c's operands (helper c stored them write-through), loaded
+    // before L_jj's write-back: A(c, j) for the TRSM, the own block (c, c)
     bool ok = true;
-    T pf[2] = {T(0), T(0)};
-    auto next_prefetch = [&]() {
+    T va[16];
+    Acc<T> own[4];
+    auto pre_wb = [&]() __attribute__((always_inline)) {
       if (!more) return;
       ok = wait_flag(&area[OP_READY + c], a.err, sh_ok);  // (uniform)
       CSTAMP(j0 / 64, 1);
       if (!ok) return;
-      const int rr = tid >> 2, cc = (tid & 3) * (128 / (int)sizeof(T));
-      if (rr < rows) {
-        pf[0] = ld_sc1(&K[(int64_t)(r0 + rr) * ld + j0 + (cc < 64 ? cc : 0)]);
-        pf[1] = ld_sc1(&K[(int64_t)(r0 + rr) * ld + r0 + (cc <= rr ? cc : 0)]);
-      }
+      fetch_tile<T, true, 4>(tid, va, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+      load_acc<T, true, true, 4>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
     };
     if (j == 0 && !a.Wprev)
-      diag64_body<true, false, T, false>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, next_prefetch, nullptr,
-                                         tid);
+      diag64_body<true, false, T, false, 4, decltype(pre_wb), false, decltype(idle0), 1, true, false, decltype(post2)>(
+          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
     else
-      diag64_body<true, false, T, true>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, next_prefetch, nullptr,
-                                        tid);
+      diag64_body<true, false, T, true, 4, decltype(pre_wb), false, decltype(idle0), 1, true, false, decltype(post2)>(
+          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
     CSTAMP(j0 / 64, 2);
-    if (!more) {
+    if (tid < 64) dsv[tid] = dsh[tid];  // D_j for its deferred write-back
+    if (!more) {  // the panel's last block: its L^{-1}, D and DIAG now
+      __syncthreads();
+      put_linv_d(j, tid, 0);
       if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
+      else publish(&area[OP_DIAG + OP_NBMAX]);  // (timeout tests: DIAG[0] never raised; a spare word)
       break;
     }
     if (!ok) return;
-    asm volatile("" ::"v"(pf[0]), "v"(pf[1]));  // the prefetches stay live (not eliminated) until here
-    // A(c, j) into M (free: L_jj is in K), the own block (c, c) into registers
-    stage_tile<T, true, 4>(tid, reinterpret_cast<T*>(M), K + (int64_t)r0 * ld + j0, ld, rows, 64);
-    Acc<T> own[4];
-    load_acc<T, true, true, 4>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
-    // DIAG[j] after these loads: the diagonal block's write-back drains beside
-    // them instead of on the chain (nothing this workgroup waits for needs
-    // DIAG[j]: helper c only uses blocks <= c - 2).  inject: timeout tests only
-    if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
-    CSTAMP(j0 / 64, 3);
+    // A(c, j) into M (L_jj's write-back has read it), 1 / d of block j
+    put_tile<T, 4>(tid, reinterpret_cast<T*>(M), va, rows, 64);
+    if (tid < 64) rdv[tid] = T(1) / (T)dsh[tid];
     T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
     __syncthreads();
+    CSTAMP(j0 / 64, 3);
     // TRSM: T = A(c, j) X_jj^T with X lower triangular (its upper part in
     // LDS is not meaningful: masked)
     Acc<T> acc[4];
     zero_acc<T, 4>(acc);
     mma_tile_lower<T, 4>(m, reinterpret_cast<const T*>(M),
                          [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); }, acc);
-    __syncthreads();  // M and X reads done
+    __syncthreads();  // M reads done
     CSTAMP(j0 / 64, 4);
     T* Lrow = K + (int64_t)r0 * ld + j0;
     T* Wrow = a.Wp + (int64_t)r0 * ldw + 64 * j;
@@ -440,18 +474,12 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
       for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
     store_acc<T, false, false, 4>(m, lacc, Lrow, ld, rows, 64);
     store_acc<T, true, false, 4>(m, acc, Wrow, ldw, rows, 64);
-    // own update (c, c) -= L(c, j) W(c, j)^T: L into X, W into M (both free:
-    // L_jj is in K, X_jj no longer needed)
-    T* Lx = reinterpret_cast<T*>(X);
+    // own update (c, c) -= L(c, j) W(c, j)^T: W into M, L = W / d read from it
     T* Wm = reinterpret_cast<T*>(M);
-    put_acc<T, 4>(m, Lx, lacc);
     put_acc<T, 4>(m, Wm, acc);
     __syncthreads();
-    mma_tile<T, true, 4>(m, Lx, [&](int r, int k) { return Wm[r * DS + k]; }, own);
-    // W(c, j) for the helpers' and the rows roles' strips: published after
-    // the update, so the stores drain beside its MFMAs (publish's barrier
-    // also ends every wave's reads of M and X)
-    publish(&area[OP_REG + j * OP_NBMAX + c]);
+    mma_tile<T, true, 4>(m, Wm, [&](int r, int k) { return Wm[r * DS + k]; }, own, rdv);
+    __syncthreads();  // every wave's reads of M done
     CSTAMP(j0 / 64, 5);
     // the next diagonal block, straight into diag64_body's image
 #pragma unroll
@@ -1096,7 +1124,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
                                                                                            int rows_launch, int rows_prev) {
   // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
   // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
-  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64];
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64 + 64];
   __shared__ unsigned sh_ok;
   int form = 0;
   const unsigned tu = draw_ticket(a, 4, rows_launch != 0, &form);
