@@ -363,18 +363,16 @@ __device__ __forceinline__ void chain_block00(const PanelArgs<T>& a, double* M, 
 }
 
 // ---- CHAIN, 4 waves (a 256-thread workgroup of either launch).  Per block
-// j: the diagonal factor (diag64_body), then -- on the critical path -- the
-// write-back of L_jj, the TRSM of block (c, j), c = j + 1, and the own update
-// of (c, c), which is the next diagonal block.  Everything else is moved off
-// that path: the operands of block row c are loaded before the write-back
-// (their latency overlaps it); L_jj^{-1} and D_j are written by waves 1..3
-// while wave 0 runs the next block's first column pass (X and a copy of D
-// are intact until then); the L / W stores of (c, j) are not drained on the
-// path -- the flags DIAG[j] and REG[j][c] are raised after that pass's
-// barrier, every store drained (diag64_body's DRAIN0 / POST2); the own
-// update reads L = W / d from the W tile in LDS (X stays intact).
+// j: the diagonal factor (diag64_body) with its write-back, then the TRSM of
+// block (c, j), c = j + 1, and the own update of (c, c), which is the next
+// diagonal block.  The operands of block row c are loaded before the
+// write-back (their latency overlaps it; loaded unmasked -- a select would
+// wait for the load -- the elements of rows past the matrix and above the
+// diagonal only reach outputs that are never stored or used); the own update
+// reads L = W / d from the W tile in LDS.
 template <typename T>
 __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsigned* sh_ok) {
+  typedef Mfma<T> MF;
   T* const K = a.K;
   const int64_t ld = a.ld;
   const int k0 = a.k0, ldw = a.ldw;
@@ -382,25 +380,9 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
   const int nb = panel_nb(a);
   double* M = smem;
   double* X = smem + 64 * DS;
-  double* dsh = smem + 2 * 64 * DS;  // 64 doubles (diag64_body's pivots)
-  double* dsv = dsh + 64;            // 64: D of the block last factored (its write-back is deferred)
-  T* rdv = reinterpret_cast<T*>(dsv + 64);  // 64: 1 / d of the block in dsh
+  double* dsh = smem + 2 * 64 * DS;         // 64 doubles (diag64_body's pivots)
+  T* rdv = reinterpret_cast<T*>(dsh + 64);  // 64: 1 / d of the block in dsh
   if (a.Wprev) chain_block00<T, 4>(a, M, X);
-  // L^{-1} (identity-padded past b) and D of block jb (X, dsv); threads
-  // [t0, 256) -- waves 1..3 in the next block's first column pass
-  auto put_linv_d = [&](int jb, int tid, int t0) __attribute__((always_inline)) {
-    const int jp0 = k0 + 64 * jb, b = panel_bsz(a, jb);
-    T* Lb = a.Lb0 + (int64_t)jb * 64 * 64;
-    for (int idx = tid - t0; idx < 64 * 64; idx += 256 - t0) {
-      const int rr = idx >> 6, cc = idx & 63;
-      st_sc1(&Lb[idx], (T)(cc > rr ? 0.0 : ((rr >= b || cc >= b) ? (rr == cc ? 1.0 : 0.0) : X[rr * DS + cc])));
-    }
-    for (int t = tid - t0; t < b; t += 256 - t0) {
-      const double dk = dsv[t];
-      st_sc1(&a.D[jp0 + t], (T)dk);
-      if (!(fabs(dk) <= 1.7976931348623157e308)) atomicMin(a.info, jp0 + t + 1);  // first non-finite pivot
-    }
-  };
   for (int j = 0; j < nb; ++j) {
     const int tid = launder((int)threadIdx.x), lane = tid & 63;
     const TMap<4> m(tid);
@@ -409,19 +391,8 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
     T* Lb = a.Lb0 + (int64_t)j * 64 * 64;
     const bool more = j + 1 < nb;
     const int c = j + 1, r0 = k0 + 64 * c, rows = more ? panel_bsz(a, c) : 0;
-    // block j-1's L^{-1} / D (waves 1..3 during the first column pass) and
-    // flags (after its barrier: every store of this workgroup is complete)
-    auto idle0 = [&]() __attribute__((always_inline)) {
-      if (j >= 1) put_linv_d(j - 1, tid, 64);
-    };
-    auto post2 = [&]() __attribute__((always_inline)) {
-      if (j >= 1 && tid == 0) {
-        if (!(a.inject && j == 1)) st_sc1(&area[OP_DIAG + j - 1], 1u);
-        st_sc1(&area[OP_REG + (j - 1) * OP_NBMAX + j], 1u);
-      }
-    };
     // block row c's operands (helper c stored them write-through), loaded
-    // before L_jj's write-back: A(c, j) for the TRSM, the own block (c, c)
+    // before the write-back: A(c, j) for the TRSM, the own block (c, c)
     bool ok = true;
     T va[16];
     Acc<T> own[4];
@@ -431,31 +402,37 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
       CSTAMP(j0 / 64, 1);
       if (!ok) return;
       fetch_tile<T, true, 4>(tid, va, K + (int64_t)r0 * ld + j0, ld, rows, 64);
-      load_acc<T, true, true, 4>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
+      const T* src = K + (int64_t)r0 * ld + r0;
+#pragma unroll
+      for (int n = 0; n < 4; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int row = 16 * m.wr + MF::row(lane, g);
+          own[n][g] = ld_sc1(&src[(int64_t)(row < rows ? row : 0) * ld + 16 * n + (lane & 15)]);
+        }
     };
     if (j == 0 && !a.Wprev)
-      diag64_body<true, false, T, false, 4, decltype(pre_wb), false, decltype(idle0), 1, true, false, decltype(post2)>(
-          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
+      diag64_body<true, false, T, false, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
+                                                              pre_wb, nullptr, tid);
     else
-      diag64_body<true, false, T, true, 4, decltype(pre_wb), false, decltype(idle0), 1, true, false, decltype(post2)>(
-          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
+      diag64_body<true, false, T, true, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
+                                                             pre_wb, nullptr, tid);
     CSTAMP(j0 / 64, 2);
-    if (tid < 64) dsv[tid] = dsh[tid];  // D_j for its deferred write-back
-    if (!more) {  // the panel's last block: its L^{-1}, D and DIAG now
-      __syncthreads();
-      put_linv_d(j, tid, 0);
+    if (!more) {
       if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
-      else publish(&area[OP_DIAG + OP_NBMAX]);  // (timeout tests: DIAG[0] never raised; a spare word)
       break;
     }
     if (!ok) return;
-    // A(c, j) into M (L_jj's write-back has read it), 1 / d of block j
+    // A(c, j) into M (free: the write-back has read L_jj), 1 / d of block j
     put_tile<T, 4>(tid, reinterpret_cast<T*>(M), va, rows, 64);
     if (tid < 64) rdv[tid] = T(1) / (T)dsh[tid];
     T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) rd[n] = T(1) / (T)dsh[16 * n + (lane & 15)];
-    __syncthreads();
+    // DIAG[j] (its write-back drained beside the operand loads; inject:
+    // timeout tests only); publish's barrier also orders M and rdv
+    if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
+    else __syncthreads();
     CSTAMP(j0 / 64, 3);
     // TRSM: T = A(c, j) X_jj^T with X lower triangular (its upper part in
     // LDS is not meaningful: masked)
@@ -463,6 +440,10 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
     zero_acc<T, 4>(acc);
     mma_tile_lower<T, 4>(m, reinterpret_cast<const T*>(M),
                          [&](int r, int k) { return k <= r ? (T)X[r * DS + k] : T(0); }, acc);
+    // the own block's loads are waited for here, before the L / W stores
+    // (a wait at its first use after them would wait for those stores too)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) asm volatile("" ::"v"(own[n]));
     __syncthreads();  // M reads done
     CSTAMP(j0 / 64, 4);
     T* Lrow = K + (int64_t)r0 * ld + j0;
@@ -479,7 +460,10 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
     put_acc<T, 4>(m, Wm, acc);
     __syncthreads();
     mma_tile<T, true, 4>(m, Wm, [&](int r, int k) { return Wm[r * DS + k]; }, own, rdv);
-    __syncthreads();  // every wave's reads of M done
+    // W(c, j) for the helpers' and the rows roles' strips: published after
+    // the update, so the stores drain beside its MFMAs (publish's barrier
+    // also ends every wave's reads of M)
+    publish(&area[OP_REG + j * OP_NBMAX + c]);
     CSTAMP(j0 / 64, 5);
     // the next diagonal block, straight into diag64_body's image
 #pragma unroll
@@ -487,7 +471,7 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
       const int col = 16 * n + (lane & 15);
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
-        const int row = 16 * m.wr + Mfma<T>::row(lane, g);
+        const int row = 16 * m.wr + MF::row(lane, g);
         M[row * DS + col] = (row < rows && col <= row) ? (double)own[n][g] : (row == col ? 1.0 : 0.0);
       }
     }
@@ -1124,7 +1108,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
                                                                                            int rows_launch, int rows_prev) {
   // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
   // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
-  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64 + 64];
+  __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64];
   __shared__ unsigned sh_ok;
   int form = 0;
   const unsigned tu = draw_ticket(a, 4, rows_launch != 0, &form);
