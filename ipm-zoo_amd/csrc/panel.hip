@@ -896,14 +896,30 @@ __device__ __forceinline__ void helper(const PanelArgs<T>& a, int c, int form, d
     for (int q = 0; q <= c; ++q)
       if (!wait_flag(&area[OP_TILE + c * OP_NBMAX + q], a.err, sh_ok)) return;
   }
+  // The own tile (c, c) stays in registers over the steps, and tile (c, j+1),
+  // final after step j's last strip, is carried in registers into step j+1
+  // as its L(c, j+1) operand; the other tiles of the row go through global
+  // with the next one's loads in flight during the current strip.
   const int jlast = c - (form == 8 ? 3 : 2);
+  Acc<T> own[NN], carry[NN];
+  if (jlast >= 0) {
+    const TMap<NW> m(launder((int)threadIdx.x));
+    if (a.Wprev) load_acc<T, true, true, NW>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
+    else load_acc<T, false, true, NW>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
+  }
   for (int j = 0; j <= jlast; ++j) {
     const int tid = launder((int)threadIdx.x), lane = tid & 63;
     const TMap<NW> m(tid);
     const int j0 = k0 + 64 * j;
     T* Lb = a.Lb0 + (int64_t)j * 64 * 64;
-    if (j || a.Wprev) stage_tile<T, true, NW>(tid, As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
-    else stage_tile<T, false, NW>(tid, As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+    if (j == 0) {
+      if (a.Wprev) stage_tile<T, true, NW>(tid, As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+      else stage_tile<T, false, NW>(tid, As, K + (int64_t)r0 * ld + j0, ld, rows, 64);
+    } else {
+      put_acc<T, NW>(m, As, carry);
+    }
+    Acc<T> tA[NN];  // tile (c, c-1): the first strip's, loaded before the DIAG wait
+    load_acc<T, true, false, NW>(m, tA, K + (int64_t)r0 * ld + k0 + 64 * (c - 1), ld, rows, panel_bsz(a, c - 1));
     if (!wait_flag(&area[OP_DIAG + j], a.err, sh_ok)) return;
     stage_tile<T, true, NW>(tid, Bs, Lb, 64, 64, 64);
     T rd[NN];
@@ -923,27 +939,41 @@ __device__ __forceinline__ void helper(const PanelArgs<T>& a, int c, int form, d
     store_acc<T, true, false, NW>(m, acc, a.Wp + (int64_t)r0 * ldw + 64 * j, ldw, rows, 64);
     publish(&area[OP_REG + j * OP_NBMAX + c]);
     put_acc<T, NW>(m, As, lacc);
-    // strips: (c, q) -= L(c, j) W(q, j)^T, q = c, c-1 .. j+1: the own tile
-    // (its W in registers) first, the tile whose W the chain publishes
-    // (q = c-1 for j = c-2) last, its tile loaded before that wait -- so
-    // READY[c] follows REG[c-2][c-1] by one strip
-    for (int q = c; q > j; --q) {
+    put_acc<T, NW>(m, Bs, acc);
+    __syncthreads();
+    mma_tile<T, true, NW>(m, As, [&](int r, int k) { return Bs[r * DS + k]; }, own);  // (c, c) -= L W^T
+    __syncthreads();
+    // strips q = c-1 .. j+1: the tile whose W the chain publishes (q = j+1)
+    // last, so READY[c] follows that REG flag by one strip
+    for (int q = c - 1; q > j; --q) {
       const int q0 = k0 + 64 * q, qrows = panel_bsz(a, q);
-      Acc<T> tile[NN];
-      if (q == c) load_acc<T, true, true, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
-      else load_acc<T, true, false, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
-      if (q == c) {
-        put_acc<T, NW>(m, Bs, acc);
-      } else {
-        if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], a.err, sh_ok)) return;
-        stage_tile<T, true, NW>(tid, Bs, a.Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, 64);
-      }
+      if (!wait_flag(&area[OP_REG + j * OP_NBMAX + q], a.err, sh_ok)) return;
+      T vw[64 / NW];
+      fetch_tile<T, true, NW>(tid, vw, a.Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, 64);
+      Acc<T> tB[NN];
+      if (q - 1 > j)
+        load_acc<T, true, false, NW>(m, tB, K + (int64_t)r0 * ld + q0 - 64, ld, rows, panel_bsz(a, q - 1));
+      put_tile<T, NW>(tid, Bs, vw, qrows, 64);
       __syncthreads();
-      mma_tile<T, true, NW>(m, As, [&](int r, int k) { return Bs[r * DS + k]; }, tile);
-      if (q == c) store_acc<T, true, true, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, rows);
-      else store_acc<T, true, false, NW>(m, tile, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+      mma_tile<T, true, NW>(m, As, [&](int r, int k) { return Bs[r * DS + k]; }, tA);
+      if (q == j + 1 && j < jlast) {
+#pragma unroll
+        for (int i = 0; i < NN; ++i)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) carry[i][g] = tA[i][g];
+      } else {
+        store_acc<T, true, false, NW>(m, tA, K + (int64_t)r0 * ld + q0, ld, rows, qrows);
+      }
       __syncthreads();  // Bs reused by the next piece
+#pragma unroll
+      for (int i = 0; i < NN; ++i)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) tA[i][g] = tB[i][g];
     }
+  }
+  if (jlast >= 0) {
+    const TMap<NW> m(launder((int)threadIdx.x));
+    store_acc<T, true, true, NW>(m, own, K + (int64_t)r0 * ld + r0, ld, rows, rows);
   }
   publish(&area[OP_READY + c]);
   HSTAMP(r0 / 64, 0);

@@ -384,8 +384,20 @@ int main(int argc, char** argv) {
     int lo = 0, hi = 0;
     CK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     hipStream_t sA, sB, sC;
-    CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
-    CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+    const int rcu = std::getenv("KB_CUS") ? std::atoi(std::getenv("KB_CUS")) : 0;
+    if (rcu > 0) {  // chain stream on the top rcu CUs, trailing stream on the rest
+      hipDeviceProp_t pr;
+      CK(hipGetDeviceProperties(&pr, 0));
+      const int ncu = pr.multiProcessorCount;
+      std::vector<uint32_t> ma((ncu + 31) / 32, 0u), mb((ncu + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) (i >= ncu - rcu ? ma : mb)[i / 32] |= 1u << (i % 32);
+      CK(hipExtStreamCreateWithCUMask(&sA, (uint32_t)ma.size(), ma.data()));
+      CK(hipExtStreamCreateWithCUMask(&sB, (uint32_t)mb.size(), mb.data()));
+      std::printf("chain stream on %d of %d CUs, trailing on the rest\n", rcu, ncu);
+    } else {
+      CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
+      CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+    }
     CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
     static unsigned long long cs[IPMZ_CHAIN_STAMP_BLOCKS][16], hs[IPMZ_CHAIN_STAMP_BLOCKS][4];
     for (int rep = 0; rep < 4; ++rep) {
