@@ -315,16 +315,18 @@ int64_t ipmz_ldlt_workspace_bytes(ipmz_ctx* ctx, int N) {
   return ws_layout(N, nbo_for(ctx, N), ctx->nbi).total;
 }
 
-static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, char* ws, TrailTimer* timer) {
+// info2: a caller's own info word, reset in the same launch
+static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, char* ws, TrailTimer* timer,
+                       int* info2 = nullptr) {
   const WsLayout l = ws_layout(N, nbo_for(ctx, N), ctx->nbi);
   int* info = reinterpret_cast<int*>(ws + l.info_off);
   double* Linv = reinterpret_cast<double*>(ws + l.linv_off);
   double* W = reinterpret_cast<double*>(ws + l.w_off);
   unsigned* pctrl = reinterpret_cast<unsigned*>(ws + l.pctrl_off);
-  HIP_OK(hipMemsetAsync(info, 0x7f, sizeof(int), ctx->stream));
-  HIP_OK(hipMemsetAsync(pctrl, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * sizeof(unsigned), ctx->stream));
+  // one launch: info, the panel ctrl words and the persistent solve's state
+  // for this factor
   HIP_OK(solve_reset(ws + l.y_off, ws + l.z_off, sizeof(double), N, reinterpret_cast<unsigned*>(ws + l.ctrl_off),
-                     ctx->stream));  // the persistent solve's state for this factor
+                     ctx->stream, info, pctrl, panel_ctrl_words(N, nbo_for(ctx, N)), info2));
   const int nbo = nbo_for(ctx, N);
   const int npan = (N + nbo - 1) / nbo;
   // the persistent solve's per-block operators, built once from this factor
@@ -408,10 +410,10 @@ int ipmz_ldlt_prepare_solve(ipmz_ctx* ctx, int N, const double* L, int64_t ld, v
     HIP_OK(solve_prep(L, ld, N, reinterpret_cast<const double*>(static_cast<char*>(ws) + l.linv_off),
                       reinterpret_cast<double*>(static_cast<char*>(ws) + l.prep_off), ctx->stream));
   // no factorization ran in this workspace: clear its sticky error words
-  HIP_OK(hipMemsetAsync(static_cast<char*>(ws) + l.pctrl_off, 0, panel_ctrl_words(N, nbo_for(ctx, N)) * 4,
-                        ctx->stream));
   HIP_OK(solve_reset(static_cast<char*>(ws) + l.y_off, static_cast<char*>(ws) + l.z_off, sizeof(double), N,
-                     reinterpret_cast<unsigned*>(static_cast<char*>(ws) + l.ctrl_off), ctx->stream));
+                     reinterpret_cast<unsigned*>(static_cast<char*>(ws) + l.ctrl_off), ctx->stream, nullptr,
+                     reinterpret_cast<unsigned*>(static_cast<char*>(ws) + l.pctrl_off),
+                     panel_ctrl_words(N, nbo_for(ctx, N))));
   return IPMZ_OK;
 }
 
@@ -505,8 +507,7 @@ NormalWs normal_ws(char* base, int n, int mp, const ipmz_ctx* ctx) {
 static int normal_factor_impl(ipmz_ctx* ctx, int n, int mp, double* K, int64_t ld, double* D, const NormalWs& w,
                               TrailTimer* timer) {
   hipStream_t st = ctx->stream;
-  HIP_OK(hipMemsetAsync(w.info, 0x7f, sizeof(int), st));
-  int rc = factor_impl(ctx, n + mp, K, ld, D, w.wsK, timer);
+  int rc = factor_impl(ctx, n + mp, K, ld, D, w.wsK, timer, w.info);
   if (rc) return rc;
   HIP_OK(ne_check_sign(D, n, 0, 1.0, w.info, st));
   HIP_OK(ne_check_sign(D + n, mp, n, -1.0, w.info, st));

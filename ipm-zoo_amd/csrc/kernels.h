@@ -6,6 +6,9 @@
 
 #define IPMZ_NBO_MAX 512
 #define IPMZ_PANEL_CTRL_WORDS 256
+// fused factor: largest N whose chain launches start beside the previous
+// panel's rows launch (ldlt.hip)
+#define IPMZ_EARLY_CHAIN_MAX_N 4096
 #define IPMZ_CHAIN_STAMP_BLOCKS 512  // (debug stamps: N <= 32768)
 #define IPMZ_SOLVE_BLOCK 128     // rows per block of the persistent solve
 #define IPMZ_SOLVE_CTRL_WORDS 8  // its control words (error, tickets, sweep counters)
@@ -128,11 +131,13 @@ inline int64_t panel_ctrl_words(int N, int nbo) {
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
                         const double* pre00_in, double* pre00_out,
                         int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
-                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows,
+                        const unsigned* parea = nullptr);
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                         const float* pre00_in, float* pre00_out,
                         int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
-                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows);
+                        bool rows_prev, hipStream_t st_chain, hipStream_t st_rows,
+                        const unsigned* parea = nullptr);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,
@@ -155,8 +160,11 @@ hipError_t ldlt_solve_batched(const double* K, int64_t ld, int N, const double* 
 int64_t solve_prep_elems(int N);
 // the persistent solve's state after a factorization: control words zero,
 // y / x buffers (N elements of size elem) all-ones sentinels; the solve
-// launches keep it so for the next solve
-hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st);
+// launches keep it so for the next solve.  Optionally in the same launch:
+// info / info2 words set to 0x7f7f7f7f ("no failed pivot") and nwords words
+// zeroed (a factor's panel ctrl words)
+hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st,
+                       int* info = nullptr, unsigned* words = nullptr, int64_t nwords = 0, int* info2 = nullptr);
 hipError_t solve_stamps(unsigned long long* out);  // DEBUG
 hipError_t chain_stamps(unsigned long long* c, unsigned long long* h);  // DEBUG (-DIPMZ_CHAIN_STAMPS)
 hipError_t solve_prep(const double* K, int64_t ld, int N, const double* Linv, double* P, hipStream_t st);

@@ -509,6 +509,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   auto area = [&](int k) { return pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + k); };
   unsigned* err = pctrl ? pctrl + PANEL_ERR_WORD : nullptr;
   hipStream_t sC = (two && fused) ? st3 : st;  // rows launches
+  // early: panel k+1's chain launch does not wait for panel k's rows launch
+  // (flags cover what it reads: RDONE).  It then holds its CUs beside that
+  // launch's tail -- a gain where the panel chain is the critical path (small
+  // N), a loss where the trailing GEMM is (it waits for that tail)
+  const bool early = two && fused && N <= IPMZ_EARLY_CHAIN_MAX_N;
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
   T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
@@ -518,7 +523,8 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (!fused) return factor_panel(K, ld, N, D, Linv, Wb(k), k0, pw(k), nbo, nbi, info, st);
     return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo,
                         (two && prev) ? slot00(k) : nullptr, two ? slot00(k + 1) : nullptr, info, area(k), err,
-                        prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC);
+                        prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC,
+                        (early && prev) ? area(k - 1) : nullptr);
   };
   hipError_t e = hipSuccess;
   if (!two) {  // single stream: factor, then the whole trailing update
@@ -555,7 +561,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   if (fused) {
     if ((e = stream_record(evA[0], st)) != hipSuccess) return e;
     if ((e = stream_record(evC[0], sC)) != hipSuccess) return e;
-    if ((e = stream_wait(st, evC[0])) != hipSuccess) return e;
+    if (!early && (e = stream_wait(st, evC[0])) != hipSuccess) return e;
   }
   for (int k = 0; k < npan; ++k) {
     const int k0 = k * nbo, bo = pw(k);
@@ -568,10 +574,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     // ---- stream B: P_{k+2} columns first, then the rest (four streams: the
     // P_{k+2} strip on st4 after B's previous trailing update, which last
     // touched those columns; B goes straight on with the rest)
+    // (early: panel k's rows launch on C as well -- A no longer waits for it)
     if ((e = stream_wait(st2, evP[k])) != hipSuccess) return e;
+    if (early && (e = stream_wait(st2, evC[k])) != hipSuccess) return e;
     hipStream_t sN = four ? st4 : st2;  // the stream of the P_{k+2} strip and N_k
     if (four) {
       if ((e = stream_wait(st4, evP[k])) != hipSuccess) return e;
+      if (early && (e = stream_wait(st4, evC[k])) != hipSuccess) return e;
       if (k >= 1 && (e = stream_wait(st4, evT[k - 1])) != hipSuccess) return e;
     }
     if (p2 < N) {
@@ -606,12 +615,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if ((e = factor(k + 1, true)) != hipSuccess) return e;
       if ((e = stream_record(evA[k + 1], st)) != hipSuccess) return e;
       if ((e = stream_record(evC[k + 1], sC)) != hipSuccess) return e;
-      if ((e = stream_wait(st, evC[k + 1])) != hipSuccess) return e;
+      if (!early && (e = stream_wait(st, evC[k + 1])) != hipSuccess) return e;
     } else {
       if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
       if ((e = factor(k + 1, false)) != hipSuccess) return e;
     }
   }
+  if (early && (e = stream_wait(st, evC[npan - 1])) != hipSuccess) return e;  // the last rows launch
   if ((e = stream_record(evJoin, st2)) != hipSuccess) return e;
   if (four) {
     if ((e = stream_record(evJoin4, st4)) != hipSuccess) return e;

@@ -257,10 +257,9 @@ hipError_t mixed_factor(const double* K, int64_t ld, MixedWs& w, hipStream_t st,
   if (N <= 0) return hipSuccess;
   hipLaunchKernelGGL(k_mx_scale, dim3((N + MNT - 1) / MNT), dim3(MNT), 0, st, K, ld, N, w.s);
   hipLaunchKernelGGL(k_mx_to_f32, dim3(N), dim3(MNT), 0, st, K, ld, N, w.s, w.K32, w.ld32);
-  hipError_t e = hipMemsetAsync(w.info, 0x7f, sizeof(int), st);
+  hipError_t e = solve_reset(w.y32, w.z32, sizeof(float), N, w.ctrl, st, w.info, w.pctrl,
+                             panel_ctrl_words(N, w.nbo));
   if (e != hipSuccess) return e;
-  if ((e = hipMemsetAsync(w.pctrl, 0, panel_ctrl_words(N, w.nbo) * sizeof(unsigned), st)) != hipSuccess) return e;
-  if ((e = solve_reset(w.y32, w.z32, sizeof(float), N, w.ctrl, st)) != hipSuccess) return e;
   if (debug_inject_mask() & IPMZ_DEBUG_CONVERT_ONLY) return hipGetLastError();
   return ldlt_factor(w.K32, w.ld32, N, w.D32, w.Linv32, w.W32, w.nbo, 64, w.info, st, timer, st2, st3, ev, nev,
                      w.pctrl, st4);

@@ -82,11 +82,12 @@ namespace {
 // ctrl words of a panel: OP_TICKET (chain tickets 1.., rows tickets), OP_FORM
 // (claimed by the workgroup that runs the chain: 4 or 8, its wave count --
 // the helpers' contract depends on it), DIAG[j], REG[j][q], READY[c], TILE[c][q]
-enum { OP_TICKET = 0, OP_FORM = 2, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128 };
+enum { OP_TICKET = 0, OP_FORM = 2, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128, OP_RDONE = 192 };
 constexpr int OP_NBMAX = IPMZ_NBO_MAX / 64;
 static_assert(OP_DIAG + OP_NBMAX <= OP_REG && OP_REG + OP_NBMAX * OP_NBMAX <= OP_READY, "ctrl layout");
 static_assert(OP_READY + OP_NBMAX <= OP_TILE, "ctrl layout");
-static_assert(OP_TILE + OP_NBMAX * OP_NBMAX <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
+static_assert(OP_TILE + OP_NBMAX * OP_NBMAX <= OP_RDONE, "ctrl layout");
+static_assert(OP_RDONE + OP_NBMAX <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
 
 // area[OP_TICKET]: TK_CLAIM | the chain's form (TK_F4: chain4, TK_F8: chain8)
 // | (chain tickets drawn) * TK_ONE -- one word, so the chain's form is fixed
@@ -193,13 +194,13 @@ __device__ __forceinline__ void stage_tile(int tid, T* dst, const T* src, int64_
 // one 64 x 64 tile with the previous outer panel (W_prev rows at Wr, ld ldw;
 // L_prev rows at Lr, ld ld; both written by earlier launches), 64-deep
 // chunks staged through As / Bs with the next chunk's loads in flight.
-template <typename T, int NW>
+template <typename T, int NW, bool SC = false>
 __device__ __forceinline__ void prev_update(int tid, Acc<T> (&acc)[TMap<NW>::NN], const T* Wr, int64_t ldw,
                                             const T* Lr, int64_t ld, int rows, int qrows, int bop, T* As, T* Bs) {
   const TMap<NW> m(tid);
   T va[64 / NW], vb[64 / NW];
-  fetch_tile<T, false, NW>(tid, va, Wr, ldw, rows, bop < 64 ? bop : 64);
-  fetch_tile<T, false, NW>(tid, vb, Lr, ld, qrows, bop < 64 ? bop : 64);
+  fetch_tile<T, SC, NW>(tid, va, Wr, ldw, rows, bop < 64 ? bop : 64);
+  fetch_tile<T, SC, NW>(tid, vb, Lr, ld, qrows, bop < 64 ? bop : 64);
   for (int kk = 0; kk < bop; kk += 64) {
     const int kw = bop - kk < 64 ? bop - kk : 64;
     __syncthreads();  // previous chunk's reads of As / Bs done
@@ -208,8 +209,8 @@ __device__ __forceinline__ void prev_update(int tid, Acc<T> (&acc)[TMap<NW>::NN]
     __syncthreads();
     if (kk + 64 < bop) {
       const int kn = bop - kk - 64 < 64 ? bop - kk - 64 : 64;
-      fetch_tile<T, false, NW>(tid, va, Wr + kk + 64, ldw, rows, kn);
-      fetch_tile<T, false, NW>(tid, vb, Lr + kk + 64, ld, qrows, kn);
+      fetch_tile<T, SC, NW>(tid, va, Wr + kk + 64, ldw, rows, kn);
+      fetch_tile<T, SC, NW>(tid, vb, Lr + kk + 64, ld, qrows, kn);
     }
     mma_tile<T, false, NW>(m, As, [&](int r, int k) { return Bs[r * DS + k]; }, acc);
   }
@@ -324,6 +325,10 @@ struct PanelArgs {
   int kprev, boprev;
   const T* pre00_in;  // this panel's block (0, 0) update, accumulated by the previous rows role 0
   T* pre00_out;       // the next panel's, accumulated by rows role 0
+  // the previous panel's ctrl area when its rows launch may still run beside
+  // this launch: its rows roles r < OP_NBMAX (this panel's rows) raise
+  // RDONE[r] once their L / W rows (and pre00) are stored write-through
+  const unsigned* parea;
   int nchain;         // chain-role tickets
   int nrows;          // rows-role tickets
 };
@@ -342,7 +347,9 @@ __device__ __forceinline__ int panel_bsz(const PanelArgs<T>& a, int j) {
 // Block (0, 0) of the panel with the previous panel's update, straight into
 // diag64_body's image M (all NW waves)
 template <typename T, int NW>
-__device__ __forceinline__ void chain_block00(const PanelArgs<T>& a, double* M, double* X) {
+__device__ __forceinline__ bool chain_block00(const PanelArgs<T>& a, double* M, double* X) {
+  __shared__ unsigned sh_w;
+  if (a.parea && !wait_flag(const_cast<unsigned*>(&a.parea[OP_RDONE]), a.err, &sh_w)) return false;
   const int tid = launder((int)threadIdx.x);
   const TMap<NW> m(tid);
   const int k0 = a.k0, b0 = panel_bsz(a, 0);
@@ -350,16 +357,24 @@ __device__ __forceinline__ void chain_block00(const PanelArgs<T>& a, double* M, 
   if (a.pre00_in) {
     // accumulated by the previous panel's rows role 0 (the same MFMA order as
     // prev_update), so this role starts with the diagonal factor
-    load_acc<T, false, false, NW>(m, own, a.pre00_in, 64, 64, 64);
+    if (a.parea) load_acc<T, true, false, NW>(m, own, a.pre00_in, 64, 64, 64);
+    else load_acc<T, false, false, NW>(m, own, a.pre00_in, 64, 64, 64);
   } else {
     zero_acc<T, TMap<NW>::NN>(own);
-    prev_update<T, NW>(tid, own, a.Wprev + (int64_t)k0 * a.ldw, a.ldw, a.K + (int64_t)k0 * a.ld + a.kprev, a.ld, b0,
-                       b0, a.boprev, reinterpret_cast<T*>(M), reinterpret_cast<T*>(X));
+    const T* Wr = a.Wprev + (int64_t)k0 * a.ldw;
+    const T* Lr = a.K + (int64_t)k0 * a.ld + a.kprev;
+    if (a.parea)
+      prev_update<T, NW, true>(tid, own, Wr, a.ldw, Lr, a.ld, b0, b0, a.boprev, reinterpret_cast<T*>(M),
+                               reinterpret_cast<T*>(X));
+    else
+      prev_update<T, NW>(tid, own, Wr, a.ldw, Lr, a.ld, b0, b0, a.boprev, reinterpret_cast<T*>(M),
+                         reinterpret_cast<T*>(X));
   }
   Acc<T> a0[TMap<NW>::NN];
   load_acc<T, false, true, NW>(m, a0, a.K + (int64_t)k0 * a.ld + k0, a.ld, b0, b0);
   put_diag_image<T, NW>(m, M, a0, own, b0);
   // (diag64_body's first barrier orders these stores before its reads)
+  return true;
 }
 
 // ---- CHAIN, 4 waves (a 256-thread workgroup of either launch).  Per block
@@ -382,7 +397,7 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
   double* X = smem + 64 * DS;
   double* dsh = smem + 2 * 64 * DS;         // 64 doubles (diag64_body's pivots)
   T* rdv = reinterpret_cast<T*>(dsh + 64);  // 64: 1 / d of the block in dsh
-  if (a.Wprev) chain_block00<T, 4>(a, M, X);
+  if (a.Wprev && !chain_block00<T, 4>(a, M, X)) return;
   for (int j = 0; j < nb; ++j) {
     const int tid = launder((int)threadIdx.x), lane = tid & 63;
     const TMap<4> m(tid);
@@ -525,7 +540,7 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
   T* Wb = reinterpret_cast<T*>(smem + 2 * 64 * DS + 64);  // 64 x DS: W of the row block last formed
   T* rdb = Wb + 64 * DS;                                  // 64: 1 / d of the block last factored
   if (threadIdx.x == 0) *sh_abort = 0u;
-  if (a.Wprev) chain_block00<T, 8>(a, M, X);  // (its barriers / diag64_body's first order sh_abort too)
+  if (a.Wprev && !chain_block00<T, 8>(a, M, X)) return;  // (its barriers / diag64_body's first order sh_abort too)
   const bool chain_group = __builtin_amdgcn_readfirstlane(threadIdx.x >> 8) == 0;  // (a uniform branch)
   if (chain_group) {
     for (int j = 0; j < nb; ++j) {
@@ -853,7 +868,7 @@ __device__ __forceinline__ void chain8(const PanelArgs<T>& a, double* smem, unsi
 // ---- TILE WORKER: region block (c, q), 1 <= c < nb, q <= c: the look-ahead
 // update with the previous panel, stored write-through, then TILE[c][q]
 template <typename T, int NW>
-__device__ __forceinline__ void tile_worker(const PanelArgs<T>& a, int t, double* smem) {
+__device__ __forceinline__ void tile_worker(const PanelArgs<T>& a, int t, double* smem, unsigned* sh_ok) {
   const int tid = launder((int)threadIdx.x);
   const TMap<NW> m(tid);
   const int nb = panel_nb(a);
@@ -865,8 +880,18 @@ __device__ __forceinline__ void tile_worker(const PanelArgs<T>& a, int t, double
   const int q = w, r0 = a.k0 + 64 * c, q0 = a.k0 + 64 * q, rows = panel_bsz(a, c), qrows = panel_bsz(a, q);
   Acc<T> upd[TMap<NW>::NN], tile[TMap<NW>::NN];
   zero_acc<T, TMap<NW>::NN>(upd);
-  prev_update<T, NW>(tid, upd, a.Wprev + (int64_t)r0 * a.ldw, a.ldw, a.K + (int64_t)q0 * a.ld + a.kprev, a.ld, rows,
-                     qrows, a.boprev, reinterpret_cast<T*>(smem), reinterpret_cast<T*>(smem + 64 * DS));
+  const T* Wr = a.Wprev + (int64_t)r0 * a.ldw;
+  const T* Lr = a.K + (int64_t)q0 * a.ld + a.kprev;
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
+  if (a.parea) {  // W rows c and L rows q from the previous panel's rows roles c and q
+    if (!wait_flag(const_cast<unsigned*>(&a.parea[OP_RDONE + c]), a.err, sh_ok) ||
+        !wait_flag(const_cast<unsigned*>(&a.parea[OP_RDONE + q]), a.err, sh_ok))
+      return;
+    prev_update<T, NW, true>(tid, upd, Wr, a.ldw, Lr, a.ld, rows, qrows, a.boprev, As, Bs);
+  } else {
+    prev_update<T, NW>(tid, upd, Wr, a.ldw, Lr, a.ld, rows, qrows, a.boprev, As, Bs);
+  }
   T* dst = a.K + (int64_t)r0 * a.ld + q0;
   if (q == c) load_acc<T, false, true, NW>(m, tile, dst, a.ld, rows, rows);
   else load_acc<T, false, false, NW>(m, tile, dst, a.ld, rows, qrows);
@@ -984,7 +1009,7 @@ template <typename T>
 __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, int form, double* smem, unsigned* sh_ok) {
   const int nb = panel_nb(a);
   if (t == 0) chain4<T>(a, smem, sh_ok);
-  else if (t >= nb) tile_worker<T, 4>(a, t, smem);
+  else if (t >= nb) tile_worker<T, 4>(a, t, smem, sh_ok);
   else helper<T, 4>(a, t, form, smem, sh_ok);
 }
 
@@ -1030,6 +1055,7 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
   // would sum in the next chain role -- and leaves it in pre00_out.
   if (r == 0) HSTAMP(k0 / 64, 1);
   T* const p00 = r == 0 ? a.pre00_out : nullptr;
+  const bool wt = r < OP_NBMAX;  // rows of the next panel's diagonal region: RDONE[r]
   Acc<T> a00[4];
   zero_acc<T, 4>(a00);
   bool ok = true;
@@ -1058,8 +1084,13 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
     for (int n = 0; n < 4; ++n)
 #pragma unroll
       for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
-    store_acc<T, false, false, 4>(m, lacc, Krow + j0, ld, rows, bj);
-    store_acc<T, false, false, 4>(m, acc, a.Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
+    if (wt) {  // the next panel's launch may read them before this launch ends
+      store_acc<T, true, false, 4>(m, lacc, Krow + j0, ld, rows, bj);
+      store_acc<T, true, false, 4>(m, acc, a.Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
+    } else {
+      store_acc<T, false, false, 4>(m, lacc, Krow + j0, ld, rows, bj);
+      store_acc<T, false, false, 4>(m, acc, a.Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
+    }
     put_acc<T, 4>(m, As, lacc);
     if (p00) {  // a00 += W(rows, j) L(rows, j)^T (W staged in Bs, L in As)
       put_acc<T, 4>(m, Bs, acc);
@@ -1080,7 +1111,8 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
       __syncthreads();
     }
   }
-  if (p00 && ok) store_acc<T, false, false, 4>(TMap<4>(launder((int)threadIdx.x)), a00, p00, 64, 64, 64);
+  if (p00 && ok) store_acc<T, true, false, 4>(TMap<4>(launder((int)threadIdx.x)), a00, p00, 64, 64, 64);
+  if (wt && ok) publish(&a.area[OP_RDONE + r]);
   if (r == 0) HSTAMP(k0 / 64, 2);
 }
 
@@ -1175,11 +1207,25 @@ __global__ __launch_bounds__(512) void panel_chain8_kernel(PanelArgs<double> a, 
 }
 
 // ---------------------------------------------------------------------------
+// dynamic LDS of the chain launch on top of panel_kernel's static 66.5 KB:
+// 95 KB in all, more than a CU has left beside another panel workgroup
+// (66.5 KB), so no two share a CU; one trailing-GEMM workgroup (48 KB) still
+// fits beside it
+template <typename T>
+static size_t chain_lds_pad() {
+  constexpr size_t total = 95 * 1024, own = (2 * 64 * DS + 64 + 64) * sizeof(double) + 64;
+  static const bool set = [] {
+    return hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel<T>),
+                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)(total - own)) == hipSuccess;
+  }();
+  return set ? total - own : 0;
+}
+
 template <typename T>
 static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw,
                                  const T* pre00_in, T* pre00_out, int* info,
                                  unsigned* area, unsigned* err, const T* Wprev, int kprev, int boprev, bool rows_prev,
-                                 hipStream_t st_chain, hipStream_t st_rows) {
+                                 hipStream_t st_chain, hipStream_t st_rows, const unsigned* parea) {
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
   const int ce = k0 + bo;
   const int nb = (bo + 63) / 64;
@@ -1202,6 +1248,7 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   a.boprev = boprev;
   a.pre00_in = Wprev ? pre00_in : nullptr;
   a.pre00_out = pre00_out;
+  a.parea = parea;
   // chain + nb - 1 helpers (+ one tile worker per region block below the
   // diagonal block (0, 0) when the look-ahead update is applied here)
   a.nchain = nb + (Wprev ? nb * (nb + 1) / 2 - 1 : 0);
@@ -1212,7 +1259,11 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
     if constexpr (std::is_same<T, double>::value)
       hipLaunchKernelGGL(panel_chain8_kernel, dim3(1), dim3(512), 0, st_chain, a, (dbg & IPMZ_DEBUG_ROWS_CHAIN) ? 0 : 1);
   } else if (!(dbg & IPMZ_DEBUG_ROWS_CHAIN)) {
-    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), 0, st_chain, a, 0, rows_prev ? 1 : 0);
+    // every chain role; the padding (dynamic LDS) makes each of its
+    // workgroups hold a CU with no other panel workgroup (the chain's
+    // barrier-bound blocks lose a third of their speed beside a helper)
+    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(), st_chain, a, 0,
+                       rows_prev ? 1 : 0);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1226,16 +1277,16 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
                         const double* pre00_in, double* pre00_out, int* info, unsigned* area, unsigned* err,
                         const double* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
-                        hipStream_t st_rows) {
+                        hipStream_t st_rows, const unsigned* parea) {
   return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                                boprev, rows_prev, st_chain, st_rows);
+                                boprev, rows_prev, st_chain, st_rows, parea);
 }
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                         const float* pre00_in, float* pre00_out, int* info, unsigned* area, unsigned* err,
                         const float* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
-                        hipStream_t st_rows) {
+                        hipStream_t st_rows, const unsigned* parea) {
   return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                               boprev, rows_prev, st_chain, st_rows);
+                               boprev, rows_prev, st_chain, st_rows, parea);
 }
 
 }  // namespace ipmz

@@ -90,18 +90,23 @@ __device__ __forceinline__ T lanes16_sum(T v) {
 // ---------------------------------------------------------------------------
 // prep helpers: 64 x 64 fp64 tiles in LDS (stride TDS), 256 threads, the
 // v_mfma_f64_16x16x4 layout of Mfma<double> (wave w: output rows 16w..16w+15)
+// a 64 x 64 tile into registers (16 loads in flight per thread; f(r, c)
+// coalesced along c), then into LDS as is or transposed
 template <typename F>
-__device__ __forceinline__ void stage64(double* dst, F f) {
-  double v[16];  // all 16 loads in flight
+__device__ __forceinline__ void fetch64(double (&v)[16], F f) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int i = threadIdx.x + 256 * q;
     v[q] = f(i >> 6, i & 63);
   }
+}
+template <bool TR>
+__device__ __forceinline__ void put64(double* dst, const double (&v)[16]) {
 #pragma unroll
   for (int q = 0; q < 16; ++q) {
     const int i = threadIdx.x + 256 * q;
-    dst[(i >> 6) * TDS + (i & 63)] = v[q];
+    if (TR) dst[(i & 63) * TDS + (i >> 6)] = v[q];
+    else dst[(i >> 6) * TDS + (i & 63)] = v[q];
   }
 }
 // acc[n] += op(A)[16w.., :] B[:, 16n..], op(A) = A or A^T
@@ -143,16 +148,21 @@ __device__ __forceinline__ void out4(T* dst, int r0, int c0, const double4_t (&a
 }
 }  // namespace
 
-// One workgroup per 128-row block J: X_J from the two 64 x 64 inverses
-// (X = [[Xa, 0], [-Xb L_ba Xa, Xb]]), then M_J and Q_J (fp64 MFMA, stored
-// as T).  Rows / columns past N are zero.
+// Five workgroups per 128-row block J (blockIdx.y = part): each builds
+// X_J from the two 64 x 64 inverses (X = [[Xa, 0], [-Xb L_ba Xa, Xb]]);
+// part 0 stores X_J and X_J^T, parts 1-2 the column halves of M_J, parts 3-4
+// those of Q_J (fp64 MFMA, stored as T).  A part's two L operands are loaded
+// with the X operands.  Rows / columns past N are zero.
 template <typename T>
 __global__ __launch_bounds__(256) void solve_prep_kernel(const T* __restrict__ K, int64_t ld, int N,
                                                          const T* __restrict__ Linv, T* __restrict__ X,
                                                          T* __restrict__ XT, T* __restrict__ M, T* __restrict__ Q,
                                                          int nb) {
   __shared__ double S[4][64 * TDS];  // 133 KB: Xa, Xb, X21, one L operand
-  const int J = blockIdx.x, J0 = J * SB;
+  const int J = blockIdx.x, part = blockIdx.y, J0 = J * SB;
+  if ((part == 1 || part == 2) && J == 0) return;
+  if (part >= 3 && J + 1 >= nb) return;
+  const int h = (part - 1) & 1;
   const int R = N - J0 < SB ? N - J0 : SB;
   const bool two = R > 64;
   double* Xa = S[0];
@@ -161,9 +171,22 @@ __global__ __launch_bounds__(256) void solve_prep_kernel(const T* __restrict__ K
   double* Ls = S[3];
   auto Kat = [&](int r, int c) -> double { return (r < N && c < N) ? (double)K[(int64_t)r * ld + c] : 0.0; };
   const int64_t lb = (int64_t)2 * J * 64 * 64;  // Linv block of rows J0 .. J0+63
-  stage64(Xa, [&](int r, int c) { return (double)Linv[lb + r * 64 + c]; });
-  stage64(Xb, [&](int r, int c) { return two ? (double)Linv[lb + 4096 + r * 64 + c] : 0.0; });
-  stage64(Ls, [&](int r, int c) { return two ? Kat(J0 + 64 + r, J0 + c) : 0.0; });  // L_ba
+  double v0[16], v1[16], v2[16], va[16], vb[16];
+  fetch64(v0, [&](int r, int c) { return (double)Linv[lb + r * 64 + c]; });
+  fetch64(v1, [&](int r, int c) { return two ? (double)Linv[lb + 4096 + r * 64 + c] : 0.0; });
+  fetch64(v2, [&](int r, int c) { return two ? Kat(J0 + 64 + r, J0 + c) : 0.0; });  // L_ba
+  if (part == 1 || part == 2) {  // L_{J,J-1}, column half h: rows a, rows b
+    const int C0 = J0 - SB + 64 * h;
+    fetch64(va, [&](int r, int c) { return Kat(J0 + r, C0 + c); });
+    fetch64(vb, [&](int r, int c) { return Kat(J0 + 64 + r, C0 + c); });
+  } else if (part >= 3) {  // L_{J+1,J}, row half h: columns a, columns b (transposed into LDS)
+    const int RR = J0 + SB + 64 * h;
+    fetch64(va, [&](int r, int c) { return Kat(RR + r, J0 + c); });
+    fetch64(vb, [&](int r, int c) { return Kat(RR + r, J0 + 64 + c); });
+  }
+  put64<false>(Xa, v0);
+  put64<false>(Xb, v1);
+  put64<false>(Ls, v2);
   __syncthreads();
   double4_t acc[4], bot[4];
   zero4(acc);
@@ -175,53 +198,45 @@ __global__ __launch_bounds__(256) void solve_prep_kernel(const T* __restrict__ K
   mm64<false>(acc, Xb, Ls);  // X21 = -Xb (L_ba Xa)
   put4(X21, acc, -1.0);
   __syncthreads();
-  T* Xo = X + (int64_t)J * SB * SB;
-  T* XTo = XT + (int64_t)J * SB * SB;
-  for (int i = threadIdx.x; i < SB * SB; i += 256) {
-    const int r = i >> 7, c = i & 127;
-    double v = 0.0;
-    if (r < R && c < R) v = r < 64 ? (c < 64 ? Xa[r * TDS + c] : 0.0)
-                                   : (c < 64 ? X21[(r - 64) * TDS + c] : Xb[(r - 64) * TDS + c - 64]);
-    Xo[r * SB + c] = (T)v;
-    XTo[c * SB + r] = (T)v;
+  if (part == 0) {
+    T* Xo = X + (int64_t)J * SB * SB;
+    T* XTo = XT + (int64_t)J * SB * SB;
+    for (int i = threadIdx.x; i < SB * SB; i += 256) {
+      const int r = i >> 7, c = i & 127;
+      double v = 0.0;
+      if (r < R && c < R) v = r < 64 ? (c < 64 ? Xa[r * TDS + c] : 0.0)
+                                     : (c < 64 ? X21[(r - 64) * TDS + c] : Xb[(r - 64) * TDS + c - 64]);
+      Xo[r * SB + c] = (T)v;
+      XTo[c * SB + r] = (T)v;
+    }
+    return;
   }
-  if (J > 0) {  // M_J = X_J L_{J,J-1}, by column halves of block J-1
+  zero4(acc);
+  zero4(bot);
+  if (part <= 2) {  // M_J = X_J L_{J,J-1}, column half h
     T* Mo = M + (int64_t)J * SB * SB;
-    for (int h = 0; h < 2; ++h) {
-      const int C0 = J0 - SB + 64 * h;
-      zero4(acc);
-      zero4(bot);
-      __syncthreads();
-      stage64(Ls, [&](int r, int c) { return Kat(J0 + r, C0 + c); });  // L_a,h
-      __syncthreads();
-      mm64<false>(acc, Xa, Ls);
-      mm64<false>(bot, X21, Ls);
-      __syncthreads();
-      stage64(Ls, [&](int r, int c) { return Kat(J0 + 64 + r, C0 + c); });  // L_b,h
-      __syncthreads();
-      mm64<false>(bot, Xb, Ls);
-      out4(Mo, 0, 64 * h, acc, R);
-      out4(Mo, 64, 64 * h, bot, R);
-    }
-  }
-  if (J + 1 < nb) {  // Q_J = X_J^T L_{J+1,J}^T, by column halves (= row halves of block J+1)
+    put64<false>(Ls, va);  // L_a,h
+    __syncthreads();
+    mm64<false>(acc, Xa, Ls);
+    mm64<false>(bot, X21, Ls);
+    __syncthreads();
+    put64<false>(Ls, vb);  // L_b,h
+    __syncthreads();
+    mm64<false>(bot, Xb, Ls);
+    out4(Mo, 0, 64 * h, acc, R);
+    out4(Mo, 64, 64 * h, bot, R);
+  } else {  // Q_J = X_J^T L_{J+1,J}^T, column half h (= row half of block J+1)
     T* Qo = Q + (int64_t)J * SB * SB;
-    for (int h = 0; h < 2; ++h) {
-      const int RR = J0 + SB + 64 * h;
-      zero4(acc);
-      zero4(bot);
-      __syncthreads();
-      stage64(Ls, [&](int r, int c) { return Kat(RR + c, J0 + r); });  // (L_{h,a})^T
-      __syncthreads();
-      mm64<true>(acc, Xa, Ls);
-      __syncthreads();
-      stage64(Ls, [&](int r, int c) { return Kat(RR + c, J0 + 64 + r); });  // (L_{h,b})^T
-      __syncthreads();
-      mm64<true>(acc, X21, Ls);
-      mm64<true>(bot, Xb, Ls);
-      out4(Qo, 0, 64 * h, acc, R);
-      out4(Qo, 64, 64 * h, bot, R);
-    }
+    put64<true>(Ls, va);  // (L_{h,a})^T
+    __syncthreads();
+    mm64<true>(acc, Xa, Ls);
+    __syncthreads();
+    put64<true>(Ls, vb);  // (L_{h,b})^T
+    __syncthreads();
+    mm64<true>(acc, X21, Ls);
+    mm64<true>(bot, Xb, Ls);
+    out4(Qo, 0, 64 * h, acc, R);
+    out4(Qo, 64, 64 * h, bot, R);
   }
 }
 
@@ -549,8 +564,8 @@ static hipError_t solve_prep_t(const T* K, int64_t ld, int N, const T* Linv, T* 
   if (N <= 0) return hipSuccess;
   const int nb = (N + SB - 1) / SB;
   const int64_t q = (int64_t)nb * SB * SB;
-  hipLaunchKernelGGL(solve_prep_kernel<T>, dim3(nb), dim3(256), 0, st, K, ld, N, Linv, P, P + q, P + 2 * q, P + 3 * q,
-                     nb);
+  hipLaunchKernelGGL(solve_prep_kernel<T>, dim3(nb, 5), dim3(256), 0, st, K, ld, N, Linv, P, P + q, P + 2 * q,
+                     P + 3 * q, nb);
   return hipGetLastError();
 }
 hipError_t solve_stamps(unsigned long long* out) {  // DEBUG
@@ -607,11 +622,44 @@ hipError_t ldlt_solve_persistent_sweep(const double* K, int64_t ld, int N, const
   return hipGetLastError();
 }
 
-hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st) {
-  hipError_t e = hipMemsetAsync(ctrl, 0, IPMZ_SOLVE_CTRL_WORDS * sizeof(unsigned), st);  // tickets + sticky error
-  if (e == hipSuccess) e = hipMemsetAsync(ybuf, 0xff, (size_t)N * elem, st);
-  if (e == hipSuccess) e = hipMemsetAsync(xbuf, 0xff, (size_t)N * elem, st);
-  return e;
+namespace {
+// up to 6 word ranges, each filled with its own value: one launch for what
+// would be one memset (and one launch gap) each
+struct FillJob {
+  unsigned* p[6];
+  int64_t n[6];
+  unsigned v[6];
+};
+__global__ __launch_bounds__(256) void fill_words_kernel(FillJob f) {
+  const int r = blockIdx.y;
+  unsigned* const p = f.p[r];
+  const unsigned v = f.v[r];
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < f.n[r]; i += (int64_t)gridDim.x * 256) p[i] = v;
+}
+}  // namespace
+
+hipError_t solve_reset(void* ybuf, void* xbuf, size_t elem, int N, unsigned* ctrl, hipStream_t st, int* info,
+                       unsigned* words, int64_t nwords, int* info2) {
+  FillJob f{};
+  int cnt = 0;
+  int64_t most = 0;
+  auto add = [&](void* p, int64_t n, unsigned v) {
+    if (!p || n <= 0) return;
+    f.p[cnt] = static_cast<unsigned*>(p);
+    f.n[cnt] = n;
+    f.v[cnt++] = v;
+    most = n > most ? n : most;
+  };
+  add(ctrl, IPMZ_SOLVE_CTRL_WORDS, 0u);  // tickets + sticky error
+  add(ybuf, (int64_t)N * (int64_t)elem / 4, ~0u);
+  add(xbuf, (int64_t)N * (int64_t)elem / 4, ~0u);
+  add(info, 1, 0x7f7f7f7fu);  // "no pivot failed" (the byte pattern of hipMemset 0x7f)
+  add(info2, 1, 0x7f7f7f7fu);
+  add(words, nwords, 0u);
+  if (!cnt) return hipSuccess;
+  const int64_t gx = (most + 255) / 256;
+  hipLaunchKernelGGL(fill_words_kernel, dim3((unsigned)(gx < 64 ? gx : 64), cnt), dim3(256), 0, st, f);
+  return hipGetLastError();
 }
 
 hipError_t ldlt_solve_persistent(const double* K, int64_t ld, int N, const double* D, const double* P, double* b,

@@ -393,12 +393,13 @@ int main(int argc, char** argv) {
       for (int i = 0; i < ncu; ++i) (i >= ncu - rcu ? ma : mb)[i / 32] |= 1u << (i % 32);
       CK(hipExtStreamCreateWithCUMask(&sA, (uint32_t)ma.size(), ma.data()));
       CK(hipExtStreamCreateWithCUMask(&sB, (uint32_t)mb.size(), mb.data()));
-      std::printf("chain stream on %d of %d CUs, trailing on the rest\n", rcu, ncu);
+      CK(hipExtStreamCreateWithCUMask(&sC, (uint32_t)mb.size(), mb.data()));
+      std::printf("chain stream on %d of %d CUs, trailing and rows on the rest\n", rcu, ncu);
     } else {
       CK(hipStreamCreateWithPriority(&sA, hipStreamNonBlocking, hi));
       CK(hipStreamCreateWithPriority(&sB, hipStreamNonBlocking, lo));
+      CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
     }
-    CK(hipStreamCreateWithPriority(&sC, hipStreamNonBlocking, hi));
     static unsigned long long cs[IPMZ_CHAIN_STAMP_BLOCKS][16], hs[IPMZ_CHAIN_STAMP_BLOCKS][4];
     for (int rep = 0; rep < 4; ++rep) {
       hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, sA, K, ld, N, 7ull);
