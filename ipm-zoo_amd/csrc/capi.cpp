@@ -1096,7 +1096,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   double* scal = dev_array(s, SC_COUNT, &sScal);
   double* scal0 = dev_array(s, SC_COUNT);
   double* part = dev_array(s, 4 * 1024, &sPart);
-  double* tpart = dev_array(s, (int64_t)((m > p ? m : p) + 127) / 128 * n + 8, &sT);
+  double* tpart = dev_array(s, (int64_t)((m > p ? m : p) + IPMZ_TCHUNK - 1) / IPMZ_TCHUNK * n + 8, &sT);
   int64_t sDone;
   double* done = dev_array(s, 1, &sDone);
   s->K = dev_array(s, (int64_t)N * s->ldk, &s->sK);

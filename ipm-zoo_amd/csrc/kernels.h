@@ -9,6 +9,8 @@
 // fused factor: largest N whose chain launches start beside the previous
 // panel's rows launch (ldlt.hip)
 #define IPMZ_EARLY_CHAIN_MAX_N 4096
+// rows per partial sum of the transposed mat-vecs A^T y, C^T y (newton.hip)
+#define IPMZ_TCHUNK 32
 #define IPMZ_CHAIN_STAMP_BLOCKS 512  // (debug stamps: N <= 32768)
 #define IPMZ_SOLVE_BLOCK 128     // rows per block of the persistent solve
 #define IPMZ_SOLVE_CTRL_WORDS 8  // its control words (error, tickets, sweep counters)
@@ -296,7 +298,7 @@ struct QPDev {
   double* b;      // augmented rhs / solution, length N
   double* scal;   // SC_COUNT doubles
   double* part;   // reduction partials
-  double* tpart;  // transposed-GEMV partials
+  double* tpart;  // transposed-GEMV partials: ceil(max(m, p) / IPMZ_TCHUNK) x n
   double* K;      // KKT / factor (N x ldk)
   double* K0;     // batches of small systems: the assembled KKT kept across steps (the factor reads it, writes L to K); nullptr: none
   double *v0, *r0, *scal0;  // initial iterate snapshot (benchmark restarts)

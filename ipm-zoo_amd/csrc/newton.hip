@@ -225,7 +225,7 @@ __device__ __forceinline__ double a_dual(const QPDev& q, int i) {
 
 // A^T lambda_A -> ATl, C^T lambda_C -> CTl: column blocks of NT x row chunks
 // of 128, deterministic two-pass (chunk partials, then an ordered sum).
-constexpr int TCHUNK = 128;
+constexpr int TCHUNK = IPMZ_TCHUNK;  // 32: C2's A^T (512 x 2048) in 128 workgroups, not 32
 template <int MV>
 __global__ __launch_bounds__(NT) void k_matvec_t_part(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.z];
@@ -236,6 +236,7 @@ __global__ __launch_bounds__(NT) void k_matvec_t_part(const QPDev* __restrict__ 
   if (j >= cols) return;
   const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
   double s = 0.0;
+#pragma unroll 8
   for (int i = i0; i < i1; ++i) s += M[(int64_t)i * q.ldn + j] * (MV == MV_A ? a_dual(q, i) : q.v[LC][i]);
   q.tpart[(int64_t)blockIdx.y * cols + j] = s;
 }
