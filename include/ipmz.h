@@ -90,6 +90,9 @@ typedef struct ipmz_qp ipmz_qp;
 
 /* ---- context ---------------------------------------------------------- */
 int ipmz_ctx_create(ipmz_ctx** out, int device);
+/* Destroying a context that solvers (ipmz_qp_create / ipmz_batch_create)
+ * still use only marks it: it is freed when the last of them is destroyed
+ * (so a garbage collector may finalize the two in either order). */
 int ipmz_ctx_destroy(ipmz_ctx* ctx);
 /* Enqueue on an external HIP stream, e.g. torch.cuda.current_stream().cuda_stream.
  * NULL selects the HIP null (legacy default) stream -- what PyTorch's

@@ -54,6 +54,11 @@ struct ipmz_ctx {
   // that workspace alive until then)
   const unsigned* check_pe = nullptr;
   const unsigned* check_se = nullptr;
+  // solvers created on this context and not yet destroyed: a context
+  // destroyed before them (e.g. a garbage collector finalizing both in either
+  // order) is only marked, and freed with the last of them
+  int users = 0;
+  bool closed = false;
 };
 
 // outer panel width for an order-N factor: the context's, or by size --
@@ -133,8 +138,7 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
   return IPMZ_OK;
 }
 
-int ipmz_ctx_destroy(ipmz_ctx* ctx) {
-  if (!ctx) return IPMZ_OK;
+static void ctx_free(ipmz_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
   for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB, ctx->sC, ctx->sD})
@@ -144,6 +148,12 @@ int ipmz_ctx_destroy(ipmz_ctx* ctx) {
     }
   for (auto e : ctx->evpool) hipEventDestroy(e);
   delete ctx;
+}
+
+int ipmz_ctx_destroy(ipmz_ctx* ctx) {
+  if (!ctx || ctx->closed) return IPMZ_OK;
+  ctx->closed = true;
+  if (ctx->users == 0) ctx_free(ctx);
   return IPMZ_OK;
 }
 
@@ -1047,6 +1057,7 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   HIP_OK(hipSetDevice(ctx->device));
   auto* s = new ipmz_qp();
   s->ctx = ctx;
+  ++ctx->users;
   s->B = B;
   s->n = cfg->n;
   s->m_usr = cfg->m;
@@ -1513,7 +1524,9 @@ int ipmz_qp_destroy(ipmz_qp* s) {
   for (void* p : s->allocs) hipFree(p);
   if (s->mw.hev) hipEventDestroy(s->mw.hev);
   if (s->mw.hst) hipHostFree(s->mw.hst);
+  ipmz_ctx* ctx = s->ctx;
   delete s;
+  if (--ctx->users == 0 && ctx->closed) ctx_free(ctx);
   return IPMZ_OK;
 }
 

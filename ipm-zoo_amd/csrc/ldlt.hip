@@ -600,6 +600,9 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (k >= 1) {
       if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
       if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
+      // early: panel k-1's rows launch (and C's strip before it) are the last
+      // readers of W buffer (k + 1) % 3 -- the one this chain launch writes
+      if (early && (e = stream_wait(st, evC[k - 1])) != hipSuccess) return e;
     }
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
