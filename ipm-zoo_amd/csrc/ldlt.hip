@@ -512,8 +512,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // early: panel k+1's chain launch does not wait for panel k's rows launch
   // (flags cover what it reads: RDONE).  It then holds its CUs beside that
   // launch's tail -- a gain where the panel chain is the critical path (small
-  // N), a loss where the trailing GEMM is (it waits for that tail)
-  const bool early = two && fused && N <= IPMZ_EARLY_CHAIN_MAX_N;
+  // N), a loss where the trailing GEMM is (it waits for that tail).  Never
+  // inside a graph capture: a replay may run the two launches in either order
+  // (no edge between them), and a chain launch spinning on a launch queued
+  // behind it would only end at the spin limit.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (two && fused && hipStreamIsCapturing(st, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
+  const bool early = two && fused && N <= IPMZ_EARLY_CHAIN_MAX_N && cap == hipStreamCaptureStatusNone;
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
   T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
