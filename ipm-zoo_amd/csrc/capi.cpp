@@ -44,9 +44,10 @@ struct ipmz_ctx {
   hipStream_t own = nullptr;
   hipStream_t stream = nullptr;
   int nbo = 0, nbi = 64;  // nbo 0: by matrix order (nbo_for)
-  // factorization look-ahead: panel chain on sA and panel rows on sC (high
-  // priority), trailing updates on sB; forked from / joined to `stream`
-  hipStream_t sA = nullptr, sB = nullptr, sC = nullptr, sD = nullptr;
+  // factorization look-ahead: the panel chain on `stream` itself, panel rows
+  // on sC (high priority), trailing updates on sB, the fp32 factor's
+  // look-ahead strips on sD; forked from / joined to `stream` (ldlt_factor)
+  hipStream_t sB = nullptr, sC = nullptr, sD = nullptr;
   std::vector<hipEvent_t> evpool;
   // the sticky error words (spin timeouts of the persistent kernels) of the
   // workspace the last asynchronous device-memory solve used, resolved when
@@ -85,17 +86,6 @@ static int ensure_events(ipmz_ctx* ctx, size_t n) {
 // caller's stream waits for each of them (the chain stream A has already
 // waited for B's and C's work; the explicit waits keep every stream a capture
 // forked joined back into its origin -- ldlt.hip stream_wait)
-static hipError_t join_side_streams(ipmz_ctx* ctx, hipEvent_t* ev4, bool fourth) {
-  hipStream_t side[4] = {ctx->sA, ctx->sB, ctx->sC, ctx->sD};
-  hipEvent_t* ev3 = ev4;
-  for (int i = 0; i < (fourth ? 4 : 3); ++i) {
-    hipError_t e = stream_record(ev3[i], side[i]);
-    if (e == hipSuccess) e = stream_wait(ctx->stream, ev3[i]);
-    if (e != hipSuccess) return e;
-  }
-  return hipSuccess;
-}
-
 static int check_device(int device) {
   int count = 0;
   if (hipGetDeviceCount(&count) != hipSuccess || count <= 0)
@@ -120,15 +110,15 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
   HIP_OK(hipSetDevice(device));
   auto* c = new ipmz_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+  int least = 0, greatest = 0;
+  hipDeviceGetStreamPriorityRange(&least, &greatest);
+  // own: the steps' stream, and the factor's panel chain (high priority)
+  if (hipStreamCreateWithPriority(&c->own, hipStreamNonBlocking, greatest) != hipSuccess) {
     delete c;
     return fail(IPMZ_ERR_HIP, "hipStreamCreate failed");
   }
   c->stream = c->own;
-  int least = 0, greatest = 0;
-  hipDeviceGetStreamPriorityRange(&least, &greatest);
-  if (hipStreamCreateWithPriority(&c->sA, hipStreamNonBlocking, greatest) != hipSuccess ||
-      hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess ||
+  if (hipStreamCreateWithPriority(&c->sB, hipStreamNonBlocking, least) != hipSuccess ||
       hipStreamCreateWithPriority(&c->sC, hipStreamNonBlocking, greatest) != hipSuccess ||
       hipStreamCreateWithPriority(&c->sD, hipStreamNonBlocking, greatest) != hipSuccess) {
     ipmz_ctx_destroy(c);
@@ -141,7 +131,7 @@ int ipmz_ctx_create(ipmz_ctx** out, int device) {
 static void ctx_free(ipmz_ctx* ctx) {
   hipSetDevice(ctx->device);
   if (ctx->stream) hipStreamSynchronize(ctx->stream);
-  for (hipStream_t s : {ctx->own, ctx->sA, ctx->sB, ctx->sC, ctx->sD})
+  for (hipStream_t s : {ctx->own, ctx->sB, ctx->sC, ctx->sD})
     if (s) {
       hipStreamSynchronize(s);
       hipStreamDestroy(s);
@@ -354,22 +344,17 @@ static int factor_impl(ipmz_ctx* ctx, int N, double* K, int64_t ld, double* D, c
   int rc = ensure_events(ctx, (size_t)nev + 4);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
-  // fork: A, C (panel path) and B (trailing updates) start after the caller's stream
-  IPMZ_TRACE("factor_impl: fork");
-  HIP_OK(stream_record(ev[nev - 2], ctx->stream));
-  HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
   // the fourth look-ahead stream pays for the fp32 factor only (C5 23.6 ->
   // 22.9 ms per step); the fp64 one runs faster without it (C3 14.2 -> 14.0
   // ms), profiles/r03_s5/fourth_stream_ab.log -- not forked at all here
   const bool fourth = false;
-  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->sA, timer, ctx->sB, ctx->sC, ev, nev - 2,
+  // the panel chain on the caller's stream itself: its first launch follows
+  // the assembly in stream order, with no cross-queue hop; ldlt_factor forks
+  // B (trailing updates) and C (rows launches) from it and joins them back
+  // (a fork onto A cost the C2 step ~70 us of host enqueue before the first
+  // panel, profiles/r05_s18)
+  HIP_OK(ldlt_factor(K, ld, N, D, Linv, W, nbo, ctx->nbi, info, ctx->stream, timer, ctx->sB, ctx->sC, ev, nev - 2,
                      pctrl, fourth ? ctx->sD : nullptr));
-  // join (A has already waited for B's tail)
-  IPMZ_TRACE("factor_impl: join");
-  HIP_OK(join_side_streams(ctx, ev + nev, fourth));
-  IPMZ_TRACE("factor_impl: joined");
   HIP_OK(prep());
   return IPMZ_OK;
 }
@@ -442,14 +427,10 @@ static int mixed_factor_impl(ipmz_ctx* ctx, const double* K, int64_t ld, MixedWs
   int rc = ensure_events(ctx, (size_t)nev + 4);
   if (rc) return rc;
   hipEvent_t* ev = ctx->evpool.data();
-  HIP_OK(stream_record(ev[nev - 2], ctx->stream));
-  HIP_OK(stream_wait(ctx->sA, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sB, ev[nev - 2]));
-  HIP_OK(stream_wait(ctx->sC, ev[nev - 2]));
   const bool fourth = !(debug_inject_mask() & IPMZ_DEBUG_NO_FOURTH);
-  if (fourth) HIP_OK(stream_wait(ctx->sD, ev[nev - 2]));
-  HIP_OK(mixed_factor(K, ld, w, ctx->sA, ctx->sB, ctx->sC, ev, nev - 2, timer, fourth ? ctx->sD : nullptr));
-  HIP_OK(join_side_streams(ctx, ev + nev, fourth));
+  // the chain on the caller's stream (factor_impl); ldlt_factor forks and
+  // joins B, C and D
+  HIP_OK(mixed_factor(K, ld, w, ctx->stream, ctx->sB, ctx->sC, ev, nev - 2, timer, fourth ? ctx->sD : nullptr));
   HIP_OK(solve_prep(w.K32, w.ld32, w.N, w.Linv32, w.P32, ctx->stream));
   return IPMZ_OK;
 }

@@ -1,6 +1,6 @@
 set -o pipefail
-O=gpurun_out/${OUTD:-r05_s16}; mkdir -p $O
-T="tests/test_gpu_graph.py -k mixed"
-
-timeout -k 10 300 python -u -m pytest $T -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/t_early.log 2>&1; tail -3 $O/t_early.log
-
+O=gpurun_out/${OUTD:-r05_s19}; mkdir -p $O
+B="--no-cpu-baseline --no-instrumented --no-batched --no-configs"
+for w in c2 c3 c5; do timeout -k 10 200 python bench.py --workload $w $B > $O/bench_${w}.log 2>&1 || exit 1; done
+for f in $O/bench_*; do echo $f; tail -1 $f | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('ms_per_step'))" ; done
+OUT=$O STEPS="tests" bash tools/gpu_round.sh

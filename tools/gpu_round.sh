@@ -51,6 +51,7 @@ for s in ${STEPS:-smoke tests bench prof}; do
     kfactor) step kfactor 300 ipm-zoo_amd/build/kbench 11264 factor 384 256 512 ;;
     trace) step trace 300 rocprofv3 --kernel-trace -d "$OUT/trace" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented ;;
     c2trace) step c2trace 300 rocprofv3 --kernel-trace -d "$OUT/c2trace" -o run --output-format csv -- python bench.py --workload c2 --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented --no-configs ;;
+    c2hip) step c2hip 300 rocprofv3 --hip-trace --kernel-trace -d "$OUT/c2hip" -o run --output-format csv -- python bench.py --workload c2 --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented --no-configs ;;
     counters) step counters 120 rocprofv3 -L ;;
     panel) step panel 400 python -u -m pytest tests/test_gpu_panel_forms.py tests/test_gpu_faults.py tests/test_gpu_determinism.py -v --timeout 240 --timeout-method thread -p no:cacheprovider ;;
     chainclk) step chainclk_${CN:-2560} 120 ipm-zoo_amd/build/kbench_chain ${CN:-2560} chainclk ${CNBO:-512} ;;
