@@ -1111,7 +1111,7 @@ __global__ __launch_bounds__(FT) void k_fused_post(const QPDev* __restrict__ qs,
 // then residuals, f, res, mu): gridDim.x workgroups per QP (blockIdx.y)
 // share the matvec rows and transpose columns; the last to arrive (counter
 // q.done, reset by it) runs the residual pass and the stats.
-__global__ __launch_bounds__(FT) void k_fused_eval(const QPDev* __restrict__ qs) {
+__global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(8))) void k_fused_eval(const QPDev* __restrict__ qs) {
   const QPDev& q = qs[blockIdx.y];
   __shared__ double sh[FT / 64];
   __shared__ unsigned last;

@@ -1,6 +1,5 @@
 set -o pipefail
-O=gpurun_out/${OUTD:-r05_s19}; mkdir -p $O
-B="--no-cpu-baseline --no-instrumented --no-batched --no-configs"
-for w in c2 c3 c5; do timeout -k 10 200 python bench.py --workload $w $B > $O/bench_${w}.log 2>&1 || exit 1; done
-for f in $O/bench_*; do echo $f; tail -1 $f | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d.get('ms_per_step'))" ; done
-OUT=$O STEPS="tests" bash tools/gpu_round.sh
+O=gpurun_out/${OUTD:-r05_s20}; mkdir -p $O
+timeout -k 10 200 python bench.py --workload c4 --no-cpu-baseline > $O/bench_c4.log 2>&1 || exit 1
+tail -1 $O/bench_c4.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); print(d['value'], d['phase_ms_per_step']); s=d.get('batched_shard',{}); print(s.get('value'), s.get('phase_ms_per_step'))"
+OUT=$O STEPS="batchtests" bash tools/gpu_round.sh
