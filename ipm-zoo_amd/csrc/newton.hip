@@ -1155,22 +1155,52 @@ __global__ __launch_bounds__(FT) __attribute__((amdgpu_waves_per_eu(8))) void k_
       if (lane == 0 && r < nr) st_sc1(r < n ? &q.Qx[r] : r < n + m ? &q.Ax[r - n] : &q.Cx[r - n - m], d);
     }
   }
-  // transposes: thread per column, rows in TCHUNK chunks (the grid order)
-  auto col_sum = [&](const double* M, auto yf, int rows, int j) {
-    double tot = 0.0;
-    for (int i0 = 0; i0 < rows; i0 += TCHUNK) {
-      const int i1 = i0 + TCHUNK < rows ? i0 + TCHUNK : rows;
-      double c = 0.0;
-#pragma unroll 8
-      for (int i = i0; i < i1; ++i) c += M[(int64_t)i * q.ldn + j] * yf(i);
-      tot += c;
+  // transposes: one thread per (column j, chunk of FCH rows), the chunk
+  // summed in row order (its loads all in flight), the chunk partials then
+  // added in chunk order through LDS; passes of FT / nch columns spread over
+  // the QP's workgroups (a thread per column walking all the rows was
+  // ~16 us of dependent load batches at C4)
+  constexpr int FCH = 8;
+  __shared__ double tp[FT];
+  auto transpose = [&](const double* M, auto yf, int rows, double* out) {
+    const int nch = (rows + FCH - 1) / FCH;
+    if (nch > FT) {  // (not at the fused path's sizes) thread per column
+      for (int j = blockIdx.x * FT + tid; j < n; j += gridDim.x * FT) {
+        double tot = 0.0;
+        for (int i0 = 0; i0 < rows; i0 += FCH) {
+          const int i1 = i0 + FCH < rows ? i0 + FCH : rows;
+          double c = 0.0;
+          for (int i = i0; i < i1; ++i) c += M[(int64_t)i * q.ldn + j] * yf(i);
+          tot += c;
+        }
+        st_sc1(&out[j], tot);
+      }
+      return;
     }
-    return tot;
+    const int cpp = FT / nch;  // columns per pass
+    const int jj = tid % cpp, h = tid / cpp;
+    const int npass = (n + cpp - 1) / cpp;
+    for (int pi = blockIdx.x; pi < npass; pi += gridDim.x) {  // (uniform per workgroup)
+      const int j = pi * cpp + jj;
+      double c = 0.0;
+      if (h < nch && j < n) {
+        const int i0 = h * FCH, i1 = i0 + FCH < rows ? i0 + FCH : rows;
+#pragma unroll
+        for (int i = i0; i < i0 + FCH; ++i)
+          if (i < i1) c += M[(int64_t)i * q.ldn + j] * yf(i);
+      }
+      __syncthreads();  // the previous pass's reads of tp
+      tp[tid] = c;
+      __syncthreads();
+      if (tid < cpp && j < n) {
+        double tot = 0.0;
+        for (int k = 0; k < nch; ++k) tot += tp[k * cpp + tid];
+        st_sc1(&out[j], tot);
+      }
+    }
   };
-  for (int j = blockIdx.x * FT + tid; j < n; j += gridDim.x * FT) {
-    if (m) st_sc1(&q.ATl[j], col_sum(q.A, [&](int i) { return a_dual(q, i); }, m, j));
-    if (p) st_sc1(&q.CTl[j], col_sum(q.C, [&](int i) { return q.v[LC][i]; }, p, j));
-  }
+  if (m) transpose(q.A, [&](int i) { return a_dual(q, i); }, m, q.ATl);
+  if (p) transpose(q.C, [&](int i) { return q.v[LC][i]; }, p, q.CTl);
   // arrival (sync.h protocol: write-through data, vmcnt drained, barrier, one
   // agent-scope atomic); no cache-wide fences
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
