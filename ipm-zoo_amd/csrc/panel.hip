@@ -1116,6 +1116,38 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
   if (r == 0) HSTAMP(k0 / 64, 2);
 }
 
+// A chain launch started beside the previous panel's rows launch (a.parea):
+// the rows of this panel's region from that launch (RDONE of every region
+// block row) within 1 ms, else no role is drawn -- the launch may have been
+// dispatched ahead of that rows launch (a serialized dispatch, rocprofv3
+// --pmc), and the rows launch of this panel, queued behind it, then takes
+// every chain role.  true: draw.
+template <typename T>
+__device__ __forceinline__ bool prev_rows_ready(const PanelArgs<T>& a) {
+  if (!a.parea) return true;
+  __shared__ unsigned sh_rr;
+  if (threadIdx.x == 0) {
+    const int nb = panel_nb(a);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    unsigned ok = 0;
+    for (int r = 0;;) {
+      if (r == nb) {
+        ok = 1;
+        break;
+      }
+      if (__hip_atomic_load(&a.parea[OP_RDONE + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        ++r;
+        continue;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull) break;  // 1 ms
+      __builtin_amdgcn_s_sleep(2);
+    }
+    sh_rr = ok;
+  }
+  __syncthreads();
+  return sh_rr != 0;
+}
+
 // draw a role.  form 4 (the 256-thread kernel): the CHAIN (chain4) if it is
 // still unclaimed, else the next chain ticket while any is left, else -- rows
 // launch -- a rows ticket.  form 8 (the chain8 kernel): the chain only.
@@ -1173,6 +1205,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64];
   __shared__ unsigned sh_ok;
   int form = 0;
+  if (!rows_launch && !prev_rows_ready(a)) return;
   const unsigned tu = draw_ticket(a, 4, rows_launch != 0, &form);
   if (tu == ~0u) return;
   const int t = (int)tu;
@@ -1199,6 +1232,7 @@ __global__ __launch_bounds__(512) void panel_chain8_kernel(PanelArgs<double> a, 
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64 * DS + 64];
   __shared__ unsigned sh_abort;
   int form = 0;
+  if (!prev_rows_ready(a)) return;
   const unsigned tu = draw_ticket(a, take ? 8 : 0, false, &form);
   if (tu != 0u) return;
   HSTAMP(a.k0 / 64 + 1, 3);
