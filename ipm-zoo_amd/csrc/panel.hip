@@ -1240,6 +1240,9 @@ __global__ __launch_bounds__(512) void panel_chain8_kernel(PanelArgs<double> a, 
   chain8<double>(a, smem, &sh_abort);
 }
 
+#ifndef IPMZ_CHAIN_LDS_KB
+#define IPMZ_CHAIN_LDS_KB 95
+#endif
 // ---------------------------------------------------------------------------
 // dynamic LDS of the chain launch on top of panel_kernel's static 66.5 KB:
 // 95 KB in all, more than a CU has left beside another panel workgroup
@@ -1247,7 +1250,7 @@ __global__ __launch_bounds__(512) void panel_chain8_kernel(PanelArgs<double> a, 
 // fits beside it
 template <typename T>
 static size_t chain_lds_pad() {
-  constexpr size_t total = 95 * 1024, own = (2 * 64 * DS + 64 + 64) * sizeof(double) + 64;
+  constexpr size_t total = IPMZ_CHAIN_LDS_KB * 1024, own = (2 * 64 * DS + 64 + 64) * sizeof(double) + 64;
   static const bool set = [] {
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel<T>),
                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)(total - own)) == hipSuccess;
