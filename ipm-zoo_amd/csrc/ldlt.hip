@@ -518,7 +518,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // behind it would only end at the spin limit.
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
   if (two && fused && hipStreamIsCapturing(st, &cap) != hipSuccess) cap = hipStreamCaptureStatusActive;
-  const bool early = two && fused && N <= IPMZ_EARLY_CHAIN_MAX_N && cap == hipStreamCaptureStatusNone;
+  const bool early_ok = two && fused && cap == hipStreamCaptureStatusNone;
+  // per panel j: its chain launch starts early once the order left from
+  // its start is small enough (the chain-bound periods; C2 from its first
+  // panel, C3 / C5 their last ones)
+  auto early_at = [&](int j) { return early_ok && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
   T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
@@ -529,7 +533,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo,
                         (two && prev) ? slot00(k) : nullptr, two ? slot00(k + 1) : nullptr, info, area(k), err,
                         prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC,
-                        (early && prev) ? area(k - 1) : nullptr);
+                        (early_at(k) && prev) ? area(k - 1) : nullptr);
   };
   hipError_t e = hipSuccess;
   if (!two) {  // single stream: factor, then the whole trailing update
@@ -566,7 +570,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   if (fused) {
     if ((e = stream_record(evA[0], st)) != hipSuccess) return e;
     if ((e = stream_record(evC[0], sC)) != hipSuccess) return e;
-    if (!early && (e = stream_wait(st, evC[0])) != hipSuccess) return e;
+    if (!early_at(1) && (e = stream_wait(st, evC[0])) != hipSuccess) return e;
   }
   for (int k = 0; k < npan; ++k) {
     const int k0 = k * nbo, bo = pw(k);
@@ -581,11 +585,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     // touched those columns; B goes straight on with the rest)
     // (early: panel k's rows launch on C as well -- A no longer waits for it)
     if ((e = stream_wait(st2, evP[k])) != hipSuccess) return e;
-    if (early && (e = stream_wait(st2, evC[k])) != hipSuccess) return e;
+    if (early_at(k + 1) && (e = stream_wait(st2, evC[k])) != hipSuccess) return e;
     hipStream_t sN = four ? st4 : st2;  // the stream of the P_{k+2} strip and N_k
     if (four) {
       if ((e = stream_wait(st4, evP[k])) != hipSuccess) return e;
-      if (early && (e = stream_wait(st4, evC[k])) != hipSuccess) return e;
+      if (early_at(k + 1) && (e = stream_wait(st4, evC[k])) != hipSuccess) return e;
       if (k >= 1 && (e = stream_wait(st4, evT[k - 1])) != hipSuccess) return e;
     }
     if (p2 < N) {
@@ -607,7 +611,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
       // early: panel k-1's rows launch (and C's strip before it) are the last
       // readers of W buffer (k + 1) % 3 -- the one this chain launch writes
-      if (early && (e = stream_wait(st, evC[k - 1])) != hipSuccess) return e;
+      if (early_at(k + 1) && (e = stream_wait(st, evC[k - 1])) != hipSuccess) return e;
     }
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
@@ -623,13 +627,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if ((e = factor(k + 1, true)) != hipSuccess) return e;
       if ((e = stream_record(evA[k + 1], st)) != hipSuccess) return e;
       if ((e = stream_record(evC[k + 1], sC)) != hipSuccess) return e;
-      if (!early && (e = stream_wait(st, evC[k + 1])) != hipSuccess) return e;
+      if (!early_at(k + 2) && (e = stream_wait(st, evC[k + 1])) != hipSuccess) return e;
     } else {
       if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p1, p2, false, st)) != hipSuccess) return e;
       if ((e = factor(k + 1, false)) != hipSuccess) return e;
     }
   }
-  if (early && (e = stream_wait(st, evC[npan - 1])) != hipSuccess) return e;  // the last rows launch
+  if (early_ok && (e = stream_wait(st, evC[npan - 1])) != hipSuccess) return e;  // the last rows launch
   if ((e = stream_record(evJoin, st2)) != hipSuccess) return e;
   if (four) {
     if ((e = stream_record(evJoin4, st4)) != hipSuccess) return e;

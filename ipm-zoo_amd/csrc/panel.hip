@@ -1244,8 +1244,9 @@ __global__ __launch_bounds__(512) void panel_chain8_kernel(PanelArgs<double> a, 
 // dynamic LDS of the chain launch on top of panel_kernel's static 66.5 KB.
 // 95 KB in all: more than a CU has left beside another panel workgroup
 // (66.5 KB), so no two share a CU, while one trailing-GEMM workgroup (48 KB)
-// still fits beside it.  113 KB for small orders (N <= IPMZ_EARLY_CHAIN_MAX_N,
-// where the chain is the critical path): no GEMM workgroup beside it either
+// still fits beside it.  113 KB where the order left from the panel is small
+// (<= IPMZ_EARLY_CHAIN_MAX_N: the chain is the critical path): no GEMM
+// workgroup beside it either
 // (kbench N = 2560: 1.15 -> 1.10 ms; at N = 11264, where the trailing GEMM
 // is, 10.97 -> 11.2 ms, so not there; profiles/r05_s/chain_lds_pad_ab.txt)
 template <typename T>
@@ -1301,7 +1302,7 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
     // every chain role; the padding (dynamic LDS) makes each of its
     // workgroups hold a CU with no other panel workgroup (the chain's
     // barrier-bound blocks lose a third of their speed beside a helper)
-    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N), st_chain, a, 0,
+    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N - k0), st_chain, a, 0,
                        rows_prev ? 1 : 0);
   }
   hipError_t e = hipGetLastError();
