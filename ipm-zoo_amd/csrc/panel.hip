@@ -140,6 +140,22 @@ __device__ __forceinline__ void mma_tile(const TMap<NW>& m, const T* As, BF bf, 
   }
 }
 
+// One column block n of mma_tile: the same MFMAs into acc in the same order
+// (so a tile computed this way is bitwise mma_tile's)
+template <typename T, bool NEG, int NW, typename BF>
+__device__ __forceinline__ void mma_nblk(const TMap<NW>& m, const T* As, BF bf, Acc<T>& acc, int n,
+                                         const T* ascale) {
+  typedef Mfma<T> MF;
+  const int arow = 16 * m.wr + (m.lane & 15);
+#pragma unroll 4
+  for (int s = 0; s < 16; ++s) {
+    const int k = 4 * s + (m.lane >> 4);
+    const T av = ascale ? As[arow * DS + k] * ascale[k] : As[arow * DS + k];
+    const T a = NEG ? -av : av;
+    acc = MF::mma(a, bf(16 * n + (m.lane & 15), k), acc);
+  }
+}
+
 // acc[i] += A[16 wr.., :] B[16 n.., :]^T for a LOWER-triangular B (the
 // diagonal block's inverse): k-chunks past column block n's diagonal are zero
 // and skipped (40 of 64 MFMAs per 4-wave tile), the diagonal chunk masked
@@ -426,12 +442,41 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
           own[n][g] = ld_sc1(&src[(int64_t)(row < rows ? row : 0) * ld + 16 * n + (lane & 15)]);
         }
     };
+    // block j >= 1: the own update of its block with W(j, j-1) (in X) beyond
+    // column block 0 -- tiles (w, n), 1 <= n <= w, of wave w's rows -- runs
+    // on waves 1..3 while wave 0 factors column block 0 (diag64_body's IDLE0:
+    // that pass reads column block 0 only; X is first written after its
+    // barrier); every wave drains its L / W stores before that barrier
+    // (DRAIN0) and REG[j-1][j] is raised after it (POST2)
+    auto idle0 = [&]() __attribute__((always_inline)) {
+      const T* Wx = reinterpret_cast<const T*>(X);
+      static_for<3>([&](auto nc) {
+        constexpr int n = decltype(nc)::value + 1;
+        if (n <= m.wr) {  // (wave-uniform)
+          Acc<T> t;
+#pragma unroll
+          for (int g = 0; g < 4; ++g) t[g] = (T)M[(16 * m.wr + MF::row(lane, g)) * DS + 16 * n + (lane & 15)];
+          mma_nblk<T, true, 4>(m, Wx, [&](int r, int k) { return Wx[r * DS + k]; }, t, n, rdv);
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int row = 16 * m.wr + MF::row(lane, g), col = 16 * n + (lane & 15);
+            M[row * DS + col] = (row < bj && col <= row) ? (double)t[g] : (row == col ? 1.0 : 0.0);
+          }
+        }
+      });
+    };
+    auto post2 = [&]() __attribute__((always_inline)) {
+      if (threadIdx.x == 0) st_sc1(&area[OP_REG + (j - 1) * OP_NBMAX + j], 1u);
+    };
     if (j == 0 && !a.Wprev)
       diag64_body<true, false, T, false, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
                                                               pre_wb, nullptr, tid);
-    else
+    else if (j == 0)
       diag64_body<true, false, T, true, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
                                                              pre_wb, nullptr, tid);
+    else
+      diag64_body<true, false, T, true, 4, decltype(pre_wb), true, decltype(idle0), 1, true, true, decltype(post2)>(
+          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
     CSTAMP(j0 / 64, 2);
     if (!more) {
       if (!(a.inject && j == 0)) publish(&area[OP_DIAG + j]);
@@ -470,17 +515,16 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
       for (int g = 0; g < 4; ++g) lacc[n][g] = acc[n][g] * rd[n];
     store_acc<T, false, false, 4>(m, lacc, Lrow, ld, rows, 64);
     store_acc<T, true, false, 4>(m, acc, Wrow, ldw, rows, 64);
-    // own update (c, c) -= L(c, j) W(c, j)^T: W into M, L = W / d read from it
-    T* Wm = reinterpret_cast<T*>(M);
-    put_acc<T, 4>(m, Wm, acc);
+    // own update (c, c) -= L(c, j) W(c, j)^T, column block 0 here (what
+    // diag(c)'s first column pass reads), the rest in diag(c)'s IDLE0: W into
+    // X (free: the TRSM's reads of X_jj are done), L = W / d read from it
+    T* Wx = reinterpret_cast<T*>(X);
+    put_acc<T, 4>(m, Wx, acc);
     __syncthreads();
-    mma_tile<T, true, 4>(m, Wm, [&](int r, int k) { return Wm[r * DS + k]; }, own, rdv);
-    // W(c, j) for the helpers' and the rows roles' strips: published after
-    // the update, so the stores drain beside its MFMAs (publish's barrier
-    // also ends every wave's reads of M)
-    publish(&area[OP_REG + j * OP_NBMAX + c]);
+    mma_nblk<T, true, 4>(m, Wx, [&](int r, int k) { return Wx[r * DS + k]; }, own[0], 0, rdv);
     CSTAMP(j0 / 64, 5);
-    // the next diagonal block, straight into diag64_body's image
+    // the next diagonal block, straight into diag64_body's image (column
+    // blocks >= 1 not yet updated: IDLE0 above, in the next iteration)
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
       const int col = 16 * n + (lane & 15);
