@@ -142,11 +142,12 @@ __device__ __forceinline__ void mma_tile(const TMap<NW>& m, const T* As, BF bf, 
 
 // One column block n of mma_tile: the same MFMAs into acc in the same order
 // (so a tile computed this way is bitwise mma_tile's)
+// (row block wr: the caller's, default the wave's)
 template <typename T, bool NEG, int NW, typename BF>
 __device__ __forceinline__ void mma_nblk(const TMap<NW>& m, const T* As, BF bf, Acc<T>& acc, int n,
-                                         const T* ascale) {
+                                         const T* ascale, int wr = -1) {
   typedef Mfma<T> MF;
-  const int arow = 16 * m.wr + (m.lane & 15);
+  const int arow = 16 * (wr < 0 ? m.wr : wr) + (m.lane & 15);
 #pragma unroll 4
   for (int s = 0; s < 16; ++s) {
     const int k = 4 * s + (m.lane >> 4);
@@ -450,18 +451,19 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
     // (DRAIN0) and REG[j-1][j] is raised after it (POST2)
     auto idle0 = [&]() __attribute__((always_inline)) {
       const T* Wx = reinterpret_cast<const T*>(X);
-      static_for<3>([&](auto nc) {
-        constexpr int n = decltype(nc)::value + 1;
-        if (n <= m.wr) {  // (wave-uniform)
-          Acc<T> t;
+      // two tiles per wave: wave 1 (1,1) (3,3), wave 2 (2,1) (2,2), wave 3 (3,1) (3,2)
+      static_for<2>([&](auto hc) {
+        constexpr int h = decltype(hc)::value;
+        const int i = m.wr == 1 ? (h ? 3 : 1) : m.wr;                       // (wave-uniform)
+        const int n = m.wr == 1 ? (h ? 3 : 1) : (m.wr == 2 ? 1 + h : 1 + h);
+        Acc<T> t;
 #pragma unroll
-          for (int g = 0; g < 4; ++g) t[g] = (T)M[(16 * m.wr + MF::row(lane, g)) * DS + 16 * n + (lane & 15)];
-          mma_nblk<T, true, 4>(m, Wx, [&](int r, int k) { return Wx[r * DS + k]; }, t, n, rdv);
+        for (int g = 0; g < 4; ++g) t[g] = (T)M[(16 * i + MF::row(lane, g)) * DS + 16 * n + (lane & 15)];
+        mma_nblk<T, true, 4>(m, Wx, [&](int r, int k) { return Wx[r * DS + k]; }, t, n, rdv, i);
 #pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int row = 16 * m.wr + MF::row(lane, g), col = 16 * n + (lane & 15);
-            M[row * DS + col] = (row < bj && col <= row) ? (double)t[g] : (row == col ? 1.0 : 0.0);
-          }
+        for (int g = 0; g < 4; ++g) {
+          const int row = 16 * i + MF::row(lane, g), col = 16 * n + (lane & 15);
+          M[row * DS + col] = (row < bj && col <= row) ? (double)t[g] : (row == col ? 1.0 : 0.0);
         }
       });
     };
