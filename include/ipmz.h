@@ -112,7 +112,8 @@ const char* ipmz_last_error(void);
  * 0 (default) for normal operation. */
 int ipmz_debug_inject(int mask);
 /* Blocking of the factorization: outer panel nbo (multiple of nbi, <= 512;
- * 0 = by matrix order: 512 for N >= 2048 with nbi 64, else 256), inner
+ * 0 = by matrix order: with nbi 64, 512 for N > 4096, 384 for 2048 <= N <= 4096,
+ * else 256), inner
  * diagonal block nbi (64 or 128).  Defaults 0 / 64.  Workspace sizes depend
  * on it: query them after setting the blocking. */
 int ipmz_ctx_set_blocking(ipmz_ctx* ctx, int nbo, int nbi);

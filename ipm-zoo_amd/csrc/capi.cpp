@@ -63,13 +63,15 @@ struct ipmz_ctx {
 };
 
 // outer panel width for an order-N factor: the context's, or by size --
-// 512 for N >= 2048 (kbench factor, N = 11264: 12.95 ms at 384, 12.34 at
-// 512; N = 16384: 32.1 -> 31.2 ms; N = 2560, C2's pipelined normal
-// equations: 1.46 ms at 256, 1.30 at 512), 256 below.  Every workspace
+// 512 for N > 4096 (kbench factor, N = 11264: 12.95 ms at 384, 12.34 at
+// 512; N = 16384: 32.1 -> 31.2 ms), 384 for 2048 <= N <= 4096 (C2, N = 2560,
+// chain-bound: 679-689 steps/s at 512, 711-718 at 384 in round 5,
+// profiles/r05_s/c2_nbo_ab.txt; 256: 675), 256 below.  Every workspace
 // layout and every factor / solve of an order-N matrix uses this same value.
 static int nbo_for(const ipmz_ctx* ctx, int N) {
   if (ctx->nbo > 0) return ctx->nbo;
-  return N >= 2048 && ctx->nbi == 64 ? 512 : 256;
+  if (ctx->nbi != 64 || N < 2048) return 256;
+  return N <= 4096 ? 384 : 512;
 }
 
 static int ensure_events(ipmz_ctx* ctx, size_t n) {
