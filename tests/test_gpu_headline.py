@@ -134,7 +134,7 @@ def test_c5_mixed_bench_setting_vs_oracle(ctx):
 def test_c2_normal_newton_steps_vs_oracle(ctx):
     """C2 (BASELINE.json configs[1]): n=2048, m=512, the normal-equations
     reduction (Cholesky of H, TRSM, SYRK, Cholesky of S as one pipelined
-    factor, 512-wide outer panels at this size) against the oracle's
+    factor, 384-wide outer panels at this size) against the oracle's
     augmented reference-order LDL^T from the same iterate -- the Newton
     directions are the same system's solution (Optimizer.cpp:137-217,
     SymbolicOptimization.cpp:465-478), at iterate 0 and after 4 steps."""
@@ -144,7 +144,7 @@ def test_c2_normal_newton_steps_vs_oracle(ctx):
     g = I.Optimizer(n, m, p, ctx)
     g.generate(seed)
     g.set_reduction(I.REDUCTION_NORMAL)
-    assert ctx.blocking(n + m)[0] == 512  # the blocking bench.py's C2 line runs
+    assert ctx.blocking(n + m)[0] == 384  # the blocking bench.py's C2 line runs
     assert np.array_equal(g.vars(), o.vars())
     for label, warm in (("C2 iterate 0", 0), ("C2 iterate 4", 4)):
         for _ in range(warm):
