@@ -39,7 +39,7 @@ def _pair(ctx, n, m, p, mode):
 @pytest.mark.parametrize("n,m,p,mode,torch_stream", [
     (1024, 256, 128, "augmented", False),   # N = 1408: 6 outer panels of 256
     (1024, 256, 128, "augmented", True),    # on torch's (legacy default) stream: captured on the context's own
-    (2048, 512, 0, "normal", False),        # C2's shape: the pipelined normal-equations factor, 5 panels of 512
+    (2048, 512, 0, "normal", False),        # C2's shape: the pipelined normal-equations factor, 7 panels of 384
     (1536, 0, 0, "mixed", False),           # fp32 factor + fp64 refinement, 6 panels
     (5120, 0, 0, "mixed", False),           # 10 panels of 512: the 128 x 128 f32 trailing tiles too
 ])

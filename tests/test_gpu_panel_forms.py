@@ -52,7 +52,8 @@ def _with_mask(mask, fn):
 @pytest.mark.parametrize("N", [200, 1408, 2560, 4100])
 def test_fp64_chain_forms_bitwise(ctx, N):
     """N = 200: one outer panel with a ragged last block; 1408: 256-wide
-    panels; 2560 (C2's order), 4100: 512-wide panels, ragged last panel."""
+    panels; 2560 (C2's order): 384-wide panels, ragged last panel; 4100:
+    512-wide panels, ragged last panel."""
     K = _qd(N, 7 * N)
     wsb = ctx.workspace_bytes(N)
     ws = torch.zeros(wsb // 8 + 1, dtype=torch.float64, device="cuda")
