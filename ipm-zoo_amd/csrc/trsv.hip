@@ -360,7 +360,9 @@ __global__ __launch_bounds__(64 * NW) void trsv_small_kernel(const double* __res
     double lv[RW], acc[RW];
 #pragma unroll
     for (int k = 0; k < RW; ++k) {
-      lv[k] = Lb[(wave * RW + k) * 64 + lane];
+      // (the strict upper triangle of Linv_J is zero: not loaded, 62.5 % of
+      // the block's 128-byte lines fetched)
+      lv[k] = lane <= wave * RW + k ? Lb[(wave * RW + k) * 64 + lane] : 0.0;
       acc[k] = 0.0;
     }
     // (W16) 128-column chunks as 16-byte loads (lane: columns c0 + 2 lane,
@@ -413,7 +415,7 @@ __global__ __launch_bounds__(64 * NW) void trsv_small_kernel(const double* __res
     const double* Lb = Linv + (int64_t)J * 64 * 64;
     double lv[RW];
 #pragma unroll
-    for (int k = 0; k < RW; ++k) lv[k] = Lb[(wave * RW + k) * 64 + lane];
+    for (int k = 0; k < RW; ++k) lv[k] = lane <= wave * RW + k ? Lb[(wave * RW + k) * 64 + lane] : 0.0;
     // two rows per load instruction: half-wave h takes rows i = J0 + 64 +
     // 2 wave + h (+ 2 NW), lane l & 31 columns 2 (l & 31), + 1 (16 bytes)
     const int h = lane >> 5, c2 = 2 * (lane & 31);
