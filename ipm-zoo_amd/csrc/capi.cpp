@@ -910,6 +910,12 @@ int factor_batch(ipmz_qp* s, TrailTimer* tt, bool info_reset) {
 // batches of small systems: the O(N) / O(n^2) phases as three per-QP
 // workgroup kernels (newton.hip k_fused_*)
 bool fused_phases(const ipmz_qp* s) { return s->B > 1 && s->N <= IPMZ_FUSED_NMAX; }
+// ... whose solves are the small batched solve (solve_batch's last branch,
+// nbi 64): then both solves and the phases between them run as one launch
+bool fused_solves(const ipmz_qp* s) {
+  return fused_phases(s) && !s->eqnone && !s->normal && !s->mixed && s->ctx->nbi == 64 && fused_solves_ok(s->N, s->ldk) &&
+         !(debug_inject_mask() & IPMZ_DEBUG_NO_FUSED_SOLVES);
+}
 // the fused step keeps the assembled matrix in K0 when the small batched
 // factor (nbi 64) consumes it; otherwise the whole matrix is assembled into K
 bool uses_k0(const ipmz_qp* s) {
@@ -939,13 +945,23 @@ int run_step(ipmz_qp* s, int flags) {
     mark(1);
     if ((rc = factor_batch(s, nullptr, true))) return rc;
     mark(2);
-    if ((rc = solve_batch(s, st, 0))) return rc;
-    mark(3);
-    HIP_OK(qp_fused_mid(qb, st));
-    mark(4);
-    if ((rc = solve_batch(s, st, 1))) return rc;
-    mark(5);
-    HIP_OK(qp_fused_post(qb, freeze, st));
+    if (fused_solves(s)) {
+      // both solves and the phases between them in one launch (the solve
+      // phase then holds mid and post too; eval = the evaluation alone)
+      HIP_OK(qp_fused_solves(qb, s->K, s->ldk, s->N, s->D, s->bLinv, q0(s).b, s->sK, s->sD, s->sL, s->sb, freeze, st));
+      mark(3);
+      mark(4);
+      mark(5);
+      HIP_OK(qp_fused_eval(qb, st));
+    } else {
+      if ((rc = solve_batch(s, st, 0))) return rc;
+      mark(3);
+      HIP_OK(qp_fused_mid(qb, st));
+      mark(4);
+      if ((rc = solve_batch(s, st, 1))) return rc;
+      mark(5);
+      HIP_OK(qp_fused_post(qb, freeze, st));
+    }
     mark(6);
     mark(7);
   } else {

@@ -34,12 +34,13 @@ namespace ipmz {
 // 2048 = the panel's chain launch runs the 512-thread kernel with the 8-wave chain roles (chain8, A/B),
 // 4096 = the chain launch draws no ticket: the rows launch runs every chain role in its 4-wave form
 //        (what a serialized dispatch order can produce; the forms must factor bitwise alike),
-// 8192 = batches assemble the whole KKT into K every step (not the kept K0) (A/B)
+// 8192 = batches assemble the whole KKT into K every step (not the kept K0) (A/B),
+// 16384 = batches run the two solves and the phases between them as separate launches (A/B)
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
        IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_CHAIN8 = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
-       IPMZ_DEBUG_NO_K0 = 8192 };
+       IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -342,5 +343,12 @@ enum { KMODE_K = 0, KMODE_K0_DIAG = 1, KMODE_K0_OFFDIAG = 2 };
 hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t st, int kmode = KMODE_K);
 hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st);
 hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st);  // (+ the evaluation)
+// predictor solve + mid + corrector solve + post in one workgroup per QP
+// (the small batched solve, ldlt_solve_batched's nbi = 64 path: N <=
+// TRSV_SMALL_NMAX, even ld), then the evaluation alone
+inline bool fused_solves_ok(int N, int64_t ld) { return N <= 4096 && !(ld & 1); }
+hipError_t qp_fused_solves(const QPBatch& qb, const double* K, int64_t ld, int N, const double* D, const double* Linv,
+                           double* b, int64_t sK, int64_t sD, int64_t sL, int64_t sb, int freeze, hipStream_t st);
+hipError_t qp_fused_eval(const QPBatch& qb, hipStream_t st);
 
 }  // namespace ipmz

@@ -17,6 +17,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "sync.h"
+#include "trsv_small.h"
 
 namespace ipmz {
 
@@ -1055,21 +1056,21 @@ __global__ __launch_bounds__(FT) void k_fused_pre(const QPDev* __restrict__ qs, 
 
 // predictor back-substitution, alpha_aff, mu_aff / sigma, corrector rows,
 // corrector rhs
-__global__ __launch_bounds__(FT) void k_fused_mid(const QPDev* __restrict__ qs) {
-  const QPDev& q = qs[blockIdx.x];
-  __shared__ double sh[FT / 64];
+// (T threads per QP; sh: T / 64 doubles of LDS)
+template <int T>
+__device__ __forceinline__ void fused_mid_body(const QPDev& q, double* sh) {
   const int tid = threadIdx.x;
   const int N = q.N, nm = q.n + q.m;
   const DSel D = dsel(q, 0);
-  for (int t = tid; t < N; t += FT) backsub_elem(q, D, t);
+  for (int t = tid; t < N; t += T) backsub_elem(q, D, t);
   __syncthreads();
   double a = 1.0;
-  for (int t = tid; t < nm; t += FT) ratio_elem(q, D, t, a);
-  a = block_allmin<FT>(a, sh);
+  for (int t = tid; t < nm; t += T) ratio_elem(q, D, t, a);
+  a = block_allmin<T>(a, sh);
   if (tid == 0) q.scal[SC_ALPHA_AFF] = a;
   double s = 0.0;
-  for (int t = tid; t < nm; t += FT) mu_aff_elem(q, t, a, s);
-  s = block_allsum<FT>(s, sh);
+  for (int t = tid; t < nm; t += T) mu_aff_elem(q, t, a, s);
+  s = block_allsum<T>(s, sh);
   // every thread evaluates the same scalars; thread 0 stores them
   const int cnt = comp_count(q);
   const double mu_aff = cnt == 0 ? 0.0 : s / (double)cnt;
@@ -1077,34 +1078,75 @@ __global__ __launch_bounds__(FT) void k_fused_mid(const QPDev* __restrict__ qs) 
   const double sigma = mu > 0.0 ? pow(mu_aff / mu, 3.0) : 0.0;
   const double mu_new = mu * sigma;
   const int rows = nm + (q.eqpen ? q.p : 0);
-  for (int t = tid; t < rows; t += FT) corrector_elem(q, t, mu_new);
+  for (int t = tid; t < rows; t += T) corrector_elem(q, t, mu_new);
   __syncthreads();  // SC_MU read by every thread; corrector rows written
   if (tid == 0) {
     q.scal[SC_MU_AFF] = mu_aff;
     q.scal[SC_SIGMA] = sigma;
     q.scal[SC_MU_NEW] = mu_new;
   }
-  for (int t = tid; t < N; t += FT) rhs_elem(q, t);
+  for (int t = tid; t < N; t += T) rhs_elem(q, t);
+}
+__global__ __launch_bounds__(FT) void k_fused_mid(const QPDev* __restrict__ qs) {
+  __shared__ double sh[FT / 64];
+  fused_mid_body<FT>(qs[blockIdx.x], sh);
 }
 
 // corrector back-substitution, alpha, the update (one workgroup per QP)
-__global__ __launch_bounds__(FT) void k_fused_post(const QPDev* __restrict__ qs, int freeze) {
-  const QPDev& q = qs[blockIdx.x];
-  __shared__ double sh[FT / 64];
+template <int T>
+__device__ __forceinline__ void fused_post_body(const QPDev& q, int freeze, double* sh) {
   const int tid = threadIdx.x;
   const int n = q.n, m = q.m, p = q.p, N = q.N;
   const DSel D = dsel(q, 1);
   const bool frozen = freeze && q.scal[SC_CONVERGED] != 0.0;
-  for (int t = tid; t < N; t += FT) backsub_elem(q, D, t);
+  for (int t = tid; t < N; t += T) backsub_elem(q, D, t);
   __syncthreads();
   double a = 1.0;
-  for (int t = tid; t < n + m; t += FT) ratio_elem(q, D, t, a);
-  a = block_allmin<FT>(a, sh);
+  for (int t = tid; t < n + m; t += T) ratio_elem(q, D, t, a);
+  a = block_allmin<T>(a, sh);
   if (tid == 0) q.scal[SC_ALPHA] = a;
   if (!frozen) {
     const int mx = max(n, max(m, p));
-    for (int t = tid; t < mx; t += FT) update_elem(q, t, 0.995 * a);
+    for (int t = tid; t < mx; t += T) update_elem(q, t, 0.995 * a);
   }
+}
+__global__ __launch_bounds__(FT) void k_fused_post(const QPDev* __restrict__ qs, int freeze) {
+  __shared__ double sh[FT / 64];
+  fused_post_body<FT>(qs[blockIdx.x], freeze, sh);
+}
+
+// The four per-QP phases between the factor and the evaluation in ONE
+// workgroup per QP: predictor solve, the middle phase (k_fused_mid), corrector
+// solve, the corrector back-substitution and update (k_fused_post) -- no
+// dependency crosses QPs, so a QP moves on when its own phase is done instead
+// of waiting for the whole batch at three kernel boundaries.  Each phase is
+// the kernel's code (trsv_small.h, the bodies above) with a workgroup
+// barrier in between (its global stores visible to the next phase's loads:
+// every wave of the workgroup shares the CU's L1).  NW = 8: the same values
+// as the separate launches, bitwise; NW = 16: the middle / post reductions
+// over 16 wave partials.  (NW = 8: at most 128 VGPRs, two workgroups per CU
+// like trsv_small_kernel<8>.)
+template <int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1))) void k_fused_solves(const QPDev* __restrict__ qs, const double* __restrict__ K,
+                                                          int64_t ld, int N, const double* __restrict__ D,
+                                                          const double* __restrict__ Linv, double* __restrict__ b,
+                                                          int64_t sK, int64_t sD, int64_t sL, int64_t sb,
+                                                          int freeze) {
+  extern __shared__ __attribute__((aligned(16))) double sm[];
+  __shared__ double sh[NW];
+  const int64_t i = blockIdx.x;
+  const QPDev& q = qs[i];
+  K += i * sK;
+  D += i * sD;
+  Linv += i * sL;
+  b += i * sb;
+  trsv_small_body<NW>(K, ld, N, D, Linv, b, sm);
+  __syncthreads();
+  fused_mid_body<64 * NW>(q, sh);
+  __syncthreads();
+  trsv_small_body<NW>(K, ld, N, D, Linv, b, sm);
+  __syncthreads();
+  fused_post_body<64 * NW>(q, freeze, sh);
 }
 
 // Evaluation of the new iterate (Qx, Ax, Cx, A^T lambda_A, C^T lambda_C,
@@ -1244,6 +1286,22 @@ hipError_t qp_fused_pre(const QPBatch& qb, int restart, int* info, hipStream_t s
 }
 hipError_t qp_fused_mid(const QPBatch& qb, hipStream_t st) {
   hipLaunchKernelGGL(k_fused_mid, dim3(qb.B), dim3(FT), 0, st, qb.d);
+  return hipGetLastError();
+}
+hipError_t qp_fused_solves(const QPBatch& qb, const double* K, int64_t ld, int N, const double* D, const double* Linv,
+                           double* b, int64_t sK, int64_t sD, int64_t sL, int64_t sb, int freeze, hipStream_t st) {
+  if (!fused_solves_ok(N, ld)) return hipErrorInvalidValue;
+  // 16 waves when the batch leaves a CU per QP, 8 when QPs share CUs (trsv.hip)
+  if (qb.B <= device_cus())
+    hipLaunchKernelGGL(k_fused_solves<16>, dim3(qb.B), dim3(64 * 16), trsv_small_lds(N, 16), st, qb.d, K, ld, N, D,
+                       Linv, b, sK, sD, sL, sb, freeze);
+  else
+    hipLaunchKernelGGL(k_fused_solves<8>, dim3(qb.B), dim3(64 * 8), trsv_small_lds(N, 8), st, qb.d, K, ld, N, D, Linv,
+                       b, sK, sD, sL, sb, freeze);
+  return hipGetLastError();
+}
+hipError_t qp_fused_eval(const QPBatch& qb, hipStream_t st) {
+  hipLaunchKernelGGL(k_fused_eval, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d);
   return hipGetLastError();
 }
 hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st) {
