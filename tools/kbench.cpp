@@ -37,6 +37,10 @@ __global__ void fill_qd(double* K, int64_t ld, int N, unsigned long long seed) {
   }
 }
 
+__global__ void kb_to_f32(const double* __restrict__ s, float* __restrict__ d, int64_t n) {
+  for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) d[i] = (float)s[i];
+}
+
 struct Timer {
   hipEvent_t a, b;
   Timer() {
@@ -79,6 +83,75 @@ int main(int argc, char** argv) {
   CK(hipMemset(pctrl, 0, ipmz::panel_ctrl_words(N, 64) * 4));
   Timer t;
   hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
+  if (mode == "solvecmp") {  // kbench_stamps N solvecmp: the persistent solve in fp64 and fp32 on one factor
+    hipStream_t sB, sC;
+    CK(hipStreamCreate(&sB));
+    CK(hipStreamCreate(&sC));
+    std::vector<hipEvent_t> ev(3 * (N / 64 + 2) + 8);
+    for (size_t i = 0; i < ev.size(); ++i) CK(hipEventCreateWithFlags(&ev[i], hipEventDisableTiming));
+    CK(ipmz::ldlt_factor(K, ld, N, D, Linv, W, 512, 64, info, st, nullptr, sB, sC, ev.data(), (int)ev.size(), pctrl));
+    CK(hipStreamSynchronize(st));
+    CK(hipDeviceSynchronize());
+    const int nb = (N + 127) / 128;
+    static unsigned long long stp[2][256][6];
+    auto report = [&](const char* tag, float ms) {
+      CK(ipmz::solve_stamps(&stp[0][0][0]));
+      double hop = 0, det = 0, post = 0, wait = 0;
+      int late = 0, cnt = 0;
+      for (int j = 4; j < nb && j < 256; ++j) {
+        const double s1 = (double)stp[0][j - 1][3], s = (double)stp[0][j][3], seen = (double)stp[0][j][4],
+                     cin = (double)stp[0][j][2];
+        hop += s - s1, det += seen - s1, post += s - seen, wait += seen - cin;
+        late += cin > s1;
+        ++cnt;
+      }
+      std::printf("%s N=%d: %.3f ms per solve (2 sweeps); forward hops %d..%d: hop %.2f us = detect %.2f + post %.2f; "
+                  "critical wait %.2f us; blocks whose bulk finished after y_{J-1}: %d\n",
+                  tag, N, ms, 4, nb - 1, hop / cnt / 100.0, det / cnt / 100.0, post / cnt / 100.0, wait / cnt / 100.0,
+                  late);
+      // block J's clocks relative to the store of y_{J-1}
+      double rel[5] = {0, 0, 0, 0, 0};
+      for (int j = 4; j < nb && j < 256; ++j)
+        for (int i = 0; i < 5; ++i) rel[i] += ((double)stp[0][j][i] - (double)stp[0][j - 1][3]) / 100.0;
+      std::printf("   block J vs y_{J-1} stored (us): start %.2f, bulk done %.2f, at hand-off %.2f, "
+                  "y_{J-1} seen %.2f, y_J stored %.2f; previous stores: y_{J-2} %.2f, y_{J-3} %.2f\n",
+                  rel[0] / cnt, rel[1] / cnt, rel[2] / cnt, rel[4] / cnt, rel[3] / cnt, -hop / cnt / 100.0,
+                  -2 * hop / cnt / 100.0);
+    };
+    double* P;
+    CK(hipMalloc(&P, ipmz::solve_prep_elems(N) * 8));
+    CK(hipMemsetAsync(b, 0, N * 8, st));
+    CK(ipmz::solve_reset(yb, xb, 8, N, ctrl, st));
+    CK(ipmz::solve_prep(K, ld, N, Linv, P, st));
+    CK(ipmz::ldlt_solve_persistent(K, ld, N, D, P, b, yb, xb, ctrl, st));
+    t.start(st);
+    for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve_persistent(K, ld, N, D, P, b, yb, xb, ctrl, st));
+    report("fp64", t.stop(st) / 5);
+    // the same factor in fp32
+    float *K32, *D32, *L32, *P32, *b32, *y32, *x32;
+    const int64_t nl = (int64_t)(N + 127) / 64 * 128 * 128;
+    CK(hipMalloc(&K32, ld * N * 4));
+    CK(hipMalloc(&D32, N * 4));
+    CK(hipMalloc(&L32, nl * 4));
+    CK(hipMalloc(&P32, ipmz::solve_prep_elems(N) * 4));
+    CK(hipMalloc(&b32, N * 4));
+    CK(hipMalloc(&y32, N * 4));
+    CK(hipMalloc(&x32, N * 4));
+    hipLaunchKernelGGL(kb_to_f32, dim3(2048), dim3(256), 0, st, K, K32, ld * N);
+    hipLaunchKernelGGL(kb_to_f32, dim3(64), dim3(256), 0, st, D, D32, (int64_t)N);
+    hipLaunchKernelGGL(kb_to_f32, dim3(512), dim3(256), 0, st, Linv, L32, nl);
+    CK(hipMemsetAsync(b32, 0, N * 4, st));
+    CK(ipmz::solve_reset(y32, x32, 4, N, ctrl, st));
+    CK(ipmz::solve_prep(K32, ld, N, L32, P32, st));
+    CK(ipmz::ldlt_solve_persistent(K32, ld, N, D32, P32, b32, y32, x32, ctrl, st));
+    t.start(st);
+    for (int r = 0; r < 5; ++r) CK(ipmz::ldlt_solve_persistent(K32, ld, N, D32, P32, b32, y32, x32, ctrl, st));
+    report("fp32", t.stop(st) / 5);
+    unsigned hctrl[8];
+    CK(hipMemcpy(hctrl, ctrl, sizeof(hctrl), hipMemcpyDeviceToHost));
+    std::printf("%s\ndone\n", hctrl[ipmz::SOLVE_ERR_WORD] ? "SOLVE ERROR" : "ok");
+    return 0;
+  }
   if (mode == "capture") {  // kbench N capture NBO DBG: the product factor's fork/join under hipStreamBeginCapture
     const int nbo = argc > 3 ? std::atoi(argv[3]) : 256;
     const int dbg = argc > 4 ? std::atoi(argv[4]) : 0;
