@@ -493,9 +493,12 @@ __global__ __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2))) void l
       // runs diag(J)'s first column pass -- off the transition's critical path
       auto linv_prev = [&]() {
         double* dst = Linv + (int64_t)(J - 1) * 64 * 64;
+        // the lower triangle only, to the end of the diagonal's 32-byte
+        // sector: the batched solve (trsv_small.h) never reads above the
+        // diagonal, and whole sectors of zeros need no HBM write
         for (int idx = tid - 64; idx < 64 * 64; idx += 192) {
           const int rr = idx >> 6, cc = idx & 63;
-          dst[idx] = cc > rr ? 0.0 : X[rr * DS + cc];  // (block J-1 < NB-1: full)
+          if (cc <= (rr | 3)) dst[idx] = cc > rr ? 0.0 : X[rr * DS + cc];  // (block J-1 < NB-1: full)
         }
       };
       if (J == 0)
