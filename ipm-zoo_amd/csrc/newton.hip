@@ -1300,13 +1300,24 @@ hipError_t qp_fused_solves(const QPBatch& qb, const double* K, int64_t ld, int N
                        b, sK, sD, sL, sb, freeze);
   return hipGetLastError();
 }
+// the evaluation's workgroups per QP: enough for two row passes (4 rows per
+// wave, 8 waves) as long as the whole grid stays resident (8 waves per SIMD
+// at 64 VGPRs: 4 workgroups per CU).  C4: B = 1024 -> 1, B = 128 -> 5
+// (0.038 -> 0.035 ms against the 4 of fused_split; 2 or 8 slower,
+// profiles/r05_s/c4_eval_split_ab.txt)
+static int eval_split(const QPBatch& qb) {
+  const int cap = 4 * device_cus() / qb.B;
+  const int rows = (qb.h.n + qb.h.m + qb.h.p + 63) / 64;
+  const int s = rows < cap ? rows : cap;
+  return s < 1 ? 1 : (s > 8 ? 8 : s);
+}
 hipError_t qp_fused_eval(const QPBatch& qb, hipStream_t st) {
-  hipLaunchKernelGGL(k_fused_eval, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d);
+  hipLaunchKernelGGL(k_fused_eval, dim3(eval_split(qb), qb.B), dim3(FT), 0, st, qb.d);
   return hipGetLastError();
 }
 hipError_t qp_fused_post(const QPBatch& qb, int freeze, hipStream_t st) {
   hipLaunchKernelGGL(k_fused_post, dim3(qb.B), dim3(FT), 0, st, qb.d, freeze);
-  hipLaunchKernelGGL(k_fused_eval, dim3(fused_split(qb.B), qb.B), dim3(FT), 0, st, qb.d);
+  hipLaunchKernelGGL(k_fused_eval, dim3(eval_split(qb), qb.B), dim3(FT), 0, st, qb.d);
   return hipGetLastError();
 }
 
