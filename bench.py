@@ -402,9 +402,39 @@ def main():
             for w, sub in out.get("configs", {}).items():
                 if w in cpu:
                     sub["cpu_baseline"] = cpu[w]
+        # last key of the line: every config's figures in a few hundred
+        # bytes, so a record that keeps only the line's tail still has them
+        out["summary"] = summary(out, args.workload)
         print(json.dumps(out))
     if world > 1:
         dist.destroy_process_group()
+
+
+def summary(out, workload):
+    """{config: [value, unit, ms/step, factor ms/step, roofline frac, cpu
+    baseline value]} for the headline and every sub-line."""
+    def row(d):
+        if not d or "value" not in d:
+            return None
+        ph = d.get("phase_ms_per_step") or {}
+        roof = d.get("roofline") or {}
+        cpu = (d.get("cpu_baseline") or {}).get("value")
+
+        def r(x, k=4):
+            return None if x is None else float(f"{x:.{k}g}")
+        return [r(d["value"], 6), d.get("unit"), r(d.get("ms_per_step")), r(ph.get("factor")),
+                r(roof.get("frac"), 3), r(cpu)]
+    head = out.get("config", {}).get("workload", workload)
+    if head == "c4":
+        head = f"c4_b{out['config'].get('global_batch')}"
+    sm = {"columns": ["value", "unit", "ms_per_step", "factor_ms", "frac", "cpu_value"], head: row(out)}
+    if "batched" in out:
+        sm[f"c4_b{out['batched']['config']['global_batch']}"] = row(out["batched"])
+    if "batched_shard" in out:
+        sm["c4_b128"] = row(out["batched_shard"])
+    for w, sub in out.get("configs", {}).items():
+        sm[w] = row(sub)
+    return sm
 
 
 if __name__ == "__main__":

@@ -92,7 +92,11 @@ typedef struct ipmz_qp ipmz_qp;
 int ipmz_ctx_create(ipmz_ctx** out, int device);
 /* Destroying a context that solvers (ipmz_qp_create / ipmz_batch_create)
  * still use only marks it: it is freed when the last of them is destroyed
- * (so a garbage collector may finalize the two in either order). */
+ * (so a garbage collector may finalize the two in either order; the calls
+ * are thread-safe with respect to each other).  A marked context first
+ * drains an external stream set with ipmz_ctx_set_stream and then runs its
+ * remaining solvers on its own stream; creating a solver on it returns
+ * IPMZ_ERR_STATE. */
 int ipmz_ctx_destroy(ipmz_ctx* ctx);
 /* Enqueue on an external HIP stream, e.g. torch.cuda.current_stream().cuda_stream.
  * NULL selects the HIP null (legacy default) stream -- what PyTorch's

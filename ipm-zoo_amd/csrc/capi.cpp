@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -57,10 +58,14 @@ struct ipmz_ctx {
   const unsigned* check_se = nullptr;
   // solvers created on this context and not yet destroyed: a context
   // destroyed before them (e.g. a garbage collector finalizing both in either
-  // order) is only marked, and freed with the last of them
+  // order) is only marked, and freed with the last of them.  Both fields are
+  // read and written only under g_ctx_mutex (ctypes drops the GIL around
+  // every call, and finalizers run on any thread).
   int users = 0;
   bool closed = false;
 };
+
+static std::mutex g_ctx_mutex;
 
 // outer panel width for an order-N factor: the context's, or by size --
 // 512 for N > 4096 (kbench factor, N = 11264: 12.95 ms at 384, 12.34 at
@@ -143,9 +148,25 @@ static void ctx_free(ipmz_ctx* ctx) {
 }
 
 int ipmz_ctx_destroy(ipmz_ctx* ctx) {
-  if (!ctx || ctx->closed) return IPMZ_OK;
-  ctx->closed = true;
-  if (ctx->users == 0) ctx_free(ctx);
+  if (!ctx) return IPMZ_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mutex);
+    if (ctx->closed) return IPMZ_OK;
+    ctx->closed = true;
+    if (ctx->users > 0) {
+      // freed with its last solver: from now on the solvers run on the
+      // context's own stream, so that late free never touches a caller's
+      // stream whose owner may have released it after this call (what the
+      // solvers enqueued there is drained first)
+      if (ctx->stream != ctx->own) {
+        hipSetDevice(ctx->device);
+        hipStreamSynchronize(ctx->stream);
+      }
+      ctx->stream = ctx->own;
+      return IPMZ_OK;
+    }
+  }
+  ctx_free(ctx);
   return IPMZ_OK;
 }
 
@@ -1056,7 +1077,14 @@ int create_solver(ipmz_ctx* ctx, const ipmz_qp_config* cfg, int B, ipmz_qp** out
   HIP_OK(hipSetDevice(ctx->device));
   auto* s = new ipmz_qp();
   s->ctx = ctx;
-  ++ctx->users;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mutex);
+    if (ctx->closed) {
+      delete s;
+      return fail(IPMZ_ERR_STATE, "context already destroyed");
+    }
+    ++ctx->users;
+  }
   s->B = B;
   s->n = cfg->n;
   s->m_usr = cfg->m;
@@ -1525,7 +1553,12 @@ int ipmz_qp_destroy(ipmz_qp* s) {
   if (s->mw.hst) hipHostFree(s->mw.hst);
   ipmz_ctx* ctx = s->ctx;
   delete s;
-  if (--ctx->users == 0 && ctx->closed) ctx_free(ctx);
+  bool last;
+  {
+    std::lock_guard<std::mutex> lk(g_ctx_mutex);
+    last = --ctx->users == 0 && ctx->closed;
+  }
+  if (last) ctx_free(ctx);
   return IPMZ_OK;
 }
 

@@ -31,7 +31,9 @@ namespace ipmz {
 // 256 = the fp32 factor's look-ahead strip on the trailing stream before the trailing update (no fourth stream),
 // 512 = the eager mixed-precision solve enqueues all max_refine + 1 passes (no host stop test),
 // 1024 = the fp64 trailing and strip updates on gemm.h's register-staged kernel instead of gemm64.h's (A/B),
-// 2048 = the panel's chain launch runs the 512-thread kernel with the 8-wave chain roles (chain8, A/B),
+// 2048 = an early chain launch (started beside the previous panel's rows launch) never sees that
+//        launch's RDONE flags: it gives its roles back after 1 ms and the rows launch takes them
+//        (the serialized-dispatch path, tests/test_gpu_panel_forms.py),
 // 4096 = the chain launch draws no ticket: the rows launch runs every chain role in its 4-wave form
 //        (what a serialized dispatch order can produce; the forms must factor bitwise alike),
 // 8192 = batches assemble the whole KKT into K every step (not the kept K0) (A/B),
@@ -39,7 +41,7 @@ namespace ipmz {
 enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4, IPMZ_DEBUG_CONVERT_ONLY = 16,
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
-       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_CHAIN8 = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
+       IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_GIVEBACK = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
        IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \

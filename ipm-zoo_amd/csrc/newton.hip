@@ -1128,10 +1128,12 @@ __global__ __launch_bounds__(FT) void k_fused_post(const QPDev* __restrict__ qs,
 // like trsv_small_kernel<8>.)
 template <int NW>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW == 8 ? 4 : 1))) void k_fused_solves(const QPDev* __restrict__ qs, const double* __restrict__ K,
-                                                          int64_t ld, int N, const double* __restrict__ D,
-                                                          const double* __restrict__ Linv, double* __restrict__ b,
+                                                          int64_t ld, int N, const double* D,
+                                                          const double* __restrict__ Linv, double* b,
                                                           int64_t sK, int64_t sD, int64_t sL, int64_t sb,
                                                           int freeze) {
+  // (b and D without __restrict__: the middle and post phases reach the
+  // same vectors through qs[i].b / the QP's D as well)
   extern __shared__ __attribute__((aligned(16))) double sm[];
   __shared__ double sh[NW];
   const int64_t i = blockIdx.x;

@@ -260,3 +260,43 @@ def test_c4_pair_kernel_rejected_when_not_coresident(ctx):
     with pytest.raises(I.IpmzError):
         bt.set_factor_kernel(4)
     bt.close()
+
+
+NO_FUSED_SOLVES = 16384  # kernels.h IPMZ_DEBUG_NO_FUSED_SOLVES
+
+
+def _fused_vs_separate(ctx, B, steps, mask):
+    I.debug_inject(mask)
+    try:
+        bt = I.Batch(N_, M_, 0, B, ctx)
+        bt.generate(0)
+        out = []
+        for _ in range(steps):
+            bt.step()
+            out.append((bt.batch_scalars().copy(),
+                        np.stack([np.concatenate([bt.state(i, 0), bt.state(i, 1), bt.state(i, 2)])
+                                  for i in range(0, B, max(1, B // 64))])))
+        bt.close()
+        return out
+    finally:
+        I.debug_inject(0)
+
+
+@pytest.mark.parametrize("B", [1024, 128])
+def test_c4_fused_solves_vs_separate_launches(ctx, B):
+    """k_fused_solves (both solves + the middle and post phases in one per-QP
+    launch, the default) against the separate launches (debug bit 16384):
+    at B = 1024 (8 waves per QP) the same operations in the same order --
+    bitwise; at B = 128 (16 waves) the middle / post reductions sum 16 wave
+    partials instead of 8 -- within 1e-12 relative over 5 steps."""
+    steps = 5
+    fused = _fused_vs_separate(ctx, B, steps, 0)
+    sep = _fused_vs_separate(ctx, B, steps, NO_FUSED_SOLVES)
+    for it, ((sf, vf), (ss, vs)) in enumerate(zip(fused, sep)):
+        if B == 1024:
+            assert np.array_equal(sf, ss), it
+            assert np.array_equal(vf, vs), it
+        else:
+            np.testing.assert_allclose(sf[:, :8], ss[:, :8], rtol=1e-12, atol=1e-300, err_msg=str(it))
+            scale = np.maximum(np.abs(vs), 1.0)
+            assert (np.abs(vf - vs) / scale).max() < 1e-12, it

@@ -72,3 +72,49 @@ def test_fp32_mixed_factor_bitwise_repeatable(ctx, N):
     for r in range(1, REPS):
         assert np.isfinite(out[r][0]).all()
         assert np.array_equal(out[r][0], out[0][0]) and np.array_equal(out[r][1], out[0][1]), r
+
+
+@pytest.mark.parametrize("N,reps", [(2560, 300), (4096, 200)])
+def test_fp64_early_chain_factor_run_to_run_long(ctx, N, reps):
+    """The early-chain panel path (each chain launch starts beside the
+    previous panel's rows launch, gated by RDONE flags; 384-wide panels at
+    C2's N = 2560, the last panels of N = 4096) over hundreds of factors in
+    one process, bitwise against the first: the cross-launch gates are the
+    kind of race a 4-factor check cannot see (the C4 factor's was once in
+    ~360 factors, test_c4_eager_steps_run_to_run_bitwise)."""
+    K = _qd(N, N + 2)
+    wsb = ctx.workspace_bytes(N)
+    ws = torch.zeros(wsb // 8 + 1, dtype=torch.float64, device="cuda")
+    D = torch.zeros(N, dtype=torch.float64, device="cuda")
+    Kf = torch.empty_like(K)
+    first = None
+    bad = []
+    for r in range(reps):
+        Kf.copy_(K)
+        assert ctx.ldlt_factor(N, Kf.data_ptr(), N, D.data_ptr(), ws.data_ptr(), wsb) == 0
+        out = (torch.tril(Kf, -1), D.clone())
+        if first is None:
+            first = out
+            assert torch.isfinite(first[0]).all() and torch.isfinite(first[1]).all()
+        elif not (torch.equal(out[0], first[0]) and torch.equal(out[1], first[1])):
+            bad.append(r)
+    ctx.sync()
+    assert not bad, bad[:8]
+
+
+def test_c2_normal_steps_run_to_run_long(ctx):
+    """Two C2 solvers (n = 2048, m = 512, normal equations) from the same
+    seed, 200 eager Newton steps each, restarting converged ones: iterates
+    and directions bitwise equal after every step."""
+    g = [I.Optimizer(2048, 512, 0, ctx) for _ in range(2)]
+    for o in g:
+        o.generate(1234)
+        o.set_reduction(I.REDUCTION_NORMAL)
+    for it in range(200):
+        for o in g:
+            o.step(I.STEP_RESTART_IF_CONVERGED)
+        v0, v1 = g[0].vars(), g[1].vars()
+        assert np.array_equal(v0, v1), it
+        assert np.array_equal(g[0].dir(), g[1].dir()), it
+    for o in g:
+        o.close()

@@ -1,10 +1,14 @@
-"""The panel's chain roles in both of their forms factor bitwise alike
-(panel.hip): the 4-wave chain of the 256-thread chain launch (production),
-the 8-wave chain of the 512-thread chain launch (debug bit IPMZ_DEBUG_CHAIN8), and
-every chain role run by the rows launch in its 4-wave form (debug bit
-IPMZ_DEBUG_ROWS_CHAIN -- what a serialized dispatch order, e.g. under
-rocprofv3 --pmc, produces).  A role may land in either launch, so the forms
-must agree to the bit or the factor would not be run-to-run deterministic.
+"""The panel's chain roles factor bitwise alike whichever launch runs them
+(panel.hip): the chain launch (production), every chain role run by the
+rows launch (debug bit IPMZ_DEBUG_ROWS_CHAIN: no chain launch at all -- what
+a serialized dispatch order, e.g. under rocprofv3 --pmc, produces), and the
+early chain launch's give-back (debug bit IPMZ_DEBUG_GIVEBACK: a chain
+launch started beside the previous panel's rows launch never sees that
+launch's RDONE flags, so prev_rows_ready times out after 1 ms, the launch
+draws no role and the rows launch queued behind it takes every chain role;
+N <= 4096 left from a panel).  A role may land in either launch, so the
+forms must agree to the bit or the factor would not be run-to-run
+deterministic, and no form may raise the sticky hand-off error.
 
 fp64 (LinearSolvers::ldlt_decomposition, LinearSolvers.cpp:14-42, blocked,
 look-ahead schedule) and the fp32 factor of the mixed-precision path."""
@@ -15,8 +19,8 @@ pytestmark = pytest.mark.gpu
 I = pytest.importorskip("ipmz_amd")
 torch = pytest.importorskip("torch")
 
-CHAIN8, ROWS_CHAIN = 2048, 4096  # kernels.h IPMZ_DEBUG_CHAIN8 / IPMZ_DEBUG_ROWS_CHAIN
-MODES = [0, CHAIN8, ROWS_CHAIN]
+GIVEBACK, ROWS_CHAIN = 2048, 4096  # kernels.h IPMZ_DEBUG_GIVEBACK / IPMZ_DEBUG_ROWS_CHAIN
+MODES = [0, GIVEBACK, ROWS_CHAIN]
 
 
 @pytest.fixture(scope="module")
@@ -65,7 +69,7 @@ def test_fp64_chain_forms_bitwise(ctx, N):
         assert ctx.ldlt_factor(N, Kf.data_ptr(), N, D.data_ptr(), ws.data_ptr(), wsb) == 0
         x = b.clone()
         ctx.ldlt_solve(N, Kf.data_ptr(), N, D.data_ptr(), ws.data_ptr(), x.data_ptr())
-        ctx.sync()
+        ctx.sync()  # raises on a sticky hand-off error (IPMZ_ERR_HIP)
         return torch.tril(Kf, -1).cpu().numpy(), D.cpu().numpy(), x.cpu().numpy()
 
     out = [_with_mask(m, run) for m in MODES + [0]]
@@ -94,3 +98,23 @@ def test_fp32_chain_forms_bitwise(ctx, N):
     assert np.isfinite(out[0][0]).all()
     for r in range(1, len(out)):
         assert np.array_equal(out[r][0], out[0][0]) and np.array_equal(out[r][1], out[0][1]), MODES[r]
+
+
+def test_c2_normal_steps_giveback_bitwise(ctx):
+    """C2 (n = 2048, m = 512, normal equations, N = 2560, 384-wide panels --
+    every panel's chain launch starts early): Newton steps with every early
+    chain launch giving its roles back equal the production steps bitwise."""
+    def run():
+        g = I.Optimizer(2048, 512, 0, ctx)
+        g.generate(1234)
+        g.set_reduction(I.REDUCTION_NORMAL)
+        out = []
+        for _ in range(3):
+            g.step()
+            out.append((g.vars(), g.dir()))
+        g.close()
+        return out
+
+    a, b = run(), _with_mask(GIVEBACK, run)
+    for (va, da), (vb, db) in zip(a, b):
+        assert np.array_equal(va, vb) and np.array_equal(da, db)
