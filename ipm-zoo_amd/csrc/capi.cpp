@@ -79,10 +79,16 @@ static int nbo_for(const ipmz_ctx* ctx, int N) {
   return N <= 4096 ? 384 : 512;
 }
 
+// The pool's events only order the factor's streams on one device: no
+// system-scope release / acquire fence when one is recorded or waited for
+// (the default writes the L2 back for the host at every record, on the
+// panel chain's stream between every two chain launches); a runtime that
+// refuses the flag gets the default events
 static int ensure_events(ipmz_ctx* ctx, size_t n) {
   while (ctx->evpool.size() < n) {
     hipEvent_t e;
-    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess &&
+        hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess)
       return fail(IPMZ_ERR_HIP, "hipEventCreate failed");
     ctx->evpool.push_back(e);
   }

@@ -864,11 +864,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
 // (<= IPMZ_EARLY_CHAIN_MAX_N: the chain is the critical path): no GEMM
 // workgroup beside it either
 // (kbench N = 2560: 1.15 -> 1.10 ms; at N = 11264, where the trailing GEMM
-// is, 10.97 -> 11.2 ms, so not there; profiles/r05_s/chain_lds_pad_ab.txt)
+// is, 10.97 -> 11.2 ms, so not there; profiles/r05_s/chain_lds_pad_ab.txt).
+// 144 KB where the whole factor is that small (C2): not even a 64 x 64
+// strip-GEMM workgroup (24 KB) beside it (C2 724 -> 734 steps/s; the same
+// for C3's tail panels: 75.7 -> 74.6, so not there; profiles/r06_s8)
 template <typename T>
-static size_t chain_lds_pad(int N) {
+static size_t chain_lds_pad(int Nleft, int N) {
   constexpr size_t own = (2 * 64 * DS + 64 + 64) * sizeof(double) + 64;
-  constexpr size_t big = 113 * 1024, small = 95 * 1024;
+  constexpr size_t big = 113 * 1024, small = 95 * 1024, whole = 144 * 1024;
   // the attribute per device (a process may factor on several): 0 not yet
   // set, 1 set, 2 refused (then no padding)
   static std::atomic<unsigned char> state[64];
@@ -877,11 +880,12 @@ static size_t chain_lds_pad(int N) {
   unsigned char st = state[dev].load(std::memory_order_acquire);
   if (st == 0) {
     st = hipFuncSetAttribute(reinterpret_cast<const void*>(&panel_kernel<T>),
-                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(big - own)) == hipSuccess ? 1 : 2;
+                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)(whole - own)) == hipSuccess ? 1 : 2;
     state[dev].store(st, std::memory_order_release);
   }
   if (st != 1) return 0;
-  return (N <= IPMZ_EARLY_CHAIN_MAX_N ? big : small) - own;
+  if (N <= IPMZ_EARLY_CHAIN_MAX_N) return whole - own;
+  return (Nleft <= IPMZ_EARLY_CHAIN_MAX_N ? big : small) - own;
 }
 
 template <typename T>
@@ -922,7 +926,7 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
     // every chain role; the padding (dynamic LDS) makes each of its
     // workgroups hold a CU with no other panel workgroup (the chain's
     // barrier-bound blocks lose a third of their speed beside a helper)
-    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N - k0), st_chain, a, 0,
+    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N - k0, N), st_chain, a, 0,
                        rows_prev ? 1 : 0);
   }
   hipError_t e = hipGetLastError();
