@@ -110,7 +110,7 @@ def cpu_baselines(names):
 
 def load_json(rel):
     path = os.path.join(REPO, rel)
-    if not os.path.exists(path):
+    if not rel or not os.path.isfile(path):
         return None
     with open(path) as fh:
         out = json.load(fh)
@@ -292,7 +292,7 @@ def run_single(I, ctx, args, world, dist, torch, workload):
         tr_s = ph["trailing"] * 1e-3
         launches = ph["trailing_launches"]
         if launches:
-            trk = load_json("profiles/pmc_traffic.json") if workload == "c3" else None
+            trk = load_json({"c3": "profiles/pmc_traffic.json", "c5": "profiles/pmc_traffic_c5.json"}.get(workload, ""))
             tach = ph["trailing_flops"] / tr_s / 1e12
             roof["trailing"] = {
                 "kernel": ("sgemm_nt_kernel<128,128,...> (csrc/gemm32.h, v_mfma_f32_32x32x2_f32; trailing update "

@@ -14,15 +14,21 @@ R per launch is recovered from the grid size (triangular grid of 128 x 128
 tiles; grid / workgroup size).
 
     python tools/pmc_traffic.py gpurun_out/pmc_fetch gpurun_out/pmc_write <profile label> > profiles/pmc_traffic.json
-(IPMZ_PMC_NBO: the outer panel width of the profiled run, default 384 = C3's)
+    IPMZ_PMC_PREC=32 python tools/pmc_traffic.py ... > profiles/pmc_traffic_c5.json   (C5's fp32 trailing update)
+(IPMZ_PMC_NBO: the outer panel width of the profiled run, default 512 = C3's and C5's)
 """
 import csv
 import json
 import math
 import sys
 
-KERNEL = "dgemm_nt_glds_kernel<128, 128, 4, 4, 8, 3, 8, 0>"  # C3's trailing update (gemm64.h)
-NBO = int(__import__("os").environ.get("IPMZ_PMC_NBO", 512))  # the bench's outer panel width (C3: 512)
+import os
+
+PREC = int(os.environ.get("IPMZ_PMC_PREC", 64))
+KERNEL = ("dgemm_nt_glds_kernel<128, 128, 4, 4, 8, 3, 8, 0>" if PREC == 64  # C3's trailing update (gemm64.h)
+          else "sgemm_nt_glds_kernel<128, 128, 2, 2, 16, 3, 2, 0, true>")   # C5's (gemm32.h)
+ES = PREC // 8  # bytes per element
+NBO = int(os.environ.get("IPMZ_PMC_NBO", 512))  # the bench's outer panel width (C3, C5: 512)
 
 
 def rows(d):
@@ -44,7 +50,7 @@ def main():
         R = t * 128  # tile-rounded trailing order (upper bound of R)
         tot_f += 2.0 * float(a["Counter_Value"]) * 1024
         tot_w += float(b["Counter_Value"]) * 1024
-        tot_alg += 16.0 * R * (R + 1) / 2 + 16.0 * R * NBO
+        tot_alg += 2.0 * ES * R * (R + 1) / 2 + 2.0 * ES * R * NBO
     n = len(fr)
     per = (tot_f + tot_w) / n
     out = {
