@@ -145,6 +145,55 @@ __device__ __forceinline__ void colpass16_spec(double* M, double* dsh, int p, in
   }
   if (lane < 16) dsh[16 * p + lane] = dreg;
 }
+// The same pass with a shorter dependent chain per pivot.  The pass time is
+// the chain's latency (fewer instructions per step did not move it, round 6),
+// and the chain was readlane(1/d_k) -> l = v_k / d_k -> v_{k+1} -= l w ->
+// zero test -> select -> rcp -> two Newton steps.  Here the column-(k+1)
+// update is v_{k+1} -= (v_k w) / d_k with v_k w formed off the chain (v_k
+// and w are final one step earlier), and the zero rule is applied to the
+// reciprocal (1 / 1e-8 selected after the rcp, the test beside it):
+// readlane -> fma -> rcp -> NEWTON x (2 fma) -> select.  Other columns as in
+// colpass16_spec.  Rounding differs from it at the 1e-16 level (the product
+// order of the column-(k+1) update).
+template <int NEWTON>
+__device__ __forceinline__ void colpass16_short(double* M, double* dsh, int p, int lane) {
+  const int row = 16 * p + lane;
+  const bool act = row < 64;
+  const int rr = act ? row : 63;
+  double v[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) v[j] = M[rr * DS + 16 * p + j];
+  const double rz = fast_rcp(1e-8);  // LinearSolvers.cpp:26-28: a zero pivot is 1e-8
+  double dreg = 1.0, rl;
+  auto piv = [&](double x) {
+    double r = __builtin_amdgcn_rcp(x);
+#pragma unroll
+    for (int it = 0; it < NEWTON; ++it) r = fma(r, fma(-x, r, 1.0), r);
+    rl = x == 0.0 ? rz : r;
+  };
+  piv(v[0]);
+  static_for<16>([&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const double rdk = readlane_t(rl, k);
+    dreg = lane == k ? (v[k] == 0.0 ? 1e-8 : v[k]) : dreg;
+    if constexpr (k + 1 < 16) {
+      const double t = v[k] * readlane_t(v[k], k + 1);
+      v[k + 1] = fma(-t, rdk, v[k + 1]);
+      piv(v[k + 1]);
+    }
+    const double l = lane > k ? v[k] * rdk : 0.0;
+    static_for<(k + 2 < 16 ? 14 - k : 0)>([&](auto jc) {
+      constexpr int j = k + 2 + decltype(jc)::value;
+      v[j] = fma(-l, readlane_t(v[k], j), v[j]);  // w_j = A[j][k], row j = lane j
+    });
+    v[k] = lane > k ? l : v[k];
+  });
+  if (act) {
+#pragma unroll
+    for (int j = 0; j < 16; ++j) M[rr * DS + 16 * p + j] = v[j];
+  }
+  if (lane < 16) dsh[16 * p + lane] = dreg;
+}
 // X_pp = L_pp^{-1} of a unit-lower 16 x 16 tile: lane c (mod 16) solves
 // L x = e_c right-looking (L entries are wave-uniform LDS broadcasts)
 __device__ __forceinline__ void inv16(const double* Lt, double* Xt, int lane) {
@@ -270,6 +319,8 @@ __device__ __forceinline__ void diag64_body(TS* __restrict__ K, int64_t ld, int 
   auto xoff = [&](int p, int j) { xmul(p, j, xsum(p, j)); };  // X_pj = -X_pp sum_{k=j}^{p-1} L_pk X_kj
   auto colpass = [&](int p) {
     if constexpr (CPV == 1) colpass16_spec(M, dsh, p, lane);
+    else if constexpr (CPV == 3) colpass16_short<2>(M, dsh, p, lane);
+    else if constexpr (CPV == 4) colpass16_short<1>(M, dsh, p, lane);
     else colpass16(M, dsh, p, lane);
   };
   if (wave == 0) colpass(0);

@@ -5,7 +5,7 @@
 #include <stdio.h>
 
 #define IPMZ_NBO_MAX 512
-#define IPMZ_PANEL_CTRL_WORDS 256
+#define IPMZ_PANEL_CTRL_WORDS 320
 // fused factor: largest N whose chain launches start beside the previous
 // panel's rows launch (ldlt.hip)
 #define IPMZ_EARLY_CHAIN_MAX_N 4096

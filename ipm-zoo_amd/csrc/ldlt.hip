@@ -523,6 +523,13 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // its start is small enough (the chain-bound periods; C2 from its first
   // panel, C3 / C5 their last ones)
   auto early_at = [&](int j) { return early_ok && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
+  // per panel j >= 1: the look-ahead update of its rows below the region as
+  // strip tiles of its rows launch instead of a strip GEMM before it on C,
+  // where the order left is as small (the chain-bound periods: the rows roles
+  // then start as their own rows are done, not behind a whole GEMM launch, and
+  // keep pace with the chain; panel.hip strip_tile).  Capture or not alike, so
+  // a captured step computes what an eager one does.
+  auto tiles_at = [&](int j) { return two && fused && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
   T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
@@ -532,7 +539,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     if (!fused) return factor_panel(K, ld, N, D, Linv, Wb(k), k0, pw(k), nbo, nbi, info, st);
     return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo,
                         (two && prev) ? slot00(k) : nullptr, two ? slot00(k + 1) : nullptr, info, area(k), err,
-                        prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, false, st, sC,
+                        prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, prev && tiles_at(k), st, sC,
                         (early_at(k) && prev) ? area(k - 1) : nullptr);
   };
   hipError_t e = hipSuccess;
@@ -619,7 +626,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       // the region itself); panel k's chain roles may have run in its chain
       // launch, so C also waits for that launch
       if ((e = stream_wait(sC, evA[k])) != hipSuccess) return e;
-      if (p2 < N) {
+      if (p2 < N && !tiles_at(k + 1)) {
         if ((e = gemm_nt_sub_t<T>(N - p2, p2 - p1, bo, Wb(k) + (int64_t)p2 * nbo, nbo, K + (int64_t)p1 * ld + k0, ld,
                                   K + (int64_t)p2 * ld + p1, ld, p2, p1, false, sC, nullptr)) != hipSuccess)
           return e;

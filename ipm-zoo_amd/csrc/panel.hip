@@ -27,6 +27,14 @@
 //   rows roles (rows launch; one per 64 rows below the region): for every j:
 //     TRSM with L_jj^{-1} (waits DIAG[j]), L = T / D, W = T, and the strip
 //     pieces A[rows, q] -= L W[q, j]^T (waits REG[j][q]).
+//   strip tiles (rows launch, rows tickets before the rows roles, where the
+//     host asks for them instead of the strip GEMM on the rows stream): tile
+//     (r, q) of the rows below the region updated with the previous panel,
+//     stored write-through; PREV[r] counts row r's tiles, and rows role r
+//     waits for all nb of them.  Their inputs are complete when the launch
+//     starts (stream order), so they wait for nothing and the rows roles
+//     start as soon as their own row is updated, instead of behind a whole
+//     strip GEMM launch.
 //
 // Every role computes each element with the same operations in the same order
 // whichever launch holds it, so the factor is bitwise the same whichever
@@ -52,7 +60,8 @@ namespace ipmz {
 // -DIPMZ_CHAIN_STAMPS (tools/kbench "chainclk" only): s_memrealtime stamps of
 // the chain role per 64-column block (k0 / 64 + j): 0 diag start, 1 READY[c]
 // seen, 2 diag done, 3 operands loaded, 4 TRSM done, 5 next diagonal block
-// formed; helpers:
+// formed; rows role 0: 6 DIAG seen, 7 TRSM (+ block (0, 0) sum) done, 8 strips
+// done; helpers:
 // READY[c] published; rows role 0: start, end; launches: first workgroup
 // start per launch.
 __device__ unsigned long long g_cstamp[IPMZ_CHAIN_STAMP_BLOCKS][16];
@@ -67,6 +76,12 @@ __device__ unsigned long long g_hstamp[IPMZ_CHAIN_STAMP_BLOCKS][4];
 #define HSTAMP(jb, i)
 #endif
 #define CSTAMP(jb, i) CSTAMP_T(0, jb, i)
+// the chain's column pass (diag64.h): 4 = colpass16_short<1>, the shorter
+// per-pivot chain (in-panel block 20.0 -> 19.5-19.7 us, kbench chainclk
+// N = 2560, profiles/r06_s/chain_cpv_ab.txt); 1 = colpass16_spec
+#ifndef IPMZ_DIAG_CPV
+#define IPMZ_DIAG_CPV 4
+#endif
 hipError_t chain_stamps(unsigned long long* c, unsigned long long* h) {  // DEBUG
   hipError_t e = hipMemcpyFromSymbol(c, HIP_SYMBOL(g_cstamp), sizeof(g_cstamp));
   if (e != hipSuccess) return e;
@@ -76,12 +91,13 @@ hipError_t chain_stamps(unsigned long long* c, unsigned long long* h) {  // DEBU
 namespace {
 // ctrl words of a panel: OP_TICKET (chain tickets 0.., then rows tickets at
 // OP_TICKET + 1), DIAG[j], REG[j][q], READY[c], TILE[c][q], RDONE[r]
-enum { OP_TICKET = 0, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128, OP_RDONE = 192 };
+enum { OP_TICKET = 0, OP_R0 = 3, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128, OP_RDONE = 192, OP_PREV = 256 };
 constexpr int OP_NBMAX = IPMZ_NBO_MAX / 64;
+constexpr int OP_PREVMAX = IPMZ_PANEL_CTRL_WORDS - OP_PREV;  // rows roles that strip tiles can serve
 static_assert(OP_DIAG + OP_NBMAX <= OP_REG && OP_REG + OP_NBMAX * OP_NBMAX <= OP_READY, "ctrl layout");
 static_assert(OP_READY + OP_NBMAX <= OP_TILE, "ctrl layout");
 static_assert(OP_TILE + OP_NBMAX * OP_NBMAX <= OP_RDONE, "ctrl layout");
-static_assert(OP_RDONE + OP_NBMAX <= IPMZ_PANEL_CTRL_WORDS, "panel ctrl area too small");
+static_assert(OP_RDONE + OP_NBMAX <= OP_PREV && OP_PREVMAX >= IPMZ_EARLY_CHAIN_MAX_N / 64, "panel ctrl area too small");
 
 template <typename T>
 using Acc = typename Mfma<T>::acc_t;
@@ -337,6 +353,8 @@ struct PanelArgs {
   const unsigned* parea;
   int nchain;         // chain-role tickets
   int nrows;          // rows-role tickets
+  int nprev;          // strip-tile tickets (nrows * nb or 0), before the rows roles
+  int pre00w;         // 1: a PRE00 worker ticket after the rows roles sums pre00_out (else rows role 0)
 };
 
 template <typename T>
@@ -460,13 +478,13 @@ __device__ __forceinline__ void chain4(const PanelArgs<T>& a, double* smem, unsi
       if (threadIdx.x == 0) st_sc1(&area[OP_REG + (j - 1) * OP_NBMAX + j], 1u);
     };
     if (j == 0 && !a.Wprev)
-      diag64_body<true, false, T, false, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
-                                                              pre_wb, nullptr, tid);
+      diag64_body<true, false, T, false, 4, decltype(pre_wb), true, NoHook, IPMZ_DIAG_CPV, false, true, NoHook>(
+          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid);
     else if (j == 0)
-      diag64_body<true, false, T, true, 4, decltype(pre_wb)>(K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr,
-                                                             pre_wb, nullptr, tid);
+      diag64_body<true, false, T, true, 4, decltype(pre_wb), true, NoHook, IPMZ_DIAG_CPV, false, true, NoHook>(
+          K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid);
     else
-      diag64_body<true, false, T, true, 4, decltype(pre_wb), true, decltype(idle0), 1, true, true, decltype(post2)>(
+      diag64_body<true, false, T, true, 4, decltype(pre_wb), true, decltype(idle0), IPMZ_DIAG_CPV, true, true, decltype(post2)>(
           K, ld, j0, bj, a.D, Lb, a.info, M, X, dsh, nullptr, pre_wb, nullptr, tid, idle0, nullptr, post2);
     CSTAMP(j0 / 64, 2);
     if (!more) {
@@ -678,13 +696,10 @@ __device__ __forceinline__ void chain_roles(const PanelArgs<T>& a, int t, double
 
 // ---- a rows role (rows ticket r): the 64 rows from ce + 64 r.  Every
 // operand another role of this panel produced is read with agent-scope loads
-// (the producer may be in the other launch).  rows_prev: first the
-// look-ahead update of these rows with the PREVIOUS panel, A[rows, panel] -=
-// W_prev[rows] L_prev[panel rows]^T (the fused factor runs it as a strip GEMM
-// on the rows stream instead).
+// (the producer may be in the other launch).  With strip tiles (a.nprev),
+// it first waits for its row's look-ahead update with the previous panel.
 template <typename T>
-__device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool rows_prev, double* smem,
-                                          unsigned* sh_ok) {
+__device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, double* smem, unsigned* sh_ok) {
   T* const K = a.K;
   const int64_t ld = a.ld;
   const int k0 = a.k0, N = a.N, ldw = a.ldw;
@@ -695,42 +710,30 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
   T* As = reinterpret_cast<T*>(smem);
   T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
   T* Krow = K + (int64_t)row0 * ld;
-  if (rows_prev) {
-    for (int q = 0; q < nb; ++q) {
-      const int tid = launder((int)threadIdx.x);
-      const TMap<4> m(tid);
-      const int q0 = k0 + 64 * q, qrows = panel_bsz(a, q);
-      Acc<T> acc[4], tile[4];
-      zero_acc<T, 4>(acc);
-      prev_update<T, 4>(tid, acc, a.Wprev + (int64_t)row0 * ldw, ldw, K + (int64_t)q0 * ld + a.kprev, ld, rows, qrows,
-                        a.boprev, As, Bs);
-      load_acc<T, true, false, 4>(m, tile, Krow + q0, ld, rows, qrows);
-#pragma unroll
-      for (int n = 0; n < 4; ++n)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) tile[n][g] = tile[n][g] - acc[n][g];
-      store_acc<T, false, false, 4>(m, tile, Krow + q0, ld, rows, qrows);
-    }
-  }
+  // this row's strip tiles (rows tickets drawn before this one: running or done)
+  if (a.nprev && !wait_flag_ge(&a.area[OP_PREV + r], (unsigned)nb, a.err, sh_ok)) return;
   // ---- TRSMs and strips of this chunk's rows.  Role 0 (the next panel's
   // first 64 rows) also accumulates that panel's block (0, 0) look-ahead
   // update W(rows, j) L(rows, j)^T over j -- exactly the chunks prev_update
   // would sum in the next chain role -- and leaves it in pre00_out.
   if (r == 0) HSTAMP(k0 / 64, 1);
-  T* const p00 = r == 0 ? a.pre00_out : nullptr;
+  T* const p00 = r == 0 && !a.pre00w ? a.pre00_out : nullptr;
+  const bool r0w = r == 0 && a.pre00w;  // R0 counts this role's finished blocks for the PRE00 worker
   const bool wt = r < OP_NBMAX;  // rows of the next panel's diagonal region: RDONE[r]
-  Acc<T> a00[4];
+  Acc<T> a00[4], carry[4];
   zero_acc<T, 4>(a00);
+  __shared__ unsigned sh_pk;
   bool ok = true;
   for (int j = 0; j < nb && ok; ++j) {
     const int tid = launder((int)threadIdx.x), lane = tid & 63;
     const TMap<4> m(tid);
     const int j0 = k0 + 64 * j, bj = panel_bsz(a, j);
-    const T* Lb = a.Lb0 + (int64_t)j * 64 * 64;
     __syncthreads();  // previous block's strip finished reading As / Bs
-    stage_tile<T, true, 4>(tid, As, Krow + j0, ld, rows, bj);
+    if (j == 0) stage_tile<T, true, 4>(tid, As, Krow + j0, ld, rows, bj);
+    else put_acc<T, 4>(m, As, carry);  // tile (rows, j), final after block j-1's first strip
     if (!(ok = wait_flag(&a.area[OP_DIAG + j], a.err, sh_ok))) break;
-    stage_tile<T, true, 4>(tid, Bs, Lb, 64, 64, 64);
+    if (r == 0) CSTAMP(j0 / 64, 6);
+    stage_tile<T, true, 4>(tid, Bs, a.Lb0 + (int64_t)j * 64 * 64, 64, 64, 64);
     T rd[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n) {
@@ -741,7 +744,11 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
     Acc<T> acc[4];
     zero_acc<T, 4>(acc);
     mma_tile_lower<T, 4>(m, As, [&](int rr, int k) { return Bs[rr * DS + k]; }, acc);  // L_jj^{-1}: lower
+    // (R0: block j-1's L / W stores, long issued, drained here, off the MFMAs' way)
+    if (r0w && j > 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (r0w && j > 0 && threadIdx.x == 0)
+      __hip_atomic_store(&a.area[OP_R0], (unsigned)j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     Acc<T> lacc[4];
 #pragma unroll
     for (int n = 0; n < 4; ++n)
@@ -755,52 +762,141 @@ __device__ __forceinline__ void rows_role(const PanelArgs<T>& a, int r, bool row
       store_acc<T, false, false, 4>(m, acc, a.Wp + (int64_t)row0 * ldw + 64 * j, ldw, rows, bj);
     }
     put_acc<T, 4>(m, As, lacc);
-    if (p00) {  // a00 += W(rows, j) L(rows, j)^T (W staged in Bs, L in As)
-      put_acc<T, 4>(m, Bs, acc);
-      __syncthreads();
+    if (p00) put_acc<T, 4>(m, Bs, acc);  // W, for a00 below
+    if (r == 0) CSTAMP(j0 / 64, 7);
+    // strips: (rows, q) -= L(rows, j) W(q, j)^T, q = nb-1 .. j+1.  Their REG
+    // flags are polled together (the helpers raise them well ahead), the
+    // next strip's W and A tiles load during this one's MFMAs, and tile
+    // (rows, j+1), the next block's TRSM operand, the last one, stays in
+    // registers (carry) instead of a store and a reload.  (The poll's barrier
+    // frees Bs.)
+    if (!(ok = wait_flags(&a.area[OP_REG + j * OP_NBMAX + j + 1], nb - j - 1, nullptr, a.err, sh_ok, &sh_pk)))
+      break;
+    if (j + 1 < nb) {
+      T vw[16];
+      Acc<T> nxt[4];
+      auto fetch = [&](int q) {
+        const int qrows = panel_bsz(a, q);
+        fetch_tile<T, true, 4>(tid, vw, a.Wp + (int64_t)(k0 + 64 * q) * ldw + 64 * j, ldw, qrows, bj);
+        load_acc<T, true, false, 4>(m, nxt, Krow + k0 + 64 * q, ld, rows, qrows);
+      };
+      fetch(nb - 1);
+      if (p00) {  // a00 += W(rows, j) L(rows, j)^T (W in Bs, L in As), beside the first strip's loads
+        mma_tile<T, false, 4>(m, Bs, [&](int rr, int k) { return As[rr * DS + k]; }, a00);
+        __syncthreads();
+      }
+      for (int q = nb - 1; q > j; --q) {
+        const int q0 = k0 + 64 * q, qrows = panel_bsz(a, q);
+        put_tile<T, 4>(tid, Bs, vw, qrows, bj);
+        Acc<T> tile[4];
+#pragma unroll
+        for (int n = 0; n < 4; ++n) tile[n] = nxt[n];
+        __syncthreads();
+        if (q - 1 > j) fetch(q - 1);
+        mma_tile<T, true, 4>(m, As, [&](int rr, int k) { return Bs[rr * DS + k]; }, tile);
+        if (q == j + 1) {
+#pragma unroll
+          for (int n = 0; n < 4; ++n) carry[n] = tile[n];
+        } else {
+          store_acc<T, false, false, 4>(m, tile, Krow + q0, ld, rows, qrows);
+        }
+        __syncthreads();  // Bs reads done
+      }
+    } else if (p00) {
       mma_tile<T, false, 4>(m, Bs, [&](int rr, int k) { return As[rr * DS + k]; }, a00);
-      __syncthreads();  // Bs is reused by the strips
     }
-    // strips: (rows, q) -= L(rows, j) W(q, j)^T, q = j+1 .. nb-1
-    for (int q = j + 1; q < nb; ++q) {
-      const int q0 = k0 + 64 * q, qrows = panel_bsz(a, q);
-      if (!(ok = wait_flag(&a.area[OP_REG + j * OP_NBMAX + q], a.err, sh_ok))) break;  // (its barrier also frees Bs)
-      stage_tile<T, true, 4>(tid, Bs, a.Wp + (int64_t)q0 * ldw + 64 * j, ldw, qrows, bj);
-      Acc<T> tile[4];
-      load_acc<T, true, false, 4>(m, tile, Krow + q0, ld, rows, qrows);
-      __syncthreads();
-      mma_tile<T, true, 4>(m, As, [&](int rr, int k) { return Bs[rr * DS + k]; }, tile);
-      store_acc<T, false, false, 4>(m, tile, Krow + q0, ld, rows, qrows);
-      __syncthreads();
-    }
+    if (r == 0) CSTAMP(j0 / 64, 8);
   }
   if (p00 && ok) store_acc<T, true, false, 4>(TMap<4>(launder((int)threadIdx.x)), a00, p00, 64, 64, 64);
-  if (wt && ok) publish(&a.area[OP_RDONE + r]);
-  if (r == 0) HSTAMP(k0 / 64, 2);
+  if (r0w && ok) {  // the PRE00 worker raises RDONE[0]
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(&a.area[OP_R0], (unsigned)nb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if (wt && ok) {
+    publish(&a.area[OP_RDONE + r]);
+  }
+  if (wt) HSTAMP(k0 / 64 + r, 2);
+}
+
+// ---- the PRE00 worker (the last rows ticket, strip-tile panels): the next
+// panel's block (0, 0) look-ahead update W(rows 0, j) L(rows 0, j)^T summed
+// over j as rows role 0 finishes each block (R0) -- the same MFMAs in the same
+// order as role 0 sums it otherwise, off that role's path -- then pre00_out
+// and RDONE[0] (role 0's rows are final too: R0 = nb).
+template <typename T>
+__device__ __forceinline__ void pre00_worker(const PanelArgs<T>& a, double* smem, unsigned* sh_ok) {
+  const int nb = panel_nb(a);
+  const int ce = a.c1 < a.N ? a.c1 : a.N;
+  const int rows = a.N - ce < 64 ? a.N - ce : 64;
+  T* As = reinterpret_cast<T*>(smem);
+  T* Bs = reinterpret_cast<T*>(smem + 64 * DS);
+  Acc<T> a00[4];
+  zero_acc<T, 4>(a00);
+  for (int j = 0; j < nb; ++j) {
+    const int tid = launder((int)threadIdx.x);
+    const TMap<4> m(tid);
+    const int bj = panel_bsz(a, j);
+    if (!wait_flag_ge(&a.area[OP_R0], (unsigned)(j + 1), a.err, sh_ok)) return;  // (its barrier frees As / Bs)
+    stage_tile<T, true, 4>(tid, As, a.K + (int64_t)ce * a.ld + a.k0 + 64 * j, a.ld, rows, bj);  // L
+    stage_tile<T, true, 4>(tid, Bs, a.Wp + (int64_t)ce * a.ldw + 64 * j, a.ldw, rows, bj);     // W
+    __syncthreads();
+    mma_tile<T, false, 4>(m, Bs, [&](int rr, int k) { return As[rr * DS + k]; }, a00);
+  }
+  store_acc<T, true, false, 4>(TMap<4>(launder((int)threadIdx.x)), a00, a.pre00_out, 64, 64, 64);
+  publish(&a.area[OP_RDONE]);
+}
+
+// ---- a STRIP TILE (rows ticket u < nprev): tile (r, q), r = u / nb, of the
+// rows below the region, A[rows r, block q] -= W_prev[rows r] L_prev[q]^T --
+// the tile the strip GEMM on the rows stream computes otherwise, here in the
+// rows launch so that rows role r starts once its own nb tiles are done (its
+// inputs: the previous rows launch's W and L rows, complete in stream order).
+// Stored write-through, then PREV[r] += 1.
+template <typename T>
+__device__ __forceinline__ void strip_tile(const PanelArgs<T>& a, int u, double* smem) {
+  const int nb = panel_nb(a);
+  const int r = u / nb, q = u - r * nb;
+  const int ce = a.c1 < a.N ? a.c1 : a.N;
+  const int row0 = ce + 64 * r, rows = a.N - row0 < 64 ? a.N - row0 : 64;
+  const int q0 = a.k0 + 64 * q, qrows = panel_bsz(a, q);
+  const int tid = launder((int)threadIdx.x);
+  const TMap<4> m(tid);
+  Acc<T> upd[4], tile[4];
+  zero_acc<T, 4>(upd);
+  prev_update<T, 4>(tid, upd, a.Wprev + (int64_t)row0 * a.ldw, a.ldw, a.K + (int64_t)q0 * a.ld + a.kprev, a.ld, rows,
+                    qrows, a.boprev, reinterpret_cast<T*>(smem), reinterpret_cast<T*>(smem + 64 * DS));
+  T* dst = a.K + (int64_t)row0 * a.ld + q0;
+  load_acc<T, false, false, 4>(m, tile, dst, a.ld, rows, qrows);
+#pragma unroll
+  for (int n = 0; n < 4; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) tile[n][g] = tile[n][g] - upd[n][g];
+  store_acc<T, true, false, 4>(m, tile, dst, a.ld, rows, qrows);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(&a.area[OP_PREV + r], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // A chain launch started beside the previous panel's rows launch (a.parea):
-// the rows of this panel's region from that launch (RDONE of every region
-// block row) within 1 ms, else no role is drawn -- the launch may have been
+// that launch's RDONE[0] (this panel's first block row, and its block (0, 0)
+// update) within 1 ms, else no role is drawn -- the launch may have been
 // dispatched ahead of that rows launch (a serialized dispatch, rocprofv3
 // --pmc), and the rows launch of this panel, queued behind it, then takes
-// every chain role.  true: draw.
+// every chain role.  Once RDONE[0] is up that rows launch is running, and
+// the roles wait for its other rows with their own flags (RDONE[c] in the
+// tile workers), so the chain starts its first block without waiting for
+// the slowest of them.  true: draw.
 template <typename T>
 __device__ __forceinline__ bool prev_rows_ready(const PanelArgs<T>& a) {
   if (!a.parea) return true;
   __shared__ unsigned sh_rr;
   if (threadIdx.x == 0) {
-    const int nb = panel_nb(a);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     unsigned ok = 0;
-    for (int r = 0;;) {
-      if (r == nb) {
+    for (;;) {
+      if (!a.giveback && __hip_atomic_load(&a.parea[OP_RDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
         ok = 1;
         break;
-      }
-      if (!a.giveback && __hip_atomic_load(&a.parea[OP_RDONE + r], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
-        ++r;
-        continue;
       }
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull) break;  // 1 ms
       __builtin_amdgcn_s_sleep(2);
@@ -835,7 +931,7 @@ __device__ __forceinline__ unsigned draw_ticket(const PanelArgs<T>& a, bool rows
 // waves per SIMD) -- with more it waits for a CU with no GEMM at all.
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void panel_kernel(PanelArgs<T> a,
-                                                                                           int rows_launch, int rows_prev) {
+                                                                                           int rows_launch) {
   // M, X: diag64_body's images (66.5 KB: a panel workgroup fits the LDS one
   // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64];
@@ -851,8 +947,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
     // included) against the GEMM waves that share the CU
     __builtin_amdgcn_s_setprio(3);
     chain_roles<T>(a, t, smem, &sh_ok);
-  } else if (t < a.nchain + a.nrows) {
-    rows_role<T>(a, t - a.nchain, rows_prev != 0, smem, &sh_ok);
+  } else if (t < a.nchain + a.nprev + a.nrows) {
+    if (t < a.nchain + a.nprev) strip_tile<T>(a, t - a.nchain, smem);
+    else rows_role<T>(a, t - a.nchain - a.nprev, smem, &sh_ok);
+  } else if (t < a.nchain + a.nprev + a.nrows + a.pre00w) {
+    pre00_worker<T>(a, smem, &sh_ok);
   }
 }
 
@@ -921,13 +1020,17 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   // diagonal block (0, 0) when the look-ahead update is applied here)
   a.nchain = nb + (Wprev ? nb * (nb + 1) / 2 - 1 : 0);
   a.nrows = ce < N ? (N - ce + 63) / 64 : 0;
+  // rows_prev: the look-ahead update of the rows below the region with the
+  // previous panel as strip tiles of the rows launch (else the caller ran it)
+  if (rows_prev && (!Wprev || a.nrows > OP_PREVMAX)) return hipErrorInvalidValue;
+  a.nprev = rows_prev ? a.nrows * nb : 0;
+  a.pre00w = (a.nprev && pre00_out) ? 1 : 0;
   const int dbg = debug_inject_mask();
   if (!(dbg & IPMZ_DEBUG_ROWS_CHAIN)) {
     // every chain role; the padding (dynamic LDS) makes each of its
     // workgroups hold a CU with no other panel workgroup (the chain's
     // barrier-bound blocks lose a third of their speed beside a helper)
-    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N - k0, N), st_chain, a, 0,
-                       rows_prev ? 1 : 0);
+    hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain), dim3(256), chain_lds_pad<T>(N - k0, N), st_chain, a, 0);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -938,7 +1041,7 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   // this launch the last panel would then never be factored, which
   // test_gpu_panel_forms.py's give-back form found in round 6)
   if (a.nrows == 0 && !parea && !(dbg & IPMZ_DEBUG_ROWS_CHAIN)) return hipSuccess;
-  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain + a.nrows), dim3(256), 0, st_rows, a, 1, rows_prev ? 1 : 0);
+  hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain + a.nprev + a.nrows + a.pre00w), dim3(256), 0, st_rows, a, 1);
   return hipGetLastError();
 }
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,

@@ -51,6 +51,35 @@ __device__ __forceinline__ bool wait_flag(unsigned* flag, unsigned* err, unsigne
   return wait_flag_ge(flag, 1u, err, sh_ok);
 }
 
+// lanes 0 .. n-1 of wave 0 poll flags base[0 .. n-1] >= 1 together (one L2
+// round trip per try for all of them) and lane 63 samples *peek (no wait:
+// *sh_peek = whether it was up); everyone leaves together.  Gives up as
+// wait_flag_ge does.
+__device__ __forceinline__ bool wait_flags(unsigned* base, int n, const unsigned* peek, unsigned* err, unsigned* sh_ok,
+                                           unsigned* sh_peek) {
+  if (threadIdx.x < 64) {
+    const int l = threadIdx.x;
+    unsigned ok = 1, pk = 0;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const unsigned v = l < n ? __hip_atomic_load(&base[l], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 1u;
+      if (l == 63 && peek && !pk) pk = __hip_atomic_load(peek, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (__builtin_amdgcn_ballot_w64(v == 0u) == 0ull) break;
+      __builtin_amdgcn_s_sleep(2);
+      if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+          __hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+        if (l == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        ok = 0;
+        break;
+      }
+    }
+    if (l == 0) *sh_ok = ok;
+    if (l == 63) *sh_peek = pk != 0u;
+  }
+  __syncthreads();
+  return *sh_ok != 0;
+}
+
 // every storing wave drains its sc1 stores, then one lane raises the flag
 __device__ __forceinline__ void publish(unsigned* flag) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

@@ -54,6 +54,8 @@ for s in ${STEPS:-smoke tests bench prof}; do
     c2hip) step c2hip 300 rocprofv3 --hip-trace --kernel-trace -d "$OUT/c2hip" -o run --output-format csv -- python bench.py --workload c2 --steps 3 --warmup 1 --no-cpu-baseline --no-batched --no-instrumented --no-configs ;;
     counters) step counters 120 rocprofv3 -L ;;
     panel) step panel 400 python -u -m pytest tests/test_gpu_panel_forms.py tests/test_gpu_faults.py tests/test_gpu_determinism.py -v --timeout 240 --timeout-method thread -p no:cacheprovider ;;
+    diagclk) step diagclk 60 ipm-zoo_amd/build/kbench 256 diagclk ;;
+    chainclk_ab) for v in ${CHV:-w0 w1 w0 w1}; do step chainclk_${CN:-2560}_$v 120 ipm-zoo_amd/build/kbench_chain_$v ${CN:-2560} chainclk ${CNBO:-384}; mv "$OUT/chainclk_${CN:-2560}_$v.log" "$OUT/chainclk_${CN:-2560}_${v}_$(date +%s%N).log"; done ;;
     chainclk) step chainclk_${CN:-2560} 120 ipm-zoo_amd/build/kbench_chain ${CN:-2560} chainclk ${CNBO:-512} ;;
     graph) step graph_probe 240 python tools/dbg/graph_probe.py ${GRAPH_SIZES:-} ;;
     ktrace) step ktrace 300 rocprofv3 --kernel-trace -d "$OUT/ktrace" -o run --output-format csv -- ipm-zoo_amd/build/kbench 11264 factor 384 ;;

@@ -215,7 +215,7 @@ int main(int argc, char** argv) {
   }
   if (mode == "diagclk") {  // stage clocks of the 64 x 64 diagonal factor; column passes 0 (as shipped), 1 (variant)
     std::vector<double> ref;
-    for (int cpv : {0, 1, 0, 1}) {
+    for (int cpv : {9, 11, 12, 9, 11, 12, 9, 11, 12}) {  // kbench_probes.hip diag_clock_probe
       unsigned long long clk[32];
       for (int rep = 0; rep < 3; ++rep) {
         hipLaunchKernelGGL(fill_qd, dim3(2048), dim3(256), 0, st, K, ld, N, 7ull);
@@ -234,7 +234,7 @@ int main(int argc, char** argv) {
       if (ref.empty()) ref = cur;
       else
         for (size_t i = 0; i < cur.size(); ++i) dmax = std::max(dmax, std::fabs(cur[i] - ref[i]));
-      std::printf("diag64 cpv=%d stage clocks (s_memtime ticks from start):", cpv);
+      std::printf("diag64 v=%2d stage clocks (s_memtime ticks from start):", cpv);
       for (unsigned i = 1; i < clk[31] && i < 31; ++i) std::printf(" %llu", clk[i] - clk[0]);
       std::printf("  (max |d| vs the first: %.2e)\n", dmax);
     }
@@ -499,10 +499,8 @@ int main(int argc, char** argv) {
       std::printf("%3d %9.2f %9.2f %9.2f %9.2f %9.2f %9.2f | %9.2f | %9.2f %9.2f | %9.2f %9.2f | dur %6.2f", b,
                   us(cs[b][0]), us(cs[b][1]), us(cs[b][2]), us(cs[b][3]), us(cs[b][4]), us(cs[b][5]), us(hs[b][0]),
                   us(hs[b][1]), us(hs[b][2]), us(hs[b][3]), -1.0, nx > 0 ? nx - us(cs[b][0]) : 0.0);
-      if (cs[b][4] && cs[b][6]) {  // chain8: the bulk group's barrier clocks, relative to the window start
-        std::printf(" | bars");
-        for (int k = 4; k < 16; ++k) std::printf(" %.2f", cs[b][k] ? us(cs[b][k]) - us(cs[b][0]) : -1.0);
-      }
+      if (cs[b][6])  // rows role 0 at this block: DIAG seen, TRSM done, strips done
+        std::printf(" | rows0 %9.2f %9.2f %9.2f", us(cs[b][6]), us(cs[b][7]), us(cs[b][8]));
       std::printf("\n");
     }
     return 0;

@@ -108,16 +108,24 @@ hipError_t mfma_probe(double* out, int blocks, int iters, int threads, int nacc,
 
 // stage clocks (s_memtime) of one diag64_body run: entries [0, clk[31]) of out
 __device__ unsigned long long g_diag_clk[32];
-template <int CPV>
+template <int CPV, bool COH>
 __global__ __launch_bounds__(256) void diag_clock_kernel(double* K, int64_t ld, double* D, double* Linv, int* info) {
   __shared__ double M[64 * DS], X[64 * DS], dsh[64];
-  diag64_body<false, false, double, false, 4, NoHook, true, NoHook, CPV>(K, ld, 0, 64, D, Linv, info, M, X, dsh,
-                                                                        g_diag_clk);
+  diag64_body<COH, false, double, false, 4, NoHook, true, NoHook, CPV>(K, ld, 0, 64, D, Linv, info, M, X, dsh,
+                                                                      g_diag_clk);
 }
+// v: CPV (0 colpass16, 1 colpass16_spec, 3 / 4 colpass16_short with 2 / 1 Newton steps) + 8 COH (L^{-1}
+// stored write-through, as the panel chain)
 hipError_t diag_clock_probe(double* K, int64_t ld, double* D, double* Linv, int* info, unsigned long long* out,
-                            hipStream_t st, int cpv) {
-  if (cpv == 1) hipLaunchKernelGGL(diag_clock_kernel<1>, dim3(1), dim3(256), 0, st, K, ld, D, Linv, info);
-  else hipLaunchKernelGGL(diag_clock_kernel<0>, dim3(1), dim3(256), 0, st, K, ld, D, Linv, info);
+                            hipStream_t st, int v) {
+#define DCK(C, H) \
+  if (v == (C) + ((H) ? 8 : 0)) hipLaunchKernelGGL((diag_clock_kernel<C, H>), dim3(1), dim3(256), 0, st, K, ld, D, Linv, info)
+  DCK(0, false);
+  DCK(1, false);
+  DCK(1, true);
+  DCK(3, true);
+  DCK(4, true);
+#undef DCK
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return hipMemcpyFromSymbolAsync(out, HIP_SYMBOL(g_diag_clk), sizeof(unsigned long long) * 32, 0,

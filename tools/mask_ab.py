@@ -17,6 +17,8 @@ if side is not None:
     torch.cuda.set_stream(side)
 ctx = I.Context(0, stream=torch.cuda.current_stream().cuda_stream) if TS in ("1", "2") else I.Context(0)
 print("ctx stream", torch.cuda.current_stream().cuda_stream if TS != "0" else "own", flush=True)
+if os.environ.get("AB_NBO"):  # AB_NBO=384: that outer panel width (else by matrix order)
+    ctx.set_blocking(int(os.environ["AB_NBO"]), 64)
 mask = int(sys.argv[1])
 for wl in (sys.argv[2:] or ["c3", "c2", "c5"]):
     n, m, p, o = W[wl]
