@@ -42,7 +42,7 @@ enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
        IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_GIVEBACK = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
-       IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384 };
+       IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384, IPMZ_DEBUG_PAD_BIG = 32768 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -120,9 +120,11 @@ hipError_t ldlt_factor(float* K, int64_t ld, int N, float* D, float* Linv, float
                        hipStream_t st, TrailTimer* timer, hipStream_t st2, hipStream_t st3, hipEvent_t* ev, int nev,
                        unsigned* pctrl = nullptr, hipStream_t st4 = nullptr);
 // ctrl words of the panel path: a shared area (sticky error word) + one
-// area per outer panel, then two 64 x 64 (8-byte) tiles: the next panel's
-// block (0, 0) look-ahead update, pre-accumulated by the rows launch
-#define IPMZ_PANEL_PRE00_WORDS (2 * 64 * 64 * 2)
+// area per outer panel, then three 64 x 64 (8-byte) tiles: the next panel's
+// block (0, 0) look-ahead update, pre-accumulated by the rows launch (three,
+// so a rows launch never waits for the chain launch that read the slot it
+// reuses)
+#define IPMZ_PANEL_PRE00_WORDS (3 * 64 * 64 * 2)
 inline int64_t panel_ctrl_words(int N, int nbo) {
   return (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + (N + nbo - 1) / nbo) + IPMZ_PANEL_PRE00_WORDS;
 }

@@ -531,9 +531,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // a captured step computes what an eager one does.
   auto tiles_at = [&](int j) { return two && fused && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
-  // rows launch of panel k into slot (k + 1) & 1 (after the ctrl areas)
+  // rows launch of panel k into slot (k + 1) % 3 (after the ctrl areas): the
+  // rows launch of panel k + 1 reuses the slot that panel k - 1's chain roles
+  // read, before panel k's chain started (so C need not wait for A_k)
   T* pre00 = pctrl ? reinterpret_cast<T*>(pctrl + (int64_t)IPMZ_PANEL_CTRL_WORDS * (1 + npan)) : nullptr;
-  auto slot00 = [&](int k) { return pre00 + (int64_t)(k & 1) * 64 * 64; };
+  auto slot00 = [&](int k) { return pre00 + (int64_t)(k % 3) * 64 * 64; };
   auto factor = [&](int k, bool prev) -> hipError_t {  // panel k (prev: with the look-ahead update from k - 1)
     const int k0 = k * nbo;
     if (!fused) return factor_panel(K, ld, N, D, Linv, Wb(k), k0, pw(k), nbo, nbi, info, st);
@@ -617,15 +619,21 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
       if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
       if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
       // early: panel k-1's rows launch (and C's strip before it) are the last
-      // readers of W buffer (k + 1) % 3 -- the one this chain launch writes
-      if (early_at(k + 1) && (e = stream_wait(st, evC[k - 1])) != hipSuccess) return e;
+      // readers of W buffer (k + 1) % 3 -- the one this chain launch writes.
+      // Where panel k was early too, B waited for that launch before N_{k-1}
+      // (above), so the wait on N_{k-1} covers it: one cross-stream wait
+      // fewer before the chain launch (each costs the launch several us)
+      if (early_at(k + 1) && !early_at(k) && (e = stream_wait(st, evC[k - 1])) != hipSuccess) return e;
     }
     if (fused) {
       // the look-ahead update with P_k: the rows below P_{k+1}'s diagonal
       // region as a strip GEMM on C (beside the chain launch, which updates
       // the region itself); panel k's chain roles may have run in its chain
-      // launch, so C also waits for that launch
-      if ((e = stream_wait(sC, evA[k])) != hipSuccess) return e;
+      // launch, so C also waits for that launch -- except with strip tiles:
+      // then the rows launch reads nothing the chain launch of panel k writes
+      // but through flags, and the block (0, 0) slot it reuses was read
+      // before panel k's chain started (three slots)
+      if (!tiles_at(k + 1) && (e = stream_wait(sC, evA[k])) != hipSuccess) return e;
       if (p2 < N && !tiles_at(k + 1)) {
         if ((e = gemm_nt_sub_t<T>(N - p2, p2 - p1, bo, Wb(k) + (int64_t)p2 * nbo, nbo, K + (int64_t)p1 * ld + k0, ld,
                                   K + (int64_t)p2 * ld + p1, ld, p2, p1, false, sC, nullptr)) != hipSuccess)

@@ -936,6 +936,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   // trailing-GEMM workgroup leaves free, so it is never starved of a CU)
   __shared__ __attribute__((aligned(16))) double smem[2 * 64 * DS + 64 + 64];
   __shared__ unsigned sh_ok;
+  if (!rows_launch && blockIdx.x == 0) HSTAMP(a.k0 / 64 + 3, 3);  // the chain launch is dispatched
   if (!rows_launch && !prev_rows_ready(a)) return;
   const unsigned tu = draw_ticket(a, rows_launch != 0);
   if (tu == ~0u) return;
@@ -983,7 +984,7 @@ static size_t chain_lds_pad(int Nleft, int N) {
     state[dev].store(st, std::memory_order_release);
   }
   if (st != 1) return 0;
-  if (N <= IPMZ_EARLY_CHAIN_MAX_N) return whole - own;
+  if (N <= IPMZ_EARLY_CHAIN_MAX_N && !(debug_inject_mask() & IPMZ_DEBUG_PAD_BIG)) return whole - own;
   return (Nleft <= IPMZ_EARLY_CHAIN_MAX_N ? big : small) - own;
 }
 

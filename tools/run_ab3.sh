@@ -3,7 +3,7 @@
 set -u
 OUT=gpurun_out/$1; W=$2; shift 2; mkdir -p $OUT
 export TMPDIR=/tmp
-for i in 1 2; do
+for i in ${REPS:-1 2}; do
   for v in "$@"; do
     n=$(echo $v | tr '/.' '__')
     if [ "$v" = "." ]; then d=""; else d=$v/ipm-zoo_amd; fi
