@@ -139,12 +139,17 @@ hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D,
                         const double* pre00_in, double* pre00_out,
                         int* info, unsigned* area, unsigned* err, const double* Wprev, int kprev, int boprev,
                         bool rows_prev, hipStream_t st_chain, hipStream_t st_rows,
-                        const unsigned* parea = nullptr);
+                        const unsigned* parea = nullptr, bool wait_ready = false);
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                         const float* pre00_in, float* pre00_out,
                         int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
                         bool rows_prev, hipStream_t st_chain, hipStream_t st_rows,
-                        const unsigned* parea = nullptr);
+                        const unsigned* parea = nullptr, bool wait_ready = false);
+// wait_ready: every workgroup of the panel's two launches first waits for
+// the panel's READY-TO-FACTOR word, raised by panel_ready on the stream of
+// the look-ahead update the panel's columns needed last (instead of a
+// cross-stream wait before the launches), then acquires (agent scope)
+hipError_t panel_ready(unsigned* area, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,
                        double* C, int64_t ldc, int64_t row0, int64_t col0, bool square_lower, hipStream_t st,

@@ -530,6 +530,14 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // keep pace with the chain; panel.hip strip_tile).  Capture or not alike, so
   // a captured step computes what an eager one does.
   auto tiles_at = [&](int j) { return two && fused && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
+  // per panel j >= 2 whose previous panel was early too: the B stream's
+  // look-ahead update of its columns (N_{j-2}) reaches its two launches as a
+  // flag (panel_ready after that update on B; each workgroup polls it and
+  // acquires) instead of cross-stream waits on A and C -- each such wait costs
+  // a launch several us even when already satisfied.  N_{j-2} also stands
+  // for the rows launch of panel j - 2 (B waited for it) and so for the W
+  // buffer the panel reuses.
+  auto flag_at = [&](int j) { return j >= 2 && early_at(j - 1) && tiles_at(j); };
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) % 3 (after the ctrl areas): the
   // rows launch of panel k + 1 reuses the slot that panel k - 1's chain roles
@@ -542,7 +550,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     return panel_factor(K, ld, N, k0, pw(k), D, Linv + (int64_t)(k0 / 64) * 64 * 64, Wb(k), nbo,
                         (two && prev) ? slot00(k) : nullptr, two ? slot00(k + 1) : nullptr, info, area(k), err,
                         prev ? Wb(k - 1) : nullptr, k0 - nbo, nbo, prev && tiles_at(k), st, sC,
-                        (early_at(k) && prev) ? area(k - 1) : nullptr);
+                        (early_at(k) && prev) ? area(k - 1) : nullptr, prev && flag_at(k));
   };
   hipError_t e = hipSuccess;
   if (!two) {  // single stream: factor, then the whole trailing update
@@ -603,6 +611,7 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
     if (p2 < N) {
       if ((e = panel_update(K, ld, N, Wb(k), nbo, k0, bo, p2, p3, false, sN)) != hipSuccess) return e;
+      if (k + 2 < npan && flag_at(k + 2) && (e = panel_ready(area(k + 2), sN)) != hipSuccess) return e;
     }
     if ((e = stream_record(evN[k], sN)) != hipSuccess) return e;
     if (p3 < N) {
@@ -615,9 +624,11 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
     if (four && (e = stream_record(evT[k], st2)) != hipSuccess) return e;
     // ---- streams A (and C): update P_{k+1} with P_k, factor P_{k+1}
-    if (k >= 1) {
+    if (k >= 1 && !flag_at(k + 1)) {
       if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
       if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
+    }
+    if (k >= 1) {
       // early: panel k-1's rows launch (and C's strip before it) are the last
       // readers of W buffer (k + 1) % 3 -- the one this chain launch writes.
       // Where panel k was early too, B waited for that launch before N_{k-1}

@@ -91,7 +91,7 @@ hipError_t chain_stamps(unsigned long long* c, unsigned long long* h) {  // DEBU
 namespace {
 // ctrl words of a panel: OP_TICKET (chain tickets 0.., then rows tickets at
 // OP_TICKET + 1), DIAG[j], REG[j][q], READY[c], TILE[c][q], RDONE[r]
-enum { OP_TICKET = 0, OP_R0 = 3, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128, OP_RDONE = 192, OP_PREV = 256 };
+enum { OP_TICKET = 0, OP_NRDY = 2, OP_R0 = 3, OP_DIAG = 4, OP_REG = 16, OP_READY = 96, OP_TILE = 128, OP_RDONE = 192, OP_PREV = 256 };
 constexpr int OP_NBMAX = IPMZ_NBO_MAX / 64;
 constexpr int OP_PREVMAX = IPMZ_PANEL_CTRL_WORDS - OP_PREV;  // rows roles that strip tiles can serve
 static_assert(OP_DIAG + OP_NBMAX <= OP_REG && OP_REG + OP_NBMAX * OP_NBMAX <= OP_READY, "ctrl layout");
@@ -355,6 +355,7 @@ struct PanelArgs {
   int nrows;          // rows-role tickets
   int nprev;          // strip-tile tickets (nrows * nb or 0), before the rows roles
   int pre00w;         // 1: a PRE00 worker ticket after the rows roles sums pre00_out (else rows role 0)
+  int wait_ready;     // 1: wait for area[OP_NRDY] (panel_ready) and acquire before drawing a role
 };
 
 template <typename T>
@@ -941,6 +942,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   const unsigned tu = draw_ticket(a, rows_launch != 0);
   if (tu == ~0u) return;
   const int t = (int)tu;
+  // the look-ahead update of this panel's columns by the B stream, signalled
+  // by a flag instead of a cross-stream wait (cdna_hip_programming.md §6 G16
+  // consumer form: one relaxed poll, one agent acquire, then plain loads) --
+  // for the roles that read it: the chain roles and the strip tiles (the rows
+  // roles read their rows after the strip tiles, through PREV)
+  if (a.wait_ready && t < a.nchain + a.nprev) {
+    if (threadIdx.x == 0) {
+      unsigned ok = 1;
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(&a.area[OP_NRDY], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+        __builtin_amdgcn_s_sleep(2);
+        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
+            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
+          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          ok = 0;
+          break;
+        }
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      sh_ok = ok;
+    }
+    __syncthreads();
+    if (!sh_ok) return;
+  }
+
   if (t == 0) HSTAMP(a.k0 / 64 + 1, 3);         // the chain role's workgroup starts
   if (t == a.nchain) HSTAMP(a.k0 / 64 + 2, 3);  // the first rows role starts
   if (t < a.nchain) {
@@ -992,7 +1019,8 @@ template <typename T>
 static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, T* Lb0, T* Wp, int ldw,
                                  const T* pre00_in, T* pre00_out, int* info,
                                  unsigned* area, unsigned* err, const T* Wprev, int kprev, int boprev, bool rows_prev,
-                                 hipStream_t st_chain, hipStream_t st_rows, const unsigned* parea) {
+                                 hipStream_t st_chain, hipStream_t st_rows, const unsigned* parea,
+                                 bool wait_ready) {
   if (bo <= 0 || bo > IPMZ_NBO_MAX || k0 + bo > N) return hipErrorInvalidValue;
   const int ce = k0 + bo;
   const int nb = (bo + 63) / 64;
@@ -1026,6 +1054,7 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   if (rows_prev && (!Wprev || a.nrows > OP_PREVMAX)) return hipErrorInvalidValue;
   a.nprev = rows_prev ? a.nrows * nb : 0;
   a.pre00w = (a.nprev && pre00_out) ? 1 : 0;
+  a.wait_ready = wait_ready ? 1 : 0;
   const int dbg = debug_inject_mask();
   if (!(dbg & IPMZ_DEBUG_ROWS_CHAIN)) {
     // every chain role; the padding (dynamic LDS) makes each of its
@@ -1048,16 +1077,27 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
 hipError_t panel_factor(double* K, int64_t ld, int N, int k0, int bo, double* D, double* Lb0, double* Wp, int ldw,
                         const double* pre00_in, double* pre00_out, int* info, unsigned* area, unsigned* err,
                         const double* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
-                        hipStream_t st_rows, const unsigned* parea) {
+                        hipStream_t st_rows, const unsigned* parea, bool wait_ready) {
   return panel_launch_t<double>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                                boprev, rows_prev, st_chain, st_rows, parea);
+                                boprev, rows_prev, st_chain, st_rows, parea, wait_ready);
 }
 hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, float* Lb0, float* Wp, int ldw,
                         const float* pre00_in, float* pre00_out, int* info, unsigned* area, unsigned* err,
                         const float* Wprev, int kprev, int boprev, bool rows_prev, hipStream_t st_chain,
-                        hipStream_t st_rows, const unsigned* parea) {
+                        hipStream_t st_rows, const unsigned* parea, bool wait_ready) {
   return panel_launch_t<float>(K, ld, N, k0, bo, D, Lb0, Wp, ldw, pre00_in, pre00_out, info, area, err, Wprev, kprev,
-                               boprev, rows_prev, st_chain, st_rows, parea);
+                               boprev, rows_prev, st_chain, st_rows, parea, wait_ready);
+}
+
+// READY-TO-FACTOR of a panel (its area's OP_NRDY word): one relaxed
+// agent-scope store by a one-thread launch, ordered on its stream after the
+// look-ahead update it stands for -- whose stores that launch's end released
+__global__ void panel_ready_kernel(unsigned* w) {
+  __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+hipError_t panel_ready(unsigned* area, hipStream_t st) {
+  hipLaunchKernelGGL(panel_ready_kernel, dim3(1), dim3(1), 0, st, area + OP_NRDY);
+  return hipGetLastError();
 }
 
 }  // namespace ipmz

@@ -5,4 +5,4 @@ export TMPDIR=/tmp
 timeout -k 10 900 python -u -m pytest tests/test_gpu_panel_forms.py tests/test_gpu_determinism.py tests/test_gpu_graph.py tests/test_gpu_headline.py -x -v --timeout 300 --timeout-method thread -p no:cacheprovider > $OUT/tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 $OUT/tests.log
 [ $rc -ne 0 ] && exit $rc
-bash tools/run_ab3.sh $1 "$2" . _old
+REPS="${REPS:-1 2}" bash tools/run_ab3.sh $1 "$2" . _old
