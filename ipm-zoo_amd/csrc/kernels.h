@@ -42,7 +42,7 @@ enum { IPMZ_INJECT_SOLVE = 1, IPMZ_INJECT_PANEL = 2, IPMZ_INJECT_GRAPH_FORKS = 4
        IPMZ_DEBUG_ONE_STREAM = 32, IPMZ_DEBUG_TRACE = 64, IPMZ_DEBUG_F32_ENGINE = 128,
        IPMZ_DEBUG_NO_FOURTH = 256, IPMZ_DEBUG_IR_FULL = 512,
        IPMZ_DEBUG_F64_ENGINE = 1024, IPMZ_DEBUG_GIVEBACK = 2048, IPMZ_DEBUG_ROWS_CHAIN = 4096,
-       IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384, IPMZ_DEBUG_PAD_BIG = 32768 };
+       IPMZ_DEBUG_NO_K0 = 8192, IPMZ_DEBUG_NO_FUSED_SOLVES = 16384 };
 #define IPMZ_TRACE(...)                                                  \
   do {                                                                   \
     if (::ipmz::debug_inject_mask() & ::ipmz::IPMZ_DEBUG_TRACE) {        \
@@ -145,10 +145,10 @@ hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, f
                         int* info, unsigned* area, unsigned* err, const float* Wprev, int kprev, int boprev,
                         bool rows_prev, hipStream_t st_chain, hipStream_t st_rows,
                         const unsigned* parea = nullptr, bool wait_ready = false);
-// wait_ready: every workgroup of the panel's two launches first waits for
-// the panel's READY-TO-FACTOR word, raised by panel_ready on the stream of
-// the look-ahead update the panel's columns needed last (instead of a
-// cross-stream wait before the launches), then acquires (agent scope)
+// wait_ready: the chain roles of the panel's chain launch first wait for the
+// panel's READY-TO-FACTOR word, raised by panel_ready on the stream of the
+// look-ahead update the panel's columns needed last (instead of a
+// cross-stream wait before that launch), then acquire (agent scope)
 hipError_t panel_ready(unsigned* area, hipStream_t st);
 hipError_t linv_from_l(const double* L, int64_t ld, int N, int nbi, double* Linv, hipStream_t st);
 hipError_t gemm_nt_sub(int M, int N, int Kd, const double* A, int64_t lda, const double* B, int64_t ldb,

@@ -531,12 +531,14 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
   // a captured step computes what an eager one does.
   auto tiles_at = [&](int j) { return two && fused && N - j * nbo <= IPMZ_EARLY_CHAIN_MAX_N; };
   // per panel j >= 2 whose previous panel was early too: the B stream's
-  // look-ahead update of its columns (N_{j-2}) reaches its two launches as a
-  // flag (panel_ready after that update on B; each workgroup polls it and
-  // acquires) instead of cross-stream waits on A and C -- each such wait costs
-  // a launch several us even when already satisfied.  N_{j-2} also stands
-  // for the rows launch of panel j - 2 (B waited for it) and so for the W
-  // buffer the panel reuses.
+  // look-ahead update of its columns (N_{j-2}) reaches its chain launch as a
+  // flag (panel_ready after that update on B; the chain roles poll it and
+  // acquire) instead of a cross-stream wait on A -- each such wait costs a
+  // launch several us even when already satisfied.  N_{j-2} also stands for
+  // the rows launch of panel j - 2 (B waited for it) and so for the W buffer
+  // the panel reuses.  The rows launch keeps its wait on C: its hundreds of
+  // workgroups spinning on the flag could hold every CU the B stream's
+  // update needs (the chain launch's few dozen cannot).
   auto flag_at = [&](int j) { return j >= 2 && early_at(j - 1) && tiles_at(j); };
   // the next panel's block (0, 0) look-ahead update, pre-accumulated by the
   // rows launch of panel k into slot (k + 1) % 3 (after the ctrl areas): the
@@ -624,8 +626,8 @@ static hipError_t ldlt_factor_t(T* K, int64_t ld, int N, T* D, T* Linv, T* W, in
     }
     if (four && (e = stream_record(evT[k], st2)) != hipSuccess) return e;
     // ---- streams A (and C): update P_{k+1} with P_k, factor P_{k+1}
-    if (k >= 1 && !flag_at(k + 1)) {
-      if ((e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
+    if (k >= 1) {
+      if (!flag_at(k + 1) && (e = stream_wait(st, evN[k - 1])) != hipSuccess) return e;
       if (fused && (e = stream_wait(sC, evN[k - 1])) != hipSuccess) return e;
     }
     if (k >= 1) {

@@ -943,11 +943,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   if (tu == ~0u) return;
   const int t = (int)tu;
   // the look-ahead update of this panel's columns by the B stream, signalled
-  // by a flag instead of a cross-stream wait (cdna_hip_programming.md §6 G16
-  // consumer form: one relaxed poll, one agent acquire, then plain loads) --
-  // for the roles that read it: the chain roles and the strip tiles (the rows
-  // roles read their rows after the strip tiles, through PREV)
-  if (a.wait_ready && t < a.nchain + a.nprev) {
+  // to the chain launch by a flag instead of a cross-stream wait
+  // (cdna_hip_programming.md §6 G16 consumer form: one relaxed poll, one
+  // agent acquire, then plain loads)
+  if (a.wait_ready && t < a.nchain) {
     if (threadIdx.x == 0) {
       unsigned ok = 1;
       const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -1011,7 +1010,7 @@ static size_t chain_lds_pad(int Nleft, int N) {
     state[dev].store(st, std::memory_order_release);
   }
   if (st != 1) return 0;
-  if (N <= IPMZ_EARLY_CHAIN_MAX_N && !(debug_inject_mask() & IPMZ_DEBUG_PAD_BIG)) return whole - own;
+  if (N <= IPMZ_EARLY_CHAIN_MAX_N) return whole - own;
   return (Nleft <= IPMZ_EARLY_CHAIN_MAX_N ? big : small) - own;
 }
 
@@ -1071,6 +1070,10 @@ static hipError_t panel_launch_t(T* K, int64_t ld, int N, int k0, int bo, T* D, 
   // this launch the last panel would then never be factored, which
   // test_gpu_panel_forms.py's give-back form found in round 6)
   if (a.nrows == 0 && !parea && !(dbg & IPMZ_DEBUG_ROWS_CHAIN)) return hipSuccess;
+  // (the rows launch is ordered after the B stream's update by its stream:
+  // it never polls the ready flag -- spinning, its many workgroups could
+  // hold the CUs that update needs)
+  a.wait_ready = 0;
   hipLaunchKernelGGL(panel_kernel<T>, dim3(a.nchain + a.nprev + a.nrows + a.pre00w), dim3(256), 0, st_rows, a, 1);
   return hipGetLastError();
 }
