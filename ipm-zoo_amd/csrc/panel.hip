@@ -355,7 +355,7 @@ struct PanelArgs {
   int nrows;          // rows-role tickets
   int nprev;          // strip-tile tickets (nrows * nb or 0), before the rows roles
   int pre00w;         // 1: a PRE00 worker ticket after the rows roles sums pre00_out (else rows role 0)
-  int wait_ready;     // 1: wait for area[OP_NRDY] (panel_ready) and acquire before drawing a role
+  int wait_ready;     // 1 (chain launch): area[OP_NRDY] (panel_ready) within 1 ms, then acquire, before drawing a role
 };
 
 template <typename T>
@@ -880,27 +880,39 @@ __device__ __forceinline__ void strip_tile(const PanelArgs<T>& a, int u, double*
 
 // A chain launch started beside the previous panel's rows launch (a.parea):
 // that launch's RDONE[0] (this panel's first block row, and its block (0, 0)
-// update) within 1 ms, else no role is drawn -- the launch may have been
-// dispatched ahead of that rows launch (a serialized dispatch, rocprofv3
-// --pmc), and the rows launch of this panel, queued behind it, then takes
-// every chain role.  Once RDONE[0] is up that rows launch is running, and
-// the roles wait for its other rows with their own flags (RDONE[c] in the
-// tile workers), so the chain starts its first block without waiting for
-// the slowest of them.  true: draw.
+// update) -- and, with a.wait_ready, the panel's READY-TO-FACTOR word (the B
+// stream's look-ahead update of its columns, panel_ready) -- within 1 ms,
+// else no role is drawn: the launch may have been dispatched ahead of what
+// it waits for (a serialized dispatch, rocprofv3 --pmc), and the rows launch
+// of this panel, queued behind both on its stream, then takes every chain
+// role.  Once RDONE[0] is up that rows launch is running, and the roles wait
+// for its other rows with their own flags (RDONE[c] in the tile workers), so
+// the chain starts its first block without waiting for the slowest of them.
+// The ready word is followed by an agent-scope acquire (cdna_hip_programming.md
+// §6 G16 consumer form: one relaxed poll, one acquire, then plain loads of
+// the update's output).  true: draw.
 template <typename T>
 __device__ __forceinline__ bool prev_rows_ready(const PanelArgs<T>& a) {
-  if (!a.parea) return true;
+  if (!a.parea && !a.wait_ready) return true;
   __shared__ unsigned sh_rr;
   if (threadIdx.x == 0) {
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    bool rows = !a.parea, ready = !a.wait_ready;
     unsigned ok = 0;
     for (;;) {
-      if (!a.giveback && __hip_atomic_load(&a.parea[OP_RDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      if (!rows)
+        rows = !a.giveback && __hip_atomic_load(&a.parea[OP_RDONE], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      if (!ready) ready = __hip_atomic_load(&a.area[OP_NRDY], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+      if (rows && ready) {
         ok = 1;
         break;
       }
       if (__builtin_amdgcn_s_memrealtime() - t0 > 100000ull) break;  // 1 ms
       __builtin_amdgcn_s_sleep(2);
+    }
+    if (ok && a.wait_ready) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     sh_rr = ok;
   }
@@ -942,31 +954,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void p
   const unsigned tu = draw_ticket(a, rows_launch != 0);
   if (tu == ~0u) return;
   const int t = (int)tu;
-  // the look-ahead update of this panel's columns by the B stream, signalled
-  // to the chain launch by a flag instead of a cross-stream wait
-  // (cdna_hip_programming.md §6 G16 consumer form: one relaxed poll, one
-  // agent acquire, then plain loads)
-  if (a.wait_ready && t < a.nchain) {
-    if (threadIdx.x == 0) {
-      unsigned ok = 1;
-      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (__hip_atomic_load(&a.area[OP_NRDY], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
-        __builtin_amdgcn_s_sleep(2);
-        if (__builtin_amdgcn_s_memrealtime() - t0 > SPIN_TICKS ||
-            __hip_atomic_load(a.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u) {
-          __hip_atomic_store(a.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          ok = 0;
-          break;
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      sh_ok = ok;
-    }
-    __syncthreads();
-    if (!sh_ok) return;
-  }
-
   if (t == 0) HSTAMP(a.k0 / 64 + 1, 3);         // the chain role's workgroup starts
   if (t == a.nchain) HSTAMP(a.k0 / 64 + 2, 3);  // the first rows role starts
   if (t < a.nchain) {
