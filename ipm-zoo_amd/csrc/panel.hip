@@ -1082,11 +1082,17 @@ hipError_t panel_factor(float* K, int64_t ld, int N, int k0, int bo, float* D, f
 // READY-TO-FACTOR of a panel (its area's OP_NRDY word): one relaxed
 // agent-scope store by a one-thread launch, ordered on its stream after the
 // look-ahead update it stands for -- whose stores that launch's end released
-__global__ void panel_ready_kernel(unsigned* w) {
+// (debug bit IPMZ_DEBUG_READY_LATE: the word is raised 3 ms late, so every
+// chain launch that waits for it gives its roles back to its rows launch --
+// the path a serialized dispatch takes; tests/test_gpu_panel_forms.py)
+__global__ void panel_ready_kernel(unsigned* w, unsigned long long delay) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < delay) __builtin_amdgcn_s_sleep(64);
   __hip_atomic_store(w, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 hipError_t panel_ready(unsigned* area, hipStream_t st) {
-  hipLaunchKernelGGL(panel_ready_kernel, dim3(1), dim3(1), 0, st, area + OP_NRDY);
+  const unsigned long long delay = (debug_inject_mask() & IPMZ_DEBUG_READY_LATE) ? 300000ull : 0ull;
+  hipLaunchKernelGGL(panel_ready_kernel, dim3(1), dim3(1), 0, st, area + OP_NRDY, delay);
   return hipGetLastError();
 }
 

@@ -6,7 +6,10 @@ early chain launch's give-back (debug bit IPMZ_DEBUG_GIVEBACK: a chain
 launch started beside the previous panel's rows launch never sees that
 launch's RDONE flags, so prev_rows_ready times out after 1 ms, the launch
 draws no role and the rows launch queued behind it takes every chain role;
-N <= 4096 left from a panel).  A role may land in either launch, so the
+N <= 4096 left from a panel), and the same give-back on the panel's
+READY-TO-FACTOR word (debug bit IPMZ_DEBUG_READY_LATE: the B stream raises it
+3 ms late, so the chain launch sees RDONE[0] but not the word -- the branch a
+serialized dispatch took when it timed out in round 6).  A role may land in either launch, so the
 forms must agree to the bit or the factor would not be run-to-run
 deterministic, and no form may raise the sticky hand-off error.
 
@@ -20,7 +23,8 @@ I = pytest.importorskip("ipmz_amd")
 torch = pytest.importorskip("torch")
 
 GIVEBACK, ROWS_CHAIN = 2048, 4096  # kernels.h IPMZ_DEBUG_GIVEBACK / IPMZ_DEBUG_ROWS_CHAIN
-MODES = [0, GIVEBACK, ROWS_CHAIN]
+READY_LATE = 32768  # kernels.h IPMZ_DEBUG_READY_LATE
+MODES = [0, GIVEBACK, ROWS_CHAIN, READY_LATE]
 
 
 @pytest.fixture(scope="module")
